@@ -1,0 +1,1067 @@
+/* pob_oracle.c -- CPU restatement of the po-brax rollout hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see pob_oracle.h).  Written for clarity: AoS per env,
+ * plain loops, one helper per brax.math primitive.  Every floating-point expression
+ * is spelled in a fixed evaluation order and compiled with -ffp-contract=off so that
+ * the HIP kernels (written independently against the same spec) must
+ * agree with it bit for bit; transcendental functions use the fixed polynomial forms
+ * below (orc_atan2f / orc_sincosf) for the same reason.
+ *
+ * Reference anchors (file:line in /root/reference):
+ *   RNG            more_jp.py:57-77 ; ant_heavenhell.py:88-99 ; ant_gather.py:110-118 ;
+ *                  ant_tag.py:63-105,129-146  -> jax.random threefry (pre-partitionable)
+ *   walls          envs/utils.py:6-28 (add_box_wall_to_body), :60-83 (draw_arena),
+ *                  :87-119 (draw_t_maze)
+ *   HH             ant_heavenhell.py:13-39 (config), :75-103 (reset), :106-123 (step),
+ *                  :125-158 (obs)
+ *   GA             ant_gather.py:17-39, :85-91 (grid), :93-123 (reset), :125-150 (step),
+ *                  :152-181 (readings), :183-213 (obs)
+ *   TAG            ant_tag.py:13-25, :63-105 (reset), :107-127 (step), :129-146 (adversary),
+ *                  :148-181 (obs)
+ *   wrappers       envs/__init__.py:50-72 (create chain), envs/wrappers.py:16-24,
+ *                  :245-262 (gym autoreset); brax EpisodeWrapper / AutoResetWrapper [ext]
+ *   physics        brax v1 System.step / info / default_qp [ext] -- restated, DESIGN.md §3
+ */
+#include "pob_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NDYN 9
+#define NJ 8
+#define MAXB 27
+#define MAXW 8
+#define MAXOBJ 64
+
+/* Algorithmic FLOP counter (built with -DORC_COUNT_FLOPS, single-threaded): every
+ * float add/sub/mul/div/sqrt/min/max of the restated algorithm counts 1; comparisons,
+ * selects and negations count 0.  Only executed branches are counted (an inactive contact
+ * costs nothing), which is the algorithmic work, not the SIMT work the GPU issues. */
+#ifdef ORC_COUNT_FLOPS
+static long long g_flops = 0;
+#define FL(n) (g_flops += (n))
+#else
+#define FL(n) ((void)0)
+#endif
+long long orc_flops_read_and_reset(void) {
+#ifdef ORC_COUNT_FLOPS
+  long long f = g_flops; g_flops = 0; return f;
+#else
+  return -1;
+#endif
+}
+
+/* ----------------------------------------------------------------------------- math */
+typedef struct { float x, y, z; } v3;
+typedef struct { float w, x, y, z; } q4;
+
+static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vadd(v3 a, v3 b) { FL(3); return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { FL(3); return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vscl(v3 a, float s) { FL(3); return V(a.x * s, a.y * s, a.z * s); }
+static inline v3 vdivs(v3 a, float s) { FL(3); return V(a.x / s, a.y / s, a.z / s); }
+static inline float vdot(v3 a, v3 b) { FL(5); return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 vcross(v3 a, v3 b) {
+  FL(9);
+  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+/* brax.math.rotate: r = 2*(u.v)u + (s^2 - u.u) v + 2 s (u x v) */
+static inline v3 qrot(v3 v, q4 q) {
+  FL(2 + 1 + 12 + 6); /* w*w, c-sub, s2, r (12), + s2*cr (6); vdot x2 and vcross count themselves */
+  v3 u = V(q.x, q.y, q.z);
+  float t = vdot(u, v);
+  float c = q.w * q.w - vdot(u, u);
+  float s2 = 2.0f * q.w;
+  v3 cr = vcross(u, v);
+  v3 r = V(2.0f * (t * u.x) + c * v.x, 2.0f * (t * u.y) + c * v.y, 2.0f * (t * u.z) + c * v.z);
+  return V(r.x + s2 * cr.x, r.y + s2 * cr.y, r.z + s2 * cr.z);
+}
+/* brax.math.quat_mul */
+static inline q4 qmul(q4 u, q4 v) {
+  FL(28);
+  q4 r;
+  r.w = u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z;
+  r.x = u.w * v.x + u.x * v.w + u.y * v.z - u.z * v.y;
+  r.y = u.w * v.y - u.x * v.z + u.y * v.w + u.z * v.x;
+  r.z = u.w * v.z + u.x * v.y - u.y * v.x + u.z * v.w;
+  return r;
+}
+/* quat_mul([0, a], q) with the zero terms dropped */
+static inline q4 qmul_vq(v3 a, q4 q) {
+  FL(20);
+  q4 r;
+  r.w = -(a.x * q.x) - a.y * q.y - a.z * q.z;
+  r.x = a.x * q.w + a.y * q.z - a.z * q.y;
+  r.y = -(a.x * q.z) + a.y * q.w + a.z * q.x;
+  r.z = a.x * q.y - a.y * q.x + a.z * q.w;
+  return r;
+}
+static inline q4 qinv(q4 q) { q4 r = {q.w, -q.x, -q.y, -q.z}; return r; }
+static inline q4 qnormalize(q4 q) {
+  FL(12);
+  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  q4 r = {q.w / n, q.x / n, q.y / n, q.z / n};
+  return r;
+}
+
+/* Cephes-form atanf/atan2f (fixed polynomial; same form in the HIP kernels). */
+static float orc_atanf(float x) {
+  FL(11);
+  float sign = 1.0f, y = 0.0f;
+  if (x < 0.0f) { sign = -1.0f; x = -x; }
+  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -(1.0f / x); }
+  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = (x - 1.0f) / (x + 1.0f); }
+  float z = x * x;
+  y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -
+            3.33329491539e-1f) * z * x + x);
+  return sign * y;
+}
+static float orc_atan2f(float y, float x) {
+  if (x == 0.0f) {
+    if (y < 0.0f) return -1.5707963267948966f;
+    if (y == 0.0f) return 0.0f;
+    return 1.5707963267948966f;
+  }
+  if (y == 0.0f) return x < 0.0f ? 3.141592653589793f : 0.0f;
+  float w = 0.0f;
+  if (x < 0.0f) w = (y < 0.0f) ? -3.141592653589793f : 3.141592653589793f;
+  FL(2);
+  return w + orc_atanf(y / x);
+}
+/* Cephes-form sinf/cosf with Cody-Waite reduction by pi/4. */
+static void orc_sincosf(float x, float *s, float *c) {
+  FL(26);
+  float sgn_s = 1.0f, sgn_c = 1.0f;
+  if (x < 0.0f) { x = -x; sgn_s = -1.0f; }
+  int j = (int)(1.27323954473516f * x);
+  float y = (float)j;
+  if (j & 1) { j += 1; y += 1.0f; }
+  j &= 7;
+  if (j > 3) { sgn_s = -sgn_s; sgn_c = -sgn_c; j -= 4; }
+  if (j > 1) sgn_c = -sgn_c;
+  float xr = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+  float z = xr * xr;
+  float ps = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * xr + xr;
+  float pc = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) *
+                 z * z - 0.5f * z + 1.0f;
+  if (j == 1 || j == 2) { *s = sgn_s * pc; *c = sgn_c * ps; }
+  else { *s = sgn_s * ps; *c = sgn_c * pc; }
+}
+
+/* ------------------------------------------------------------------------ threefry */
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+void orc_threefry2x32(const uint32_t key[2], uint32_t x0, uint32_t x1, uint32_t out[2]) {
+  static const int R[2][4] = {{13, 15, 26, 6}, {17, 29, 16, 24}};
+  uint32_t ks[3] = {key[0], key[1], key[0] ^ key[1] ^ 0x1BD11BDAu};
+  uint32_t a = x0 + ks[0], b = x1 + ks[1];
+  for (int i = 0; i < 5; ++i) {
+    for (int k = 0; k < 4; ++k) {
+      a += b;
+      b = rotl32(b, R[i & 1][k]);
+      b ^= a;
+    }
+    a += ks[(i + 1) % 3];
+    b += ks[(i + 2) % 3] + (uint32_t)(i + 1);
+  }
+  out[0] = a; out[1] = b;
+}
+
+/* element j of threefry_2x32(key, iota(n)) */
+static uint32_t tf_elem(const uint32_t key[2], uint32_t n, uint32_t j) {
+  uint32_t h = (n + 1) / 2, o[2];
+  if (j < h) {
+    uint32_t x1 = j + h; if (x1 >= n) x1 = 0; /* odd-size zero pad */
+    orc_threefry2x32(key, j, x1, o); return o[0];
+  }
+  orc_threefry2x32(key, j - h, j, o); return o[1];
+}
+
+void orc_split(const uint32_t key[2], int n, uint32_t *out) {
+  for (int i = 0; i < 2 * n; ++i) out[i] = tf_elem(key, 2u * (uint32_t)n, (uint32_t)i);
+}
+static void split_k(const uint32_t key[2], int n, int i, uint32_t out[2]) {
+  out[0] = tf_elem(key, 2u * (uint32_t)n, 2u * (uint32_t)i);
+  out[1] = tf_elem(key, 2u * (uint32_t)n, 2u * (uint32_t)i + 1u);
+}
+static inline float bits_to_unit(uint32_t b) {
+  union { uint32_t u; float f; } c; c.u = (b >> 9) | 0x3F800000u; return c.f - 1.0f;
+}
+void orc_uniform(const uint32_t key[2], int n, const float *lo, const float *hi, int lohi_n,
+                 float *out) {
+  for (int i = 0; i < n; ++i) {
+    float l = lo[lohi_n > 1 ? i : 0], h = hi[lohi_n > 1 ? i : 0];
+    float f = bits_to_unit(tf_elem(key, (uint32_t)n, (uint32_t)i));
+    float v = f * (h - l) + l;
+    out[i] = v > l ? v : l;
+  }
+}
+int orc_randint(const uint32_t key[2], int lo, int hi) {
+  uint32_t k[4]; orc_split(key, 2, k);
+  uint32_t span = (uint32_t)(hi - lo);
+  uint32_t hb = tf_elem(k, 1, 0), lb = tf_elem(k + 2, 1, 0);
+  uint32_t m = (65536u % span); m = (m * m) % span;
+  uint32_t off = ((hb % span) * m + (lb % span)) % span;
+  return lo + (int)off;
+}
+/* first k of jax _shuffle(key, arange(n)) (rounds = ceil(3 ln n / ln(2^32-1))). */
+void orc_choice_idx(const uint32_t key[2], int n, int k, int *out) {
+  int rounds = (int)ceil(3.0 * log(n > 1 ? (double)n : 1.0) / log(4294967295.0));
+  int *x = (int *)malloc(sizeof(int) * n), *t = (int *)malloc(sizeof(int) * n);
+  uint32_t *sk = (uint32_t *)malloc(sizeof(uint32_t) * n);
+  uint32_t kk[2] = {key[0], key[1]};
+  for (int i = 0; i < n; ++i) x[i] = i;
+  for (int r = 0; r < rounds; ++r) {
+    uint32_t s[4]; orc_split(kk, 2, s);
+    kk[0] = s[0]; kk[1] = s[1];
+    for (int i = 0; i < n; ++i) sk[i] = tf_elem(s + 2, (uint32_t)n, (uint32_t)i);
+    /* stable sort of x by sk (insertion sort keeps stability) */
+    for (int i = 0; i < n; ++i) t[i] = i;
+    for (int i = 1; i < n; ++i) {
+      int v = t[i], j = i - 1;
+      while (j >= 0 && sk[t[j]] > sk[v]) { t[j + 1] = t[j]; --j; }
+      t[j + 1] = v;
+    }
+    int *nx = (int *)malloc(sizeof(int) * n);
+    for (int i = 0; i < n; ++i) nx[i] = x[t[i]];
+    memcpy(x, nx, sizeof(int) * n); free(nx);
+  }
+  for (int i = 0; i < k; ++i) out[i] = x[i];
+  free(x); free(t); free(sk);
+}
+
+/* ------------------------------------------------------------------ system tables */
+struct orc_env {
+  int kind, N, D, n_obj;
+  /* integrator */
+  float h, half_h, lin_damp, ang_damp, g[3];
+  int substeps;
+  float mass[NDYN], inv_mass[NDYN];
+  /* joints (ant tree; parent(j) = j odd ? j : 0, child(j) = j+1) */
+  v3 off_p[NJ], off_c[NJ], axis[NJ], ref[NJ];
+  float lim_lo[NJ], lim_hi[NJ], jdamp[NJ], strength[NJ];
+  float default_angle[NJ];
+  /* colliders: one capsule per ant body */
+  v3 cap_end[NDYN][2]; int cap_nend[NDYN]; float cap_r[NDYN];
+  int n_ground; int ground_body[NDYN]; v3 ground_end[NDYN]; float ground_r[NDYN];
+  int n_walls; v3 wall_c[MAXW], wall_h[MAXW]; float wall_cos[MAXW], wall_sin[MAXW];
+  float friction, s_pos, half_s_ang;
+  /* frozen/default bodies (default_qp rows for bodies >= 9) */
+  float frozen_pos[MAXB][3];
+  /* env params */
+  orc_params p;
+  /* GA */
+  int n_grid; float grid[400][3]; float waiting[3];
+};
+
+void orc_default_params(orc_params *p) {
+  memset(p, 0, sizeof(*p));
+  p->hh_heaven_hell[0][0] = -5.25f; p->hh_heaven_hell[0][1] = 7.0f;
+  p->hh_heaven_hell[1][0] = 5.25f; p->hh_heaven_hell[1][1] = 7.0f;
+  p->hh_priest[0] = 0.0f; p->hh_priest[1] = 7.0f;
+  p->hh_visible_radius = 2.0f; p->hh_dying_cost = -2.0f;
+  p->ga_n_apples = 8; p->ga_n_bombs = 8;
+  p->ga_cage_xy[0] = 6.0f; p->ga_cage_xy[1] = 6.0f;
+  p->ga_robot_object_spacing = 2.0f; p->ga_catch_range = 1.0f; p->ga_n_bins = 10;
+  p->ga_sensor_range = 6.0f; p->ga_sensor_span = 3.14159265358979323846f; p->ga_dying_cost = -10.0f;
+  p->tag_tag_radius = 1.5f; p->tag_visible_radius = 3.0f; p->tag_target_step = 0.5f;
+  p->tag_min_spawn_distance = 5.0f; p->tag_cage_xy[0] = 4.5f; p->tag_cage_xy[1] = 4.5f;
+  p->tag_dying_cost = -1.0f;
+  p->action_repeat = 1;
+  p->solver_scale_pos = 0.6f; p->solver_scale_ang = 0.2f;
+}
+
+/* double-precision config maths (System construction time) */
+static void d_euler_to_quat(const double e[3], double q[4]) {
+  double c1 = cos(e[0] * M_PI / 360), c2 = cos(e[1] * M_PI / 360), c3 = cos(e[2] * M_PI / 360);
+  double s1 = sin(e[0] * M_PI / 360), s2 = sin(e[1] * M_PI / 360), s3 = sin(e[2] * M_PI / 360);
+  q[0] = c1 * c2 * c3 - s1 * s2 * s3;
+  q[1] = s1 * c2 * c3 + c1 * s2 * s3;
+  q[2] = c1 * s2 * c3 - s1 * c2 * s3;
+  q[3] = c1 * c2 * s3 + s1 * s2 * c3;
+}
+static void d_rotate(const double v[3], const double q[4], double r[3]) {
+  double s = q[0], u[3] = {q[1], q[2], q[3]};
+  double t = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+  double c = s * s - (u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  double cr[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+  for (int i = 0; i < 3; ++i) r[i] = 2 * (t * u[i]) + c * v[i] + 2 * s * cr[i];
+}
+
+/* brax ant (bodies, joints) as carried by notebooks/ant_tag.ipynb:449 */
+static const double ANT_MASS[NDYN] = {10, 1, 1, 1, 1, 1, 1, 1, 1};
+static const double ANT_CAP[NDYN][3] = { /* radius, length, end */
+    {0.25, 0.5, 1}, {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1}, {0.08, 0.44284272, 0},
+    {0.08, 0.7256854, -1}, {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1},
+    {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1}};
+static const double ANT_CAPROT[NDYN][3] = {{0, 0, 0},   {90, -45, 0}, {90, -45, 0},
+                                           {90, 45, 0}, {90, 45, 0},  {-90, 45, 0},
+                                           {-90, 45, 0}, {-90, -45, 0}, {-90, -45, 0}};
+static const double ANT_JOINT[NJ][11] = { /* off_p(3) off_c(3) rot(3) lo hi */
+    {0.2, 0.2, 0, -0.1, -0.1, 0, 0, -90, 0, -30, 30},
+    {0.1, 0.1, 0, -0.2, -0.2, 0, 0, 0, 135, 30, 70},
+    {-0.2, 0.2, 0, 0.1, -0.1, 0, 0, -90, 0, -30, 30},
+    {-0.1, 0.1, 0, 0.2, -0.2, 0, 0, 0, 45, -70, -30},
+    {-0.2, -0.2, 0, 0.1, 0.1, 0, 0, -90, 0, -30, 30},
+    {-0.1, -0.1, 0, 0.2, 0.2, 0, 0, 0, 135, -70, -30},
+    {0.2, -0.2, 0, -0.1, 0.1, 0, 0, -90, 0, -30, 30},
+    {0.1, -0.1, 0, -0.2, 0.2, 0, 0, 0, 45, 30, 70}};
+
+static double f32d(double x) { return (double)(float)x; }
+
+/* utils.py:6-28 add_box_wall_to_body: from->to in xy, z rotation = arccos(x.v/|v|) */
+static void add_box_wall(orc_env *e, double fx, double fy, double tx, double ty, double half_h,
+                         double width) {
+  int w = e->n_walls++;
+  double vx = tx - fx, vy = ty - fy;
+  double len = sqrt(vx * vx + vy * vy);
+  double zr = acos((1.0 * vx + 0.0 * vy) / len) * 180.0 / M_PI;
+  /* proto floats: position/rotation/halfsize stored as float32 */
+  double mx = f32d((fx + tx) / 2), my = f32d((fy + ty) / 2);
+  double rz = f32d(zr);
+  double ang = rz * M_PI / 180.0;
+  e->wall_c[w] = V((float)mx, (float)my, 0.5f); /* Arena body at z = 0.5 */
+  e->wall_h[w] = V((float)f32d(len / 2), (float)f32d(width), (float)f32d(half_h));
+  e->wall_cos[w] = (float)cos(ang);
+  e->wall_sin[w] = (float)sin(ang);
+}
+
+orc_env *orc_env_create(int kind, const orc_params *pin) {
+  orc_env *e = (orc_env *)calloc(1, sizeof(orc_env));
+  orc_params p; if (pin) p = *pin; else orc_default_params(&p);
+  e->kind = kind; e->p = p;
+  int ar = p.action_repeat > 0 ? p.action_repeat : 1;
+  double dt = f32d(0.05) * ar; int sub = 10 * ar; /* wrappers.py:21-23 */
+  double hd = dt / sub;
+  e->substeps = sub;
+  e->h = (float)hd; e->half_h = 0.5f * e->h;
+  e->lin_damp = (float)exp(0.0 * hd);
+  e->ang_damp = (float)exp(f32d(-0.05) * hd);
+  e->g[0] = 0.0f; e->g[1] = 0.0f; e->g[2] = (float)f32d(-9.8);
+  e->friction = 1.0f;
+  e->s_pos = p.solver_scale_pos;
+  e->half_s_ang = 0.5f * p.solver_scale_ang;
+  for (int i = 0; i < NDYN; ++i) { e->mass[i] = (float)ANT_MASS[i]; e->inv_mass[i] = 1.0f / e->mass[i]; }
+  for (int j = 0; j < NJ; ++j) {
+    const double *J = ANT_JOINT[j];
+    e->off_p[j] = V((float)J[0], (float)J[1], (float)J[2]);
+    e->off_c[j] = V((float)J[3], (float)J[4], (float)J[5]);
+    double q[4], ex[3] = {1, 0, 0}, ez[3] = {0, 0, 1}, a[3], r[3];
+    d_euler_to_quat(J + 6, q);
+    d_rotate(ex, q, a); d_rotate(ez, q, r);
+    e->axis[j] = V((float)a[0], (float)a[1], (float)a[2]);
+    e->ref[j] = V((float)r[0], (float)r[1], (float)r[2]);
+    e->lim_lo[j] = (float)(J[9] * M_PI / 180.0);
+    e->lim_hi[j] = (float)(J[10] * M_PI / 180.0);
+    e->default_angle[j] = (float)((J[9] + J[10]) * M_PI / 360.0);
+    e->jdamp[j] = 20.0f; e->strength[j] = 350.0f;
+  }
+  for (int i = 0; i < NDYN; ++i) {
+    double q[4], ez[3] = {0, 0, 1}, a[3];
+    d_euler_to_quat(ANT_CAPROT[i], q);
+    d_rotate(ez, q, a);
+    double r = f32d(ANT_CAP[i][0]), len = f32d(ANT_CAP[i][1]);
+    double seg = len / 2 - r;
+    e->cap_r[i] = (float)r;
+    int end = (int)ANT_CAP[i][2];
+    if (seg == 0.0) { e->cap_nend[i] = 1; e->cap_end[i][0] = V(0, 0, 0); }
+    else {
+      e->cap_nend[i] = 2;
+      e->cap_end[i][0] = V((float)(a[0] * seg), (float)(a[1] * seg), (float)(a[2] * seg));
+      e->cap_end[i][1] = V((float)(-a[0] * seg), (float)(-a[1] * seg), (float)(-a[2] * seg));
+    }
+    /* collide_include Ant x Ground: Torso + 4 lower legs; CapsulePlane uses `end` */
+    if (i == 0 || i == 2 || i == 4 || i == 6 || i == 8) {
+      int k = e->n_ground++;
+      e->ground_body[k] = i; e->ground_r[k] = (float)r;
+      double s = (end == 0) ? 1.0 : (double)end;
+      e->ground_end[k] = V((float)(a[0] * seg * s), (float)(a[1] * seg * s), (float)(a[2] * seg * s));
+    }
+  }
+  memset(e->frozen_pos, 0, sizeof(e->frozen_pos));
+  if (kind == ORC_HH) {
+    e->N = 14; e->D = 29 + 2 * 3 * 14 + 1;
+    double tx = fmax(p.hh_heaven_hell[0][0], fmax(p.hh_heaven_hell[1][0], p.hh_priest[0])) + 1.0;
+    double ty = fmax(p.hh_heaven_hell[0][1], fmax(p.hh_heaven_hell[1][1], p.hh_priest[1])) + 1.0;
+    double hw = 2.0, r = 0.5;
+    double P[8][2] = {{-tx - r, ty + r}, {tx + r, ty + r}, {tx + r, ty - hw - r},
+                      {hw + r, ty - hw - r}, {hw + r, -r}, {-hw - r, -r},
+                      {-hw - r, ty - hw - r}, {-tx - r, ty - hw - r}};
+    for (int i = 0; i < 8; ++i) add_box_wall(e, P[i][0], P[i][1], P[(i + 1) % 8][0], P[(i + 1) % 8][1], 0.5, r);
+    e->frozen_pos[10][0] = p.hh_priest[0]; e->frozen_pos[10][1] = p.hh_priest[1]; e->frozen_pos[10][2] = 1.0f;
+    e->frozen_pos[11][2] = 0.5f; e->frozen_pos[12][2] = 0.5f; e->frozen_pos[13][2] = 0.5f;
+  } else if (kind == ORC_GA) {
+    int no = p.ga_n_apples + p.ga_n_bombs;
+    e->n_obj = no;
+    e->N = 11 + no; e->D = 29 + 2 * 3 * e->N + 2 * p.ga_n_bins;
+    double x = p.ga_cage_xy[0] + 1.0, y = p.ga_cage_xy[1] + 1.0, r = 0.5 / 2;
+    double P[4][2] = {{x + r, y + r}, {x + r, -y - r}, {-x - r, -y - r}, {-x - r, y + r}};
+    for (int i = 0; i < 4; ++i) add_box_wall(e, P[i][0], P[i][1], P[(i + 1) % 4][0], P[(i + 1) % 4][1], 0.5, r);
+    e->frozen_pos[10][2] = 0.5f;
+    for (int i = 0; i < no; ++i) e->frozen_pos[11 + i][2] = 0.25f;
+    /* ant_gather.py:88-91: meshgrid('xy') over arange(-cx, cx+1) x arange(-cy, cy+1) */
+    int n = 0;
+    float cx = p.ga_cage_xy[0], cy = p.ga_cage_xy[1];
+    for (float gy = -cy; gy < cy + 1.0f; gy += 1.0f)
+      for (float gx = -cx; gx < cx + 1.0f; gx += 1.0f) {
+        if (sqrtf(gx * gx + gy * gy) > p.ga_robot_object_spacing) {
+          e->grid[n][0] = gx; e->grid[n][1] = gy; e->grid[n][2] = 0.0f; ++n;
+        }
+      }
+    e->n_grid = n;
+    for (int c = 0; c < 3; ++c) e->waiting[c] = e->grid[n - 1][c] + p.ga_sensor_range * 2.0f;
+  } else {
+    e->N = 12; e->D = 29 + 2 * 3 * 12 + 2;
+    double x = p.tag_cage_xy[0] + 1.0, y = p.tag_cage_xy[1] + 1.0, r = 0.5 / 2;
+    double P[4][2] = {{x + r, y + r}, {x + r, -y - r}, {-x - r, -y - r}, {-x - r, y + r}};
+    for (int i = 0; i < 4; ++i) add_box_wall(e, P[i][0], P[i][1], P[(i + 1) % 4][0], P[(i + 1) % 4][1], 0.5, r);
+    e->frozen_pos[10][2] = 0.5f; e->frozen_pos[11][2] = 0.5f;
+  }
+  return e;
+}
+void orc_env_destroy(orc_env *e) { free(e); }
+void orc_env_dims(const orc_env *e, int *n, int *d, int *a) { *n = e->N; *d = e->D; *a = NJ; }
+
+/* -------------------------------------------------------------------- body state */
+typedef struct { v3 x[NDYN]; q4 q[NDYN]; v3 v[NDYN]; v3 w[NDYN]; } body_t;
+
+static inline int jparent(int j) { return (j & 1) ? j : 0; }
+static inline int jchild(int j) { return j + 1; }
+
+/* ----------------------------------------------------------------- default_qp (a4) */
+void orc_default_qp(const orc_env *e, const float *qpos, const float *qvel, float *pos, float *rot,
+                    float *vel, float *ang) {
+  body_t b;
+  b.x[0] = V(0, 0, 0); b.q[0].w = 1.0f; b.q[0].x = b.q[0].y = b.q[0].z = 0.0f;
+  b.v[0] = V(0, 0, 0); b.w[0] = V(0, 0, 0);
+  for (int j = 0; j < NJ; ++j) {
+    int p = jparent(j), c = jchild(j);
+    float s, co; orc_sincosf(qpos[j] * 0.5f, &s, &co);
+    q4 loc = {co, e->axis[j].x * s, e->axis[j].y * s, e->axis[j].z * s};
+    b.q[c] = qmul(b.q[p], loc);
+    v3 anchor = vadd(b.x[p], qrot(e->off_p[j], b.q[p]));
+    b.x[c] = vsub(anchor, qrot(e->off_c[j], b.q[c]));
+    b.w[c] = vadd(b.w[p], vscl(qrot(e->axis[j], b.q[p]), qvel[j]));
+    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
+  }
+  float zmin = 3.0e38f;
+  for (int i = 0; i < NDYN; ++i)
+    for (int k = 0; k < e->cap_nend[i]; ++k) {
+      float z = vadd(b.x[i], qrot(e->cap_end[i][k], b.q[i])).z - e->cap_r[i];
+      if (z < zmin) zmin = z;
+    }
+  for (int i = 0; i < e->N; ++i) {
+    float *P = pos + 3 * i, *R = rot + 4 * i, *Vv = vel + 3 * i, *A = ang + 3 * i;
+    if (i < NDYN) {
+      P[0] = b.x[i].x; P[1] = b.x[i].y; P[2] = b.x[i].z - zmin;
+      R[0] = b.q[i].w; R[1] = b.q[i].x; R[2] = b.q[i].y; R[3] = b.q[i].z;
+      Vv[0] = b.v[i].x; Vv[1] = b.v[i].y; Vv[2] = b.v[i].z;
+      A[0] = b.w[i].x; A[1] = b.w[i].y; A[2] = b.w[i].z;
+    } else {
+      P[0] = e->frozen_pos[i][0]; P[1] = e->frozen_pos[i][1]; P[2] = e->frozen_pos[i][2];
+      R[0] = 1.0f; R[1] = R[2] = R[3] = 0.0f;
+      Vv[0] = Vv[1] = Vv[2] = 0.0f; A[0] = A[1] = A[2] = 0.0f;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------- contacts */
+typedef struct {
+  float pen[NDYN + NDYN]; /* [0,n_ground): ground contacts; [n_ground, +9): wall per capsule */
+  v3 n[NDYN + NDYN];
+  v3 e[NDYN + NDYN];      /* end point (body frame) */
+  float r[NDYN + NDYN];
+  int body[NDYN + NDYN];
+  int count;
+} contacts_t;
+
+/* sphere (centre p, radius r) vs the z-rotated box w; returns penetration, world normal */
+static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
+  float c = e->wall_cos[w], s = e->wall_sin[w];
+  v3 h = e->wall_h[w];
+  v3 d = vsub(p, e->wall_c[w]);
+  FL(6 + 6 + 3 + 5); /* local x/y, clamp, e, d2 */
+  float lx = d.x * c + d.y * s, ly = -(d.x * s) + d.y * c, lz = d.z;
+  float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
+  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
+  float d2 = ex * ex + ey * ey + ez * ez;
+  float pen, nx, ny, nz;
+  if (d2 > 0.0f) {
+    FL(5);
+    float dist = sqrtf(d2);
+    pen = r - dist; nx = ex / dist; ny = ey / dist; nz = ez / dist;
+  } else {
+    FL(4);
+    float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
+    nx = 0.0f; ny = 0.0f; nz = 0.0f;
+    if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
+    else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
+    else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
+  }
+  FL(6);
+  *n = V(nx * c - ny * s, nx * s + ny * c, nz);
+  return pen;
+}
+
+/* contact detection for the collide substep (ground: CapsulePlane; walls: deepest
+ * sphere-box over capsule end points x walls, one contact per capsule). */
+static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
+  int k = 0;
+  for (int g = 0; g < e->n_ground; ++g, ++k) {
+    int i = e->ground_body[g];
+    v3 pe = vadd(b->x[i], qrot(e->ground_end[g], b->q[i]));
+    FL(1);
+    ct->pen[k] = e->ground_r[g] - pe.z;
+    ct->n[k] = V(0.0f, 0.0f, 1.0f);
+    ct->e[k] = e->ground_end[g]; ct->r[k] = e->ground_r[g]; ct->body[k] = i;
+  }
+  for (int i = 0; i < NDYN; ++i, ++k) {
+    float best = 0.0f; v3 bn = V(0, 0, 0), be = e->cap_end[i][0];
+    for (int w = 0; w < e->n_walls; ++w)
+      for (int q = 0; q < e->cap_nend[i]; ++q) {
+        v3 pe = vadd(b->x[i], qrot(e->cap_end[i][q], b->q[i]));
+        v3 n; float pen = sphere_box(e, w, pe, e->cap_r[i], &n);
+        if (pen > best) { best = pen; bn = n; be = e->cap_end[i][q]; }
+      }
+    ct->pen[k] = best; ct->n[k] = bn; ct->e[k] = be; ct->r[k] = e->cap_r[i]; ct->body[k] = i;
+  }
+  ct->count = k;
+}
+
+/* position-level contact projection (normal + static friction) into DX/DQ */
+static void contact_position(const orc_env *e, const body_t *b, const body_t *prev,
+                             const contacts_t *ct, v3 *DX, q4 *DQ) {
+  for (int k = 0; k < ct->count; ++k) {
+    float pen = ct->pen[k];
+    if (!(pen > 0.0f)) continue;
+    int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
+    v3 pe = vadd(b->x[i], qrot(ct->e[k], b->q[i]));
+    v3 cp = vsub(pe, vscl(n, ct->r[k]));
+    v3 rr = vsub(cp, b->x[i]);
+    v3 cn = vcross(rr, n);
+    FL(2 + 8);
+    float w = im + vdot(cn, cn);
+    float lam = pen / w;
+    v3 P = vscl(n, lam);
+    q4 dq = qmul_vq(vcross(rr, P), b->q[i]);
+    DX[i] = vadd(DX[i], vscl(P, im));
+    DQ[i].w += 0.5f * dq.w; DQ[i].x += 0.5f * dq.x; DQ[i].y += 0.5f * dq.y; DQ[i].z += 0.5f * dq.z;
+    /* static friction against the motion of the contact point over the substep */
+    v3 cprev = vadd(prev->x[i], qrot(qrot(rr, qinv(b->q[i])), prev->q[i]));
+    v3 dp = vsub(cp, cprev);
+    v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
+    float lt = sqrtf(vdot(dpt, dpt));
+    FL(1);
+    if (lt > 0.0f) {
+      v3 t = vdivs(dpt, lt);
+      v3 ctn = vcross(rr, t);
+      float wt = im + vdot(ctn, ctn);
+      float lamt = lt / wt;
+      FL(3);
+      if (lamt < e->friction * lam) {
+        FL(8);
+        v3 Pt = vscl(t, -lamt);
+        q4 dqt = qmul_vq(vcross(rr, Pt), b->q[i]);
+        DX[i] = vadd(DX[i], vscl(Pt, im));
+        DQ[i].w += 0.5f * dqt.w; DQ[i].x += 0.5f * dqt.x; DQ[i].y += 0.5f * dqt.y; DQ[i].z += 0.5f * dqt.z;
+      }
+    }
+  }
+}
+
+/* velocity-level contact solve (dynamic friction + inelastic normal), Jacobi */
+static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t *ct, v3 *dV, v3 *dW) {
+  for (int k = 0; k < ct->count; ++k) {
+    float pen = ct->pen[k];
+    if (!(pen > 0.0f)) continue;
+    int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
+    v3 pe = vadd(b->x[i], qrot(ct->e[k], b->q[i]));
+    v3 cp = vsub(pe, vscl(n, ct->r[k]));
+    v3 rr = vsub(cp, b->x[i]);
+    v3 vr = vadd(b->v[i], vcross(b->w[i], rr));
+    float vn = vdot(vr, n);
+    v3 vt = vsub(vr, vscl(n, vn));
+    float lt = sqrtf(vdot(vt, vt));
+    FL(1);
+    v3 dv = V(0.0f, 0.0f, 0.0f);
+    if (lt > 0.0f) {
+      FL(4);
+      float fr = fminf(e->friction * pen / e->h, lt);
+      dv = vscl(vt, -(fr / lt));
+    }
+    if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+    float D = sqrtf(vdot(dv, dv));
+    FL(1);
+    if (D > 0.0f) {
+      FL(1);
+      v3 dh = vdivs(dv, D);
+      v3 cd = vcross(rr, dh);
+      float w = im + vdot(cd, cd);
+      v3 P = vdivs(dv, w);
+      dV[i] = vadd(dV[i], vscl(P, im));
+      dW[i] = vadd(dW[i], vcross(rr, P));
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ the PBD step */
+static void qadd_half(q4 *acc, q4 d, float sign) {
+  FL(12);
+  acc->w += sign * (0.5f * d.w); acc->x += sign * (0.5f * d.x);
+  acc->y += sign * (0.5f * d.y); acc->z += sign * (0.5f * d.z);
+}
+
+static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
+  for (int j = 0; j < NJ; ++j) {
+    int p = jparent(j), c = jchild(j);
+    float imp = e->inv_mass[p], imc = e->inv_mass[c];
+    /* point-to-point */
+    v3 rp = qrot(e->off_p[j], b->q[p]), rc = qrot(e->off_c[j], b->q[c]);
+    v3 d = vsub(vadd(b->x[c], rc), vadd(b->x[p], rp));
+    float L = sqrtf(vdot(d, d));
+    FL(1);
+    if (L > 0.0f) {
+      FL(5);
+      v3 n = vdivs(d, L);
+      v3 cp = vcross(rp, n), cc = vcross(rc, n);
+      float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
+      float lam = (L / wsum) * e->s_pos;
+      v3 P = vscl(n, lam);
+      DX[p] = vadd(DX[p], vscl(P, imp));
+      qadd_half(&DQ[p], qmul_vq(vcross(rp, P), b->q[p]), 1.0f);
+      DX[c] = vsub(DX[c], vscl(P, imc));
+      qadd_half(&DQ[c], qmul_vq(vcross(rc, P), b->q[c]), -1.0f);
+    }
+    /* hinge axis alignment (unit inverse inertia: w_p = w_c = 1) */
+    v3 ap = qrot(e->axis[j], b->q[p]), ac = qrot(e->axis[j], b->q[c]);
+    v3 Pa = vscl(vcross(ap, ac), e->half_s_ang);
+    qadd_half(&DQ[p], qmul_vq(Pa, b->q[p]), 1.0f);
+    qadd_half(&DQ[c], qmul_vq(Pa, b->q[c]), -1.0f);
+    /* angle limits (brax math.signed_angle about the parent's hinge axis) */
+    v3 fp = qrot(e->ref[j], b->q[p]), fc = qrot(e->ref[j], b->q[c]);
+    float psi = orc_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    float dl = 0.0f;
+    if (psi < e->lim_lo[j]) { FL(1); dl = psi - e->lim_lo[j]; }
+    else if (psi > e->lim_hi[j]) { FL(1); dl = psi - e->lim_hi[j]; }
+    FL(1);
+    v3 Pl = vscl(ap, dl * e->half_s_ang);
+    qadd_half(&DQ[p], qmul_vq(Pl, b->q[p]), 1.0f);
+    qadd_half(&DQ[c], qmul_vq(Pl, b->q[c]), -1.0f);
+  }
+}
+
+static void pbd_substep(const orc_env *e, body_t *b, const float *act, int collide, v3 *cvel, v3 *cang) {
+  body_t prev = *b;
+  /* 1. acceleration level: torque actuators + joint angular damping, gravity */
+  v3 dw[NDYN];
+  for (int i = 0; i < NDYN; ++i) dw[i] = V(0, 0, 0);
+  for (int j = 0; j < NJ; ++j) {
+    int p = jparent(j), c = jchild(j);
+    v3 a = qrot(e->axis[j], b->q[p]);
+    FL(1);
+    v3 t = vscl(a, act[j] * e->strength[j]);
+    v3 d = vscl(vsub(b->w[p], b->w[c]), e->jdamp[j]);
+    v3 tt = vadd(t, d);
+    dw[p] = vsub(dw[p], tt);
+    dw[c] = vadd(dw[c], tt);
+  }
+  for (int i = 0; i < NDYN; ++i) {
+    FL(18);
+    v3 v = b->v[i], w = b->w[i];
+    b->v[i] = V(e->lin_damp * v.x + e->g[0] * e->h, e->lin_damp * v.y + e->g[1] * e->h,
+                e->lin_damp * v.z + e->g[2] * e->h);
+    b->w[i] = V(e->ang_damp * w.x + dw[i].x * e->h, e->ang_damp * w.y + dw[i].y * e->h,
+                e->ang_damp * w.z + dw[i].z * e->h);
+  }
+  /* 2. kinetic */
+  for (int i = 0; i < NDYN; ++i) {
+    b->x[i] = vadd(b->x[i], vscl(b->v[i], e->h));
+    q4 dq = qmul_vq(b->w[i], b->q[i]);
+    FL(8);
+    q4 q = b->q[i];
+    q.w = q.w + e->half_h * dq.w; q.x = q.x + e->half_h * dq.x;
+    q.y = q.y + e->half_h * dq.y; q.z = q.z + e->half_h * dq.z;
+    b->q[i] = qnormalize(q);
+  }
+  /* 3. position projection (Jacobi over joints + contacts) */
+  v3 DX[NDYN]; q4 DQ[NDYN];
+  for (int i = 0; i < NDYN; ++i) { DX[i] = V(0, 0, 0); DQ[i].w = DQ[i].x = DQ[i].y = DQ[i].z = 0.0f; }
+  joints_position(e, b, DX, DQ);
+  contacts_t ct; ct.count = 0;
+  if (collide) {
+    detect(e, b, &ct);
+    contact_position(e, b, &prev, &ct, DX, DQ);
+  }
+  for (int i = 0; i < NDYN; ++i) {
+    FL(4);
+    b->x[i] = vadd(b->x[i], DX[i]);
+    b->q[i].w += DQ[i].w; b->q[i].x += DQ[i].x; b->q[i].y += DQ[i].y; b->q[i].z += DQ[i].z;
+  }
+  /* 4. velocity projection */
+  for (int i = 0; i < NDYN; ++i) {
+    b->q[i] = qnormalize(b->q[i]);
+    b->v[i] = vdivs(vsub(b->x[i], prev.x[i]), e->h);
+    q4 dq = qmul(b->q[i], qinv(prev.q[i]));
+    float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
+    FL(9);
+    b->w[i] = V(sg * ((2.0f * dq.x) / e->h), sg * ((2.0f * dq.y) / e->h), sg * ((2.0f * dq.z) / e->h));
+  }
+  /* 5. velocity-level contact solve */
+  if (collide) {
+    v3 dV[NDYN], dW[NDYN];
+    for (int i = 0; i < NDYN; ++i) { dV[i] = V(0, 0, 0); dW[i] = V(0, 0, 0); }
+    contact_velocity(e, b, &ct, dV, dW);
+    for (int i = 0; i < NDYN; ++i) {
+      b->v[i] = vadd(b->v[i], dV[i]); b->w[i] = vadd(b->w[i], dW[i]);
+      cvel[i] = vadd(cvel[i], dV[i]); cang[i] = vadd(cang[i], dW[i]);
+    }
+  }
+}
+
+static void load_body(const orc_env *e, const float *pos, const float *rot, const float *vel,
+                      const float *ang, body_t *b) {
+  (void)e;
+  for (int i = 0; i < NDYN; ++i) {
+    b->x[i] = V(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
+    b->q[i].w = rot[4 * i]; b->q[i].x = rot[4 * i + 1]; b->q[i].y = rot[4 * i + 2]; b->q[i].z = rot[4 * i + 3];
+    b->v[i] = V(vel[3 * i], vel[3 * i + 1], vel[3 * i + 2]);
+    b->w[i] = V(ang[3 * i], ang[3 * i + 1], ang[3 * i + 2]);
+  }
+}
+static void store_body(const body_t *b, float *pos, float *rot, float *vel, float *ang) {
+  for (int i = 0; i < NDYN; ++i) {
+    pos[3 * i] = b->x[i].x; pos[3 * i + 1] = b->x[i].y; pos[3 * i + 2] = b->x[i].z;
+    rot[4 * i] = b->q[i].w; rot[4 * i + 1] = b->q[i].x; rot[4 * i + 2] = b->q[i].y; rot[4 * i + 3] = b->q[i].z;
+    vel[3 * i] = b->v[i].x; vel[3 * i + 1] = b->v[i].y; vel[3 * i + 2] = b->v[i].z;
+    ang[3 * i] = b->w[i].x; ang[3 * i + 1] = b->w[i].y; ang[3 * i + 2] = b->w[i].z;
+  }
+}
+
+/* brax System.step: substeps/2 iterations of (plain substep, collide substep) */
+static void physics_step(const orc_env *e, body_t *b, const float *act, v3 *cvel, v3 *cang) {
+  for (int i = 0; i < NDYN; ++i) { cvel[i] = V(0, 0, 0); cang[i] = V(0, 0, 0); }
+  for (int it = 0; it < e->substeps / 2; ++it) {
+    pbd_substep(e, b, act, 0, cvel, cang);
+    pbd_substep(e, b, act, 1, cvel, cang);
+  }
+}
+
+/* sys.info(qp).contact (a2): contact passes evaluated at a static state */
+static void info_contact(const orc_env *e, const body_t *b, v3 *cvel, v3 *cang) {
+  contacts_t ct; detect(e, b, &ct);
+  for (int i = 0; i < NDYN; ++i) { cvel[i] = V(0, 0, 0); cang[i] = V(0, 0, 0); }
+  contact_velocity(e, b, &ct, cvel, cang);
+}
+void orc_contact_info(const orc_env *e, const float *pos, const float *rot, const float *vel,
+                      const float *ang, float *cvel, float *cang) {
+  body_t b; load_body(e, pos, rot, vel, ang, &b);
+  v3 cv[NDYN], ca[NDYN];
+  info_contact(e, &b, cv, ca);
+  for (int i = 0; i < e->N; ++i) {
+    float *o = cvel + 3 * i, *a = cang + 3 * i;
+    if (i < NDYN) { o[0] = cv[i].x; o[1] = cv[i].y; o[2] = cv[i].z; a[0] = ca[i].x; a[1] = ca[i].y; a[2] = ca[i].z; }
+    else { o[0] = o[1] = o[2] = a[0] = a[1] = a[2] = 0.0f; }
+  }
+}
+
+/* ------------------------------------------------------------------ observations */
+static inline float clip1(float x) { return x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x); }
+
+/* sys.joints[0].angle_vel (a3): signed angle about the parent's hinge axis; d/dt */
+static void angle_vel(const orc_env *e, const body_t *b, float *angle, float *avel) {
+  for (int j = 0; j < NJ; ++j) {
+    int p = jparent(j), c = jchild(j);
+    v3 ap = qrot(e->axis[j], b->q[p]);
+    v3 fp = qrot(e->ref[j], b->q[p]), fc = qrot(e->ref[j], b->q[c]);
+    angle[j] = orc_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    avel[j] = vdot(vsub(b->w[c], b->w[p]), ap);
+  }
+}
+
+/* the 29 + 6N shared prefix (ant_*.py _get_obs) */
+static void obs_common(const orc_env *e, const body_t *b, const v3 *cvel, const v3 *cang, float *o) {
+  float ja[NJ], jv[NJ];
+  angle_vel(e, b, ja, jv);
+  o[0] = b->x[0].x; o[1] = b->x[0].y; o[2] = b->x[0].z;
+  o[3] = b->q[0].w; o[4] = b->q[0].x; o[5] = b->q[0].y; o[6] = b->q[0].z;
+  for (int j = 0; j < NJ; ++j) o[7 + j] = ja[j];
+  o[15] = b->v[0].x; o[16] = b->v[0].y; o[17] = b->v[0].z;
+  o[18] = b->w[0].x; o[19] = b->w[0].y; o[20] = b->w[0].z;
+  for (int j = 0; j < NJ; ++j) o[21 + j] = jv[j];
+  int N = e->N;
+  for (int i = 0; i < N; ++i) {
+    v3 c = i < NDYN ? cvel[i] : V(0, 0, 0), a = i < NDYN ? cang[i] : V(0, 0, 0);
+    o[29 + 3 * i] = clip1(c.x); o[29 + 3 * i + 1] = clip1(c.y); o[29 + 3 * i + 2] = clip1(c.z);
+    o[29 + 3 * N + 3 * i] = clip1(a.x); o[29 + 3 * N + 3 * i + 1] = clip1(a.y); o[29 + 3 * N + 3 * i + 2] = clip1(a.z);
+  }
+}
+
+static inline float dist2d(float ax, float ay, float bx, float by) {
+  float dx = ax - bx, dy = ay - by;
+  return sqrtf(dx * dx + dy * dy);
+}
+
+/* ant_gather.py:152-181 _get_readings (XLA-CPU scatter order: last writer wins,
+ * out-of-range bin -1 wraps to the last slot) */
+static void ga_readings(const orc_env *e, const float *pos, q4 rot0, const float *dists, float *rd) {
+  int nb = e->p.ga_n_bins, na = e->p.ga_n_apples, no = e->n_obj;
+  float half = e->p.ga_sensor_span * 0.5f; /* python float, f32 when used */
+  float half_span = (float)((double)e->p.ga_sensor_span / 2.0);
+  float bin_res = (float)((2.0 * ((double)e->p.ga_sensor_span / 2.0)) / nb);
+  (void)half;
+  for (int s = 0; s < 2 * nb; ++s) rd[s] = 0.0f;
+  q4 o = {0.0f, 1.0f, 0.0f, 0.0f};
+  q4 t = qmul(qmul(rot0, o), qinv(rot0));
+  float ori = orc_atan2f(t.y, t.x);
+  for (int k = 0; k < no; ++k) {
+    float ox = pos[3 * (11 + k)], oy = pos[3 * (11 + k) + 1];
+    float angle = orc_atan2f(ox, oy) - ori;
+    int in_range = dists[k] <= e->p.ga_sensor_range;
+    int bin = (fabsf(angle) <= half_span && in_range) ? (int)((angle + half_span) / bin_res) : -1;
+    if (k >= na) bin = bin >= 0 ? bin + na : -1;
+    float inten = bin >= 0 ? 1.0f - dists[k] / e->p.ga_sensor_range : 0.0f;
+    int slot = bin < 0 ? bin + 2 * nb : bin;
+    if (slot >= 0 && slot < 2 * nb) rd[slot] = inten;
+  }
+}
+
+/* per-env observation for the current env kind */
+static void env_obs(const orc_env *e, const body_t *b, const float *pos, const v3 *cvel, const v3 *cang,
+                    float flag, const float *dists, float *o) {
+  obs_common(e, b, cvel, cang, o);
+  int base = 29 + 6 * e->N;
+  if (e->kind == ORC_HH) {
+    float tx = pos[3 * 11];
+    float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
+    o[base] = flag > 0.0f ? sgn : 0.0f;
+  } else if (e->kind == ORC_GA) {
+    ga_readings(e, pos, b->q[0], dists, o + base);
+  } else {
+    float tx = pos[3 * 10], ty = pos[3 * 10 + 1];
+    int vis = dist2d(tx, ty, b->x[0].x, b->x[0].y) <= e->p.tag_visible_radius;
+    o[base] = vis ? tx : 0.0f; o[base + 1] = vis ? ty : 0.0f;
+  }
+}
+
+/* ---------------------------------------------------------------------------- reset */
+static void reset_one(const orc_env *e, const uint32_t key[2], float *pos, float *rot, float *vel,
+                      float *ang, float *obs, uint32_t *rng_out) {
+  const float lo1 = -0.1f, hi1 = 0.1f;
+  uint32_t ks[10];
+  int nsplit = e->kind == ORC_GA ? 4 : 5;
+  orc_split(key, nsplit, ks);
+  float noise[NJ], qpos[NJ], qvel[NJ];
+  orc_uniform(ks + 2, NJ, &lo1, &hi1, 1, noise);
+  for (int j = 0; j < NJ; ++j) qpos[j] = e->default_angle[j] + noise[j];
+  orc_uniform(ks + 4, NJ, &lo1, &hi1, 1, qvel);
+  orc_default_qp(e, qpos, qvel, pos, rot, vel, ang);
+  float dists[MAXOBJ];
+  if (e->kind == ORC_HH) {
+    float lo[2] = {-0.5f, 0.5f}, hi[2] = {0.5f, 1.5f}, axy[2];
+    orc_uniform(ks + 6, 2, lo, hi, 2, axy);
+    for (int i = 0; i <= 9; ++i) { pos[3 * i] += axy[0]; pos[3 * i + 1] += axy[1]; }
+    int idx[2]; orc_choice_idx(ks + 6, 2, 2, idx); /* rng3 reused (ant_heavenhell.py:99) */
+    for (int k = 0; k < 2; ++k) {
+      int src = idx[k];
+      pos[3 * (11 + k)] = e->p.hh_heaven_hell[src][0];
+      pos[3 * (11 + k) + 1] = e->p.hh_heaven_hell[src][1];
+      pos[3 * (11 + k) + 2] = 1.0f;
+    }
+    rng_out[0] = ks[0]; rng_out[1] = ks[1];
+  } else if (e->kind == ORC_GA) {
+    int no = e->n_obj, idx[MAXOBJ];
+    orc_choice_idx(ks + 6, e->n_grid, no, idx);
+    for (int k = 0; k < no; ++k) {
+      pos[3 * (11 + k)] = e->grid[idx[k]][0];
+      pos[3 * (11 + k) + 1] = e->grid[idx[k]][1];
+      pos[3 * (11 + k) + 2] = k < e->p.ga_n_apples ? 1.0f : e->grid[idx[k]][2];
+    }
+    for (int k = 0; k < no; ++k)
+      dists[k] = dist2d(pos[0], pos[1], pos[3 * (11 + k)], pos[3 * (11 + k) + 1]);
+    rng_out[0] = key[0]; rng_out[1] = key[1]; /* ant_gather.py:106 keeps the input key */
+  } else {
+    float lo[2] = {-e->p.tag_cage_xy[0], -e->p.tag_cage_xy[1]};
+    float hi[2] = {e->p.tag_cage_xy[0], e->p.tag_cage_xy[1]}, axy[2], txy[2];
+    orc_uniform(ks + 6, 2, lo, hi, 2, axy);
+    for (int i = 0; i <= 9; ++i) { pos[3 * i] += axy[0]; pos[3 * i + 1] += axy[1]; }
+    uint32_t r[2] = {ks[8], ks[9]};
+    orc_uniform(r, 2, lo, hi, 2, txy);
+    for (int it = 0; it < 100000 && dist2d(txy[0], txy[1], axy[0], axy[1]) <= e->p.tag_min_spawn_distance; ++it) {
+      uint32_t s[4]; orc_split(r, 2, s);
+      r[0] = s[2]; r[1] = s[3];
+      orc_uniform(r, 2, lo, hi, 2, txy);
+    }
+    pos[3 * 10] = txy[0]; pos[3 * 10 + 1] = txy[1]; pos[3 * 10 + 2] = 0.5f;
+    rng_out[0] = ks[0]; rng_out[1] = ks[1];
+  }
+  body_t b; load_body(e, pos, rot, vel, ang, &b);
+  v3 cv[NDYN], ca[NDYN];
+  info_contact(e, &b, cv, ca);
+  env_obs(e, &b, pos, cv, ca, 0.0f, dists, obs);
+}
+
+void orc_reset(const orc_env *e, int B, const uint32_t *keys, orc_state *s, int nthreads) {
+  int N = e->N, D = e->D;
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  for (int b = 0; b < B; ++b) {
+    reset_one(e, keys + 2 * b, s->pos + (size_t)b * N * 3, s->rot + (size_t)b * N * 4,
+              s->vel + (size_t)b * N * 3, s->ang + (size_t)b * N * 3, s->obs + (size_t)b * D,
+              s->rng + 2 * b);
+    s->reward[b] = 0.0f; s->done[b] = 0.0f;
+    if (s->steps) s->steps[b] = 0.0f;
+    if (s->truncation) s->truncation[b] = 0.0f;
+    if (s->m0) s->m0[b] = 0.0f;
+    if (s->m1) s->m1[b] = 0.0f;
+    if (s->m2) s->m2[b] = 0.0f;
+    if (s->first_pos) {
+      memcpy(s->first_pos + (size_t)b * N * 3, s->pos + (size_t)b * N * 3, sizeof(float) * N * 3);
+      memcpy(s->first_rot + (size_t)b * N * 4, s->rot + (size_t)b * N * 4, sizeof(float) * N * 4);
+      memcpy(s->first_vel + (size_t)b * N * 3, s->vel + (size_t)b * N * 3, sizeof(float) * N * 3);
+      memcpy(s->first_ang + (size_t)b * N * 3, s->ang + (size_t)b * N * 3, sizeof(float) * N * 3);
+      memcpy(s->first_obs + (size_t)b * D, s->obs + (size_t)b * D, sizeof(float) * D);
+    }
+  }
+}
+
+/* ----------------------------------------------------------------------------- step */
+static void step_one(const orc_env *e, int b, const orc_state *in, const float *act, orc_state *out,
+                     int flags, int L) {
+  int N = e->N, D = e->D;
+  const float *pin = in->pos + (size_t)b * N * 3;
+  float *pos = out->pos + (size_t)b * N * 3, *rot = out->rot + (size_t)b * N * 4;
+  float *vel = out->vel + (size_t)b * N * 3, *ang = out->ang + (size_t)b * N * 3;
+  float *obs = out->obs + (size_t)b * D;
+  if (out->pos != in->pos) {
+    memcpy(pos, pin, sizeof(float) * N * 3);
+    memcpy(rot, in->rot + (size_t)b * N * 4, sizeof(float) * N * 4);
+    memcpy(vel, in->vel + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(ang, in->ang + (size_t)b * N * 3, sizeof(float) * N * 3);
+  }
+  float prev_done = in->done[b];
+  float steps = in->steps ? in->steps[b] : 0.0f;
+  uint32_t rng[2] = {in->rng[2 * b], in->rng[2 * b + 1]};
+  float m0 = in->m0 ? in->m0[b] : 0.0f, m1 = in->m1 ? in->m1[b] : 0.0f, m2 = in->m2 ? in->m2[b] : 0.0f;
+  if (flags & ORC_F_AUTORESET) { if (prev_done != 0.0f) steps = 0.0f; }
+
+  body_t bd; load_body(e, pos, rot, vel, ang, &bd);
+  v3 cv[NDYN], ca[NDYN];
+  physics_step(e, &bd, act + (size_t)b * NJ, cv, ca);
+  store_body(&bd, pos, rot, vel, ang);
+
+  float tz = bd.x[0].z;
+  float dead = tz < 0.2f ? 1.0f : 0.0f;
+  dead = tz > 1.0f ? 1.0f : dead;
+  float reward, done;
+  if (e->kind == ORC_HH) {
+    reward = dead > 0.0f ? e->p.hh_dying_cost : 0.0f;
+    int inr[3];
+    for (int k = 0; k < 3; ++k) {
+      int idx = k == 0 ? 11 : (k == 1 ? 12 : 10);
+      inr[k] = dist2d(pos[3 * idx], pos[3 * idx + 1], bd.x[0].x, bd.x[0].y) <= e->p.hh_visible_radius;
+    }
+    if (inr[0]) reward = 1.0f;
+    if (inr[1]) reward = -1.0f;
+    done = reward != 0.0f ? 1.0f : 0.0f;
+    env_obs(e, &bd, pos, cv, ca, inr[2] ? 1.0f : 0.0f, NULL, obs);
+    m2 = done; /* metrics['hits'] */
+  } else if (e->kind == ORC_GA) {
+    int no = e->n_obj, na = e->p.ga_n_apples;
+    float d[MAXOBJ];
+    for (int k = 0; k < no; ++k) d[k] = dist2d(bd.x[0].x, bd.x[0].y, pos[3 * (11 + k)], pos[3 * (11 + k) + 1]);
+    env_obs(e, &bd, pos, cv, ca, 0.0f, d, obs);
+    reward = dead > 0.0f ? e->p.ga_dying_cost : 0.0f;
+    int any_a = 0, any_b = 0, na_hit = 0, nb_hit = 0, all_wait = 1;
+    for (int k = 0; k < no; ++k) {
+      int c = d[k] <= e->p.ga_catch_range;
+      if (c) { pos[3 * (11 + k)] = e->waiting[0]; pos[3 * (11 + k) + 1] = e->waiting[1]; pos[3 * (11 + k) + 2] = e->waiting[2]; }
+      if (k < na) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
+      all_wait &= (pos[3 * (11 + k)] == e->waiting[0]) & (pos[3 * (11 + k) + 1] == e->waiting[1]) &
+                  (pos[3 * (11 + k) + 2] == e->waiting[2]);
+    }
+    if (any_a && dead == 0.0f) reward = 1.0f;
+    if (any_b && dead == 0.0f) reward = -1.0f;
+    done = all_wait ? 1.0f : dead;
+    m0 = (float)na_hit; m1 = (float)nb_hit;
+  } else {
+    reward = dead > 0.0f ? e->p.tag_dying_cost : 0.0f;
+    /* _step_target (ant_tag.py:129-146) */
+    uint32_t s[4]; orc_split(rng, 2, s);
+    int ch = orc_randint(s + 2, 0, 4);
+    float ax = bd.x[0].x, ay = bd.x[0].y, tx = pos[3 * 10], ty = pos[3 * 10 + 1];
+    float vx = ax - tx, vy = ay - ty;
+    float nrm = sqrtf(vx * vx + vy * vy);
+    vx = vx / nrm; vy = vy / nrm;
+    float cx, cy;
+    if (ch == 0) { cx = vy * 1.0f; cy = vx * -1.0f; }
+    else if (ch == 1) { cx = vy * -1.0f; cy = vx * 1.0f; }
+    else if (ch == 2) { cx = -vx; cy = -vy; }
+    else { cx = 0.0f; cy = 0.0f; }
+    float nx = cx * e->p.tag_target_step + tx, ny = cy * e->p.tag_target_step + ty;
+    if (fabsf(nx) > e->p.tag_cage_xy[0] || fabsf(ny) > e->p.tag_cage_xy[1]) { nx = tx; ny = ty; }
+    pos[3 * 10] = nx; pos[3 * 10 + 1] = ny; pos[3 * 10 + 2] = 1.0f;
+    rng[0] = s[0]; rng[1] = s[1];
+    env_obs(e, &bd, pos, cv, ca, 0.0f, NULL, obs);
+    float tag = dist2d(bd.x[0].x, bd.x[0].y, nx, ny) <= e->p.tag_tag_radius ? 1.0f : 0.0f;
+    m0 = tag;
+    if (tag > 0.0f) reward = 1.0f;
+    done = (dead != 0.0f || tag != 0.0f) ? 1.0f : 0.0f;
+  }
+  float trunc = in->truncation ? in->truncation[b] : 0.0f;
+  if (flags & ORC_F_EPISODE) {
+    steps = steps + 1.0f;
+    trunc = steps >= (float)L ? 1.0f - done : 0.0f;
+    done = steps >= (float)L ? 1.0f : done;
+  }
+  if ((flags & ORC_F_AUTORESET) && done != 0.0f) {
+    memcpy(pos, in->first_pos + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(rot, in->first_rot + (size_t)b * N * 4, sizeof(float) * N * 4);
+    memcpy(vel, in->first_vel + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(ang, in->first_ang + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(obs, in->first_obs + (size_t)b * D, sizeof(float) * D);
+  }
+  if ((flags & ORC_F_AUTORESET) && out->first_pos != in->first_pos) {
+    memcpy(out->first_pos + (size_t)b * N * 3, in->first_pos + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(out->first_rot + (size_t)b * N * 4, in->first_rot + (size_t)b * N * 4, sizeof(float) * N * 4);
+    memcpy(out->first_vel + (size_t)b * N * 3, in->first_vel + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(out->first_ang + (size_t)b * N * 3, in->first_ang + (size_t)b * N * 3, sizeof(float) * N * 3);
+    memcpy(out->first_obs + (size_t)b * D, in->first_obs + (size_t)b * D, sizeof(float) * D);
+  }
+  out->reward[b] = reward; out->done[b] = done;
+  if (out->steps) out->steps[b] = steps;
+  if (out->truncation) out->truncation[b] = trunc;
+  if (out->m0) out->m0[b] = m0;
+  if (out->m1) out->m1[b] = m1;
+  if (out->m2) out->m2[b] = m2;
+  out->rng[2 * b] = rng[0]; out->rng[2 * b + 1] = rng[1];
+}
+
+void orc_step(const orc_env *e, int B, const orc_state *in, const float *act, orc_state *out, int flags,
+              int episode_length, int nthreads) {
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  for (int b = 0; b < B; ++b) step_one(e, b, in, act, out, flags, episode_length);
+}
+
+/* AutoresetVmapGymWrapper.step (wrappers.py:245-262): when any env is done, split the
+ * gym key into B+1, reset every env with keys[1:], take qp/obs where done, zero steps. */
+void orc_gym_autoreset(const orc_env *e, int B, uint32_t gym_key[2], orc_state *s, int nthreads) {
+  int any = 0;
+  for (int b = 0; b < B; ++b) any |= s->done[b] != 0.0f;
+  if (!any) return;
+  int N = e->N, D = e->D;
+  uint32_t k0[2];
+  split_k(gym_key, B + 1, 0, k0);
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+  for (int b = 0; b < B; ++b) {
+    if (s->done[b] == 0.0f) continue;
+    uint32_t kb[2], rng_unused[2];
+    split_k(gym_key, B + 1, b + 1, kb);
+    reset_one(e, kb, s->pos + (size_t)b * N * 3, s->rot + (size_t)b * N * 4, s->vel + (size_t)b * N * 3,
+              s->ang + (size_t)b * N * 3, s->obs + (size_t)b * D, rng_unused);
+    if (s->steps) s->steps[b] = 0.0f;
+  }
+  gym_key[0] = k0[0]; gym_key[1] = k0[1];
+}

@@ -1,0 +1,98 @@
+/* pob_oracle.h -- CPU restatement of the po-brax rollout hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / CPU baseline.
+ * The product (po-brax_amd/, libpob.so) never links or calls it.
+ *
+ * It restates, in plain C99 with one env per loop iteration (OpenMP over envs):
+ *   - jax.random threefry2x32 split/uniform/randint/choice   (more_jp.py:57-77)
+ *   - System.default_angle/default_qp forward kinematics      (a4)
+ *   - the PBD physics step (brax v1 dynamics_mode "pbd" as restated in DESIGN.md §3;
+ *     brax is not vendored, so this part is PARITY UNPINNED against brax itself)
+ *   - AntHeavenHell / AntGather / AntTag reset, step, obs      (ant_*.py)
+ *   - EpisodeWrapper / AutoResetWrapper / gym autoreset semantics (wrappers.py)
+ * Memory layout = the reference's batch-major pytree layout (B, N, 3) etc.
+ */
+#ifndef POB_ORACLE_H
+#define POB_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_HH = 0, ORC_GA = 1, ORC_TAG = 2 };
+
+typedef struct orc_params {
+  /* AntHeavenHell (ant_heavenhell.py:51-56) */
+  float hh_heaven_hell[2][2];
+  float hh_priest[2];
+  float hh_visible_radius;
+  float hh_dying_cost;
+  /* AntGather (ant_gather.py:59-69) */
+  int ga_n_apples, ga_n_bombs;
+  float ga_cage_xy[2];
+  float ga_robot_object_spacing, ga_catch_range;
+  int ga_n_bins;
+  float ga_sensor_range, ga_sensor_span, ga_dying_cost;
+  /* AntTag (ant_tag.py:38-45) */
+  float tag_tag_radius, tag_visible_radius, tag_target_step, tag_min_spawn_distance;
+  float tag_cage_xy[2];
+  float tag_dying_cost;
+  /* physics */
+  int action_repeat;
+  float solver_scale_pos, solver_scale_ang;
+} orc_params;
+
+typedef struct orc_state {
+  float *pos, *rot, *vel, *ang; /* (B,N,3) (B,N,4) (B,N,3) (B,N,3) */
+  float *obs;                   /* (B,D) */
+  float *reward, *done;         /* (B,) */
+  float *steps, *truncation;    /* (B,) EpisodeWrapper info */
+  float *m0, *m1, *m2;          /* metrics, env-specific */
+  uint32_t *rng;                /* (B,2) info['rng'] */
+  float *first_pos, *first_rot, *first_vel, *first_ang, *first_obs; /* AutoResetWrapper */
+} orc_state;
+
+enum {
+  ORC_F_EPISODE = 1,    /* EpisodeWrapper: steps/truncation/time-limit done   */
+  ORC_F_AUTORESET = 2,  /* brax AutoResetWrapper: first_qp/first_obs on done */
+};
+
+typedef struct orc_env orc_env;
+
+orc_env *orc_env_create(int kind, const orc_params *p);
+void orc_env_destroy(orc_env *e);
+void orc_default_params(orc_params *p);
+void orc_env_dims(const orc_env *e, int *n_bodies, int *obs_dim, int *act_dim);
+
+/* algorithmic FLOP counter (only in the -DORC_COUNT_FLOPS build; else -1) */
+long long orc_flops_read_and_reset(void);
+
+/* RNG (jax threefry, pre-partitionable) */
+void orc_threefry2x32(const uint32_t key[2], uint32_t x0, uint32_t x1, uint32_t out[2]);
+void orc_split(const uint32_t key[2], int n, uint32_t *out /* (n,2) */);
+void orc_uniform(const uint32_t key[2], int n, const float *lo, const float *hi, int lohi_n,
+                 float *out);
+int orc_randint(const uint32_t key[2], int lo, int hi);
+void orc_choice_idx(const uint32_t key[2], int n, int k, int *out);
+
+/* kinematics: qpos/qvel (8,) -> pos/rot/vel/ang (N, .) of the default qp */
+void orc_default_qp(const orc_env *e, const float *qpos, const float *qvel, float *pos,
+                    float *rot, float *vel, float *ang);
+
+/* batched env API (B envs, OpenMP over envs when nthreads > 1) */
+void orc_reset(const orc_env *e, int B, const uint32_t *keys, orc_state *s, int nthreads);
+void orc_step(const orc_env *e, int B, const orc_state *in, const float *act, orc_state *out,
+              int flags, int episode_length, int nthreads);
+/* AutoresetVmapGymWrapper.step tail (wrappers.py:245-262), in place on s. */
+void orc_gym_autoreset(const orc_env *e, int B, uint32_t gym_key[2], orc_state *s,
+                       int nthreads);
+/* sys.info(qp).contact at a static state (a2) */
+void orc_contact_info(const orc_env *e, const float *pos, const float *rot, const float *vel,
+                      const float *ang, float *cvel, float *cang);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

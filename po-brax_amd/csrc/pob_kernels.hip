@@ -1,0 +1,757 @@
+// pob_kernels.hip -- fused rollout kernels + the C ABI of libpob.so (include/pob.h).
+//
+// Kernels (one lane = one environment; 64-env wavefront tiles; batch-major HBM layout):
+//   k_step<KIND>     physics (PBD) + per-env POMDP logic + obs + Episode/AutoReset wrappers
+//   k_reset<KIND>    threefry keys -> joint noise -> forward kinematics -> env placement
+//                    (HH goal swap / GA top-16-of-156 choice / TAG rejection loop) ->
+//                    sys.info contact -> obs; also the masked "reset where done" variants
+//   k_default_qp     System.default_qp(joint_angle, joint_velocity)
+//   k_split/k_uniform/k_actions/k_advance_key   jax.random on device
+//   k_obs_gather     standard_observability_masks column gather
+// Reference anchors are given per function; DESIGN.md has the data layout and roofline.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "../../include/pob.h"
+#include "pob_physics.h"
+
+namespace pob {
+void default_params(pob_params &p);
+const char *build_system(int kind, const pob_params &p, pob_sys &s);
+int gather_grid(const pob_params &p, float *xyz, int cap);
+}  // namespace pob
+
+struct pob_env {
+  pob_sys sys;         // host copy
+  pob_sys *d_sys = nullptr;  // device copy, read by the kernels through the scalar cache
+  pob_params params;
+  float *d_grid = nullptr;
+  uint32_t *d_scratch = nullptr;  // any-done word for pob_reset_where_done without a flag
+  int device = 0;
+};
+
+// ---------------------------------------------------------------------------- state
+struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
+  float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
+  uint32_t *rng;
+  float *first_pos, *first_rot, *first_vel, *first_ang, *first_obs;
+  uint32_t *any_done;
+};
+static StatePtrs to_ptrs(const pob_state &s) {
+  StatePtrs p;
+  p.pos = s.pos; p.rot = s.rot; p.vel = s.vel; p.ang = s.ang; p.obs = s.obs;
+  p.reward = s.reward; p.done = s.done; p.steps = s.steps; p.truncation = s.truncation;
+  p.m0 = s.m0; p.m1 = s.m1; p.m2 = s.m2; p.rng = s.rng;
+  p.first_pos = s.first_pos; p.first_rot = s.first_rot; p.first_vel = s.first_vel;
+  p.first_ang = s.first_ang; p.first_obs = s.first_obs; p.any_done = s.any_done;
+  return p;
+}
+
+template <int KIND>
+POB_D int n_bodies(csys_t &S) {
+  return KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : S.N);
+}
+template <int KIND>
+POB_D int obs_dim(csys_t &S) {
+  return KIND == POB_HEAVENHELL ? 114 : (KIND == POB_TAG ? 103 : S.D);
+}
+
+POB_D void load_body(const float *pos, const float *rot, const float *vel, const float *ang, Body &b) {
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) {
+    b.x[i] = V(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
+    b.q[i].w = rot[4 * i]; b.q[i].x = rot[4 * i + 1]; b.q[i].y = rot[4 * i + 2]; b.q[i].z = rot[4 * i + 3];
+    b.v[i] = V(vel[3 * i], vel[3 * i + 1], vel[3 * i + 2]);
+    b.w[i] = V(ang[3 * i], ang[3 * i + 1], ang[3 * i + 2]);
+  }
+}
+POB_D void store_body(const Body &b, float *pos, float *rot, float *vel, float *ang) {
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) {
+    pos[3 * i] = b.x[i].x; pos[3 * i + 1] = b.x[i].y; pos[3 * i + 2] = b.x[i].z;
+    rot[4 * i] = b.q[i].w; rot[4 * i + 1] = b.q[i].x; rot[4 * i + 2] = b.q[i].y; rot[4 * i + 3] = b.q[i].z;
+    vel[3 * i] = b.v[i].x; vel[3 * i + 1] = b.v[i].y; vel[3 * i + 2] = b.v[i].z;
+    ang[3 * i] = b.w[i].x; ang[3 * i + 1] = b.w[i].y; ang[3 * i + 2] = b.w[i].z;
+  }
+}
+
+POB_D float clip1(float x) { return x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x); }
+POB_D float dist2d(float ax, float ay, float bx, float by) {
+  float dx = ax - bx, dy = ay - by;
+  return sqrtf(dx * dx + dy * dy);
+}
+
+// _get_obs prefix shared by the three envs (ant_heavenhell.py:125-158,
+// ant_gather.py:183-213, ant_tag.py:148-181): torso pos(3) rot(4) joint angles(8)
+// torso vel(3) ang(3) joint vels(8) clip(contact.vel) (N*3) clip(contact.ang) (N*3).
+// Joint angle/vel = sys.joints[0].angle_vel (a3).
+POB_D void write_obs_common(csys_t &S, int N, const Body &b, const v3 (&cv)[POB_NDYN],
+                            const v3 (&ca)[POB_NDYN], float *o) {
+  o[0] = b.x[0].x; o[1] = b.x[0].y; o[2] = b.x[0].z;
+  o[3] = b.q[0].w; o[4] = b.q[0].x; o[5] = b.q[0].y; o[6] = b.q[0].z;
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) {
+    const int p = jparent(j), c = jchild(j);
+    v3 ap = qrot(SV(S.axis[j]), b.q[p]);
+    const v3 ref = SV(S.ref[j]);
+    v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
+    o[7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    o[21 + j] = vdot(vsub(b.w[c], b.w[p]), ap);
+  }
+  o[15] = b.v[0].x; o[16] = b.v[0].y; o[17] = b.v[0].z;
+  o[18] = b.w[0].x; o[19] = b.w[0].y; o[20] = b.w[0].z;
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) {
+    o[29 + 3 * i] = clip1(cv[i].x); o[30 + 3 * i] = clip1(cv[i].y); o[31 + 3 * i] = clip1(cv[i].z);
+    o[29 + 3 * N + 3 * i] = clip1(ca[i].x); o[30 + 3 * N + 3 * i] = clip1(ca[i].y);
+    o[31 + 3 * N + 3 * i] = clip1(ca[i].z);
+  }
+  for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { o[29 + k] = 0.0f; o[29 + 3 * N + k] = 0.0f; }
+}
+
+// ant_gather.py:152-181 sensor readings, written straight into the obs row.  Scatter
+// semantics of XLA-CPU: updates applied in object order (last writer wins) and an
+// out-of-span bin -1 wraps to the last slot.
+POB_D void ga_readings_begin(csys_t &S, float *o_rd) {
+  for (int s = 0; s < 2 * S.ga_n_bins; ++s) o_rd[s] = 0.0f;
+}
+POB_D float ga_orientation(const q4 rot0) {
+  q4 ob; ob.w = 0.0f; ob.x = 1.0f; ob.y = 0.0f; ob.z = 0.0f;
+  q4 t = qmul(qmul(rot0, ob), qinv(rot0));
+  return pob_atan2f(t.y, t.x);
+}
+POB_D void ga_reading_one(csys_t &S, int k, float ox, float oy, float dist, float ori, float *o_rd) {
+  float angle = pob_atan2f(ox, oy) - ori;
+  bool in_range = dist <= S.ga_sensor_range;
+  int bin = (fabsf(angle) <= S.ga_half_span && in_range) ? (int)((angle + S.ga_half_span) / S.ga_bin_res) : -1;
+  if (k >= S.ga_n_apples) bin = bin >= 0 ? bin + S.ga_n_apples : -1;
+  float inten = bin >= 0 ? 1.0f - dist / S.ga_sensor_range : 0.0f;
+  int slot = bin < 0 ? bin + 2 * S.ga_n_bins : bin;
+  if (slot >= 0 && slot < 2 * S.ga_n_bins) o_rd[slot] = inten;
+}
+
+// ------------------------------------------------------------------------------ step
+// Fused step: brax AutoResetWrapper(VmapWrapper(EpisodeWrapper(ActionRepeat(env)))).step
+// (envs/__init__.py:59-70) with env.step = ant_heavenhell.py:106-123 /
+// ant_gather.py:125-150 / ant_tag.py:107-127 and System.step = physics_step().
+template <int KIND>
+__global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, const StatePtrs in,
+                                              const float *__restrict__ act, const StatePtrs out,
+                                              const uint32_t flags, const int L) {
+  __shared__ float lds[POB_LDS_FLOATS * 256];
+  csys_t *Sp = (csys_t *)(size_t)sysp;
+  csys_t &S = *Sp;
+  const Lds Ls{lds, 256, (int)threadIdx.x};
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  float done = 0.0f;
+  if (b < B) {
+    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+    Body bd;
+    load_body(in.pos + r3, in.rot + r4, in.vel + r3, in.ang + r3, bd);
+    float a[POB_NJ];
+#pragma unroll
+    for (int j = 0; j < POB_NJ; ++j) a[j] = act[(size_t)b * POB_NJ + j];
+    const float prev_done = in.done[b];
+    float steps = in.steps ? in.steps[b] : 0.0f;
+    if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && prev_done != 0.0f) steps = 0.0f;
+    float m0 = in.m0 ? in.m0[b] : 0.0f, m1 = in.m1 ? in.m1[b] : 0.0f, m2 = in.m2 ? in.m2[b] : 0.0f;
+    uint32_t rng0 = in.rng[2 * b], rng1 = in.rng[2 * b + 1];
+
+    physics_step(Sp, bd, a, Ls);
+    v3 cv[POB_NDYN], ca[POB_NDYN];
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) { cv[i] = Ls.get3(POB_LDS_CV(i)); ca[i] = Ls.get3(POB_LDS_CA(i)); }
+
+    float *opos = out.pos + r3, *orot = out.rot + r4, *ovel = out.vel + r3, *oang = out.ang + r3;
+    float *o = out.obs + (size_t)b * D;
+    if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
+      for (int i = POB_NDYN; i < N; ++i) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          opos[3 * i + c] = in.pos[r3 + 3 * i + c];
+          ovel[3 * i + c] = in.vel[r3 + 3 * i + c];
+          oang[3 * i + c] = in.ang[r3 + 3 * i + c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) orot[4 * i + c] = in.rot[r4 + 4 * i + c];
+      }
+    }
+    store_body(bd, opos, orot, ovel, oang);
+
+    const float tz = bd.x[0].z;
+    float dead = tz < 0.2f ? 1.0f : 0.0f;
+    dead = tz > 1.0f ? 1.0f : dead;
+    float reward;
+    write_obs_common(S, N, bd, cv, ca, o);
+    const int base = 29 + 6 * N;
+    if (KIND == POB_HEAVENHELL) {
+      // ant_heavenhell.py:106-123
+      reward = dead > 0.0f ? S.hh_dying_cost : 0.0f;
+      const float *ip = in.pos + r3;
+      bool in0 = dist2d(ip[33], ip[34], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Target (11)
+      bool in1 = dist2d(ip[36], ip[37], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Hell (12)
+      bool in2 = dist2d(ip[30], ip[31], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Priest (10)
+      if (in0) reward = 1.0f;
+      if (in1) reward = -1.0f;
+      done = reward != 0.0f ? 1.0f : 0.0f;
+      const float tx = ip[33];
+      const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
+      o[base] = in2 ? sgn : 0.0f;
+      m2 = done;  // metrics['hits']
+    } else if (KIND == POB_GATHER) {
+      // ant_gather.py:125-150 (obs from pre-relocation positions)
+      float *rd = o + base;
+      ga_readings_begin(S, rd);
+      const float ori = ga_orientation(bd.q[0]);
+      const float *ip = in.pos + r3;
+      int na_hit = 0, nb_hit = 0;
+      bool any_a = false, any_b = false, all_wait = true;
+      for (int k = 0; k < S.n_obj; ++k) {
+        const int row = 3 * (11 + k);
+        const float ox = ip[row], oy = ip[row + 1], oz = ip[row + 2];
+        const float dk = dist2d(bd.x[0].x, bd.x[0].y, ox, oy);
+        ga_reading_one(S, k, ox, oy, dk, ori, rd);
+        const bool c = dk <= S.ga_catch_range;
+        float nx = ox, ny = oy, nz = oz;
+        if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
+        opos[row] = nx; opos[row + 1] = ny; opos[row + 2] = nz;
+        if (k < S.ga_n_apples) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
+        all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
+      }
+      reward = dead > 0.0f ? S.ga_dying_cost : 0.0f;
+      if (any_a && dead == 0.0f) reward = 1.0f;
+      if (any_b && dead == 0.0f) reward = -1.0f;
+      done = all_wait ? 1.0f : dead;
+      m0 = (float)na_hit; m1 = (float)nb_hit;
+    } else {
+      // ant_tag.py:107-127, adversary _step_target :129-146
+      reward = dead > 0.0f ? S.tag_dying_cost : 0.0f;
+      uint32_t n0, n1, c0, c1;
+      tf_split(rng0, rng1, 2u, 0u, n0, n1);
+      tf_split(rng0, rng1, 2u, 1u, c0, c1);
+      uint32_t k20, k21;  // randint(rng1, (), 0, 4) = bits(split(rng1)[1]) % 4
+      tf_split(c0, c1, 2u, 1u, k20, k21);
+      const int ch = (int)(tf_elem(k20, k21, 1u, 0u) % 4u);
+      const float *ip = in.pos + r3;
+      const float ax = bd.x[0].x, ay = bd.x[0].y, tx = ip[30], ty = ip[31];
+      float vx = ax - tx, vy = ay - ty;
+      const float nrm = sqrtf(vx * vx + vy * vy);
+      vx = vx / nrm; vy = vy / nrm;
+      float cx, cy;
+      if (ch == 0) { cx = vy * 1.0f; cy = vx * -1.0f; }
+      else if (ch == 1) { cx = vy * -1.0f; cy = vx * 1.0f; }
+      else if (ch == 2) { cx = -vx; cy = -vy; }
+      else { cx = 0.0f; cy = 0.0f; }
+      float nx = cx * S.tag_target_step + tx, ny = cy * S.tag_target_step + ty;
+      if (fabsf(nx) > S.tag_cage_xy[0] || fabsf(ny) > S.tag_cage_xy[1]) { nx = tx; ny = ty; }
+      opos[30] = nx; opos[31] = ny; opos[32] = 1.0f;
+      rng0 = n0; rng1 = n1;
+      const bool vis = dist2d(nx, ny, ax, ay) <= S.tag_visible_radius;
+      o[base] = vis ? nx : 0.0f; o[base + 1] = vis ? ny : 0.0f;
+      const float tag = dist2d(ax, ay, nx, ny) <= S.tag_tag_radius ? 1.0f : 0.0f;
+      m0 = tag;
+      if (tag > 0.0f) reward = 1.0f;
+      done = (dead != 0.0f || tag != 0.0f) ? 1.0f : 0.0f;
+    }
+    float trunc = in.truncation ? in.truncation[b] : 0.0f;
+    if (flags & POB_F_EPISODE) {  // brax EpisodeWrapper.step [ext]
+      steps = steps + 1.0f;
+      trunc = steps >= (float)L ? 1.0f - done : 0.0f;
+      done = steps >= (float)L ? 1.0f : done;
+    }
+    if ((flags & POB_F_AUTORESET) && done != 0.0f) {  // brax AutoResetWrapper.step [ext]
+      for (int k = 0; k < 3 * N; ++k) {
+        opos[k] = in.first_pos[r3 + k]; ovel[k] = in.first_vel[r3 + k]; oang[k] = in.first_ang[r3 + k];
+      }
+      for (int k = 0; k < 4 * N; ++k) orot[k] = in.first_rot[r4 + k];
+      for (int k = 0; k < D; ++k) o[k] = in.first_obs[(size_t)b * D + k];
+    }
+    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+      for (int k = 0; k < 3 * N; ++k) {
+        out.first_pos[r3 + k] = in.first_pos[r3 + k]; out.first_vel[r3 + k] = in.first_vel[r3 + k];
+        out.first_ang[r3 + k] = in.first_ang[r3 + k];
+      }
+      for (int k = 0; k < 4 * N; ++k) out.first_rot[r4 + k] = in.first_rot[r4 + k];
+      for (int k = 0; k < D; ++k) out.first_obs[(size_t)b * D + k] = in.first_obs[(size_t)b * D + k];
+    }
+    out.reward[b] = reward;
+    out.done[b] = done;
+    if (out.steps) out.steps[b] = steps;
+    if (out.truncation) out.truncation[b] = trunc;
+    if (out.m0) out.m0[b] = m0;
+    if (out.m1) out.m1[b] = m1;
+    if (out.m2) out.m2[b] = m2;
+    out.rng[2 * b] = rng0;
+    out.rng[2 * b + 1] = rng1;
+  }
+  if (out.any_done) {
+    const unsigned long long m = __ballot(done != 0.0f);
+    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
+  }
+}
+
+// ----------------------------------------------------------------------------- reset
+// System.default_qp forward kinematics (a4): child.rot = parent.rot * axis_angle(axis, q),
+// child.pos = anchor - R(child) off_c with anchor = parent.pos + R(parent) off_p; then the
+// ant tree is lifted so that its lowest collider point is at z = 0.
+POB_D void fk(csys_t &S, const float (&qpos)[POB_NJ], const float (&qvel)[POB_NJ], Body &b) {
+  b.x[0] = V(0.0f, 0.0f, 0.0f);
+  b.q[0].w = 1.0f; b.q[0].x = 0.0f; b.q[0].y = 0.0f; b.q[0].z = 0.0f;
+  b.v[0] = V(0.0f, 0.0f, 0.0f); b.w[0] = V(0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) {
+    const int p = jparent(j), c = jchild(j);
+    float s, co;
+    pob_sincosf(qpos[j] * 0.5f, &s, &co);
+    const v3 axis = SV(S.axis[j]);
+    q4 loc; loc.w = co; loc.x = axis.x * s; loc.y = axis.y * s; loc.z = axis.z * s;
+    b.q[c] = qmul(b.q[p], loc);
+    v3 anchor = vadd(b.x[p], qrot(SV(S.off_p[j]), b.q[p]));
+    b.x[c] = vsub(anchor, qrot(SV(S.off_c[j]), b.q[c]));
+    b.w[c] = vadd(b.w[p], vscl(qrot(axis, b.q[p]), qvel[j]));
+    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
+  }
+  float zmin = 3.0e38f;
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) {
+#pragma unroll
+    for (int q = 0; q < (i == 0 ? 1 : 2); ++q) {
+      float z = vadd(b.x[i], qrot(SV(S.cap_end[i][q]), b.q[i])).z - S.cap_r[i];
+      if (z < zmin) zmin = z;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) b.x[i].z = b.x[i].z - zmin;
+}
+
+enum { RESET_FULL = 0, RESET_GYM = 1, RESET_OWN = 2 };
+
+// jax.random.choice(key, grid, (K,), replace=False) = first K of a stable argsort of
+// random_bits(split(key)[1], (n,)) (one shuffle round for n <= ~1600).  Per-lane
+// insertion into a sorted list kept in LDS (lane-minor, conflict-free).
+template <int BS>
+POB_D void choice_topk(uint32_t k0, uint32_t k1, int n, int K, uint32_t *lds_key, int *lds_idx) {
+  const int t = threadIdx.x;
+  uint32_t s0, s1;
+  tf_split(k0, k1, 2u, 1u, s0, s1);
+  int cnt = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t key = tf_elem(s0, s1, (uint32_t)n, (uint32_t)i);
+    if (cnt == K && key >= lds_key[(K - 1) * BS + t]) continue;
+    int pos = cnt < K ? cnt : K - 1;
+    while (pos > 0 && lds_key[(pos - 1) * BS + t] > key) {
+      lds_key[pos * BS + t] = lds_key[(pos - 1) * BS + t];
+      lds_idx[pos * BS + t] = lds_idx[(pos - 1) * BS + t];
+      --pos;
+    }
+    lds_key[pos * BS + t] = key;
+    lds_idx[pos * BS + t] = i;
+    if (cnt < K) ++cnt;
+  }
+}
+
+// Env.reset for one lane.  Writes qp rows (all N), obs; returns the new info['rng'].
+template <int KIND, int BS>
+POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *rot, float *vel,
+                      float *ang, float *o, uint32_t &rng0, uint32_t &rng1, uint32_t *lds_key, int *lds_idx) {
+  const int N = n_bodies<KIND>(S);
+  const uint32_t ns = KIND == POB_GATHER ? 4u : 5u;  // random_split(rng, 5 | 4)
+  uint32_t r[5][2];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    if (i < (int)ns) tf_split(k0, k1, ns, (uint32_t)i, r[i][0], r[i][1]);
+    else { r[i][0] = 0u; r[i][1] = 0u; }
+  }
+  float qpos[POB_NJ], qvel[POB_NJ];
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) {
+    qpos[j] = S.default_angle[j] + tf_uniform(r[1][0], r[1][1], 8u, (uint32_t)j, -0.1f, 0.1f);
+    qvel[j] = tf_uniform(r[2][0], r[2][1], 8u, (uint32_t)j, -0.1f, 0.1f);
+  }
+  Body bd;
+  fk(S, qpos, qvel, bd);
+  // frozen rows: default_qp values
+  for (int i = POB_NDYN; i < N; ++i) {
+    pos[3 * i] = S.frozen_pos[i][0]; pos[3 * i + 1] = S.frozen_pos[i][1]; pos[3 * i + 2] = S.frozen_pos[i][2];
+    rot[4 * i] = 1.0f; rot[4 * i + 1] = 0.0f; rot[4 * i + 2] = 0.0f; rot[4 * i + 3] = 0.0f;
+    vel[3 * i] = 0.0f; vel[3 * i + 1] = 0.0f; vel[3 * i + 2] = 0.0f;
+    ang[3 * i] = 0.0f; ang[3 * i + 1] = 0.0f; ang[3 * i + 2] = 0.0f;
+  }
+  if (KIND == POB_HEAVENHELL) {
+    // ant_heavenhell.py:87-103
+    const float ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, -0.5f, 0.5f);
+    const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, 0.5f, 1.5f);
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
+    pos[27] = pos[27] + ax; pos[28] = pos[28] + ay;  // Ground is in ant_indices
+    uint32_t s0, s1, y0, y1;  // choice(rng3, hhp[:2], 2, replace=False)
+    tf_split(r[3][0], r[3][1], 2u, 1u, s0, s1);
+    threefry2x32(s0, s1, 0u, 1u, y0, y1);
+    const int first = (y1 < y0) ? 1 : 0;
+    pos[33] = S.hh_hhp[first][0]; pos[34] = S.hh_hhp[first][1]; pos[35] = 1.0f;
+    pos[36] = S.hh_hhp[1 - first][0]; pos[37] = S.hh_hhp[1 - first][1]; pos[38] = 1.0f;
+    rng0 = r[0][0]; rng1 = r[0][1];
+  } else if (KIND == POB_GATHER) {
+    // ant_gather.py:109-123
+    choice_topk<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, lds_key, lds_idx);
+    for (int k = 0; k < S.n_obj; ++k) {
+      const int g = lds_idx[k * BS + threadIdx.x];
+      pos[3 * (11 + k)] = S.grid[3 * g];
+      pos[3 * (11 + k) + 1] = S.grid[3 * g + 1];
+      pos[3 * (11 + k) + 2] = k < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
+    }
+    rng0 = k0; rng1 = k1;  // ant_gather.py:106 stores the input key
+  } else {
+    // ant_tag.py:63-105
+    const float lo0 = -S.tag_cage_xy[0], lo1 = -S.tag_cage_xy[1];
+    const float ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, lo0, S.tag_cage_xy[0]);
+    const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, lo1, S.tag_cage_xy[1]);
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
+    pos[27] = pos[27] + ax; pos[28] = pos[28] + ay;
+    uint32_t q0 = r[4][0], q1 = r[4][1];
+    float tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
+    float ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
+    for (int it = 0; it < 100000 && dist2d(tx, ty, ax, ay) <= S.tag_min_spawn_distance; ++it) {
+      uint32_t n0, n1;
+      tf_split(q0, q1, 2u, 1u, n0, n1);
+      q0 = n0; q1 = n1;
+      tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
+      ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
+    }
+    pos[30] = tx; pos[31] = ty; pos[32] = 0.5f;
+    rng0 = r[0][0]; rng1 = r[0][1];
+  }
+  store_body(bd, pos, rot, vel, ang);
+  v3 cv[POB_NDYN], ca[POB_NDYN];
+  info_contact(&S, bd, cv, ca);
+  write_obs_common(S, N, bd, cv, ca, o);
+  const int base = 29 + 6 * N;
+  if (KIND == POB_HEAVENHELL) {
+    o[base] = 0.0f;  // priest_in_range = 0 at reset
+  } else if (KIND == POB_GATHER) {
+    float *rd = o + base;
+    ga_readings_begin(S, rd);
+    const float ori = ga_orientation(bd.q[0]);
+    for (int k = 0; k < S.n_obj; ++k) {
+      const float ox = pos[3 * (11 + k)], oy = pos[3 * (11 + k) + 1];
+      ga_reading_one(S, k, ox, oy, dist2d(bd.x[0].x, bd.x[0].y, ox, oy), ori, rd);
+    }
+  } else {
+    const float tx = pos[30], ty = pos[31];
+    const bool vis = dist2d(tx, ty, bd.x[0].x, bd.x[0].y) <= S.tag_visible_radius;
+    o[base] = vis ? tx : 0.0f; o[base + 1] = vis ? ty : 0.0f;
+  }
+}
+
+template <int KIND, int BS>
+__global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, const int mode,
+                                              const uint32_t *__restrict__ keys, const uint32_t *gym_in,
+                                              uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s) {
+  __shared__ uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
+  __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
+  csys_t &S = *(csys_t *)(size_t)sysp;
+  const int b = blockIdx.x * BS + threadIdx.x;
+  if (mode == RESET_GYM) {
+    const bool any = *any_flag != 0u;
+    if (b == 0 && gym_out) {
+      uint32_t g0 = gym_in[0], g1 = gym_in[1];
+      if (any) tf_split(gym_in[0], gym_in[1], (uint32_t)B + 1u, 0u, g0, g1);
+      gym_out[0] = g0; gym_out[1] = g1;
+    }
+    if (!any) return;
+  }
+  if (b >= B) return;
+  uint32_t k0, k1;
+  if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
+  else {
+    if (s.done[b] == 0.0f) return;
+    if (mode == RESET_GYM) tf_split(gym_in[0], gym_in[1], (uint32_t)B + 1u, (uint32_t)b + 1u, k0, k1);
+    else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
+  }
+  const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  uint32_t rng0, rng1;
+  reset_lane<KIND, BS>(S, k0, k1, s.pos + r3, s.rot + r4, s.vel + r3, s.ang + r3, s.obs + (size_t)b * D,
+                       rng0, rng1, lds_key, lds_idx);
+  if (mode == RESET_FULL) {
+    s.rng[2 * b] = rng0; s.rng[2 * b + 1] = rng1;
+    s.reward[b] = 0.0f; s.done[b] = 0.0f;
+    if (s.steps) s.steps[b] = 0.0f;
+    if (s.truncation) s.truncation[b] = 0.0f;
+    if (s.m0) s.m0[b] = 0.0f;
+    if (s.m1) s.m1[b] = 0.0f;
+    if (s.m2) s.m2[b] = 0.0f;
+    if (s.first_pos) {
+      for (int k = 0; k < 3 * N; ++k) {
+        s.first_pos[r3 + k] = s.pos[r3 + k]; s.first_vel[r3 + k] = s.vel[r3 + k]; s.first_ang[r3 + k] = s.ang[r3 + k];
+      }
+      for (int k = 0; k < 4 * N; ++k) s.first_rot[r4 + k] = s.rot[r4 + k];
+      for (int k = 0; k < D; ++k) s.first_obs[(size_t)b * D + k] = s.obs[(size_t)b * D + k];
+    }
+  } else if (mode == RESET_GYM) {
+    if (s.steps) s.steps[b] = 0.0f;
+  }
+}
+
+__global__ void k_any_done(const float *done, int B, uint32_t *flag) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool d = b < B && done[b] != 0.0f;
+  const unsigned long long m = __ballot(d);
+  if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+template <int KIND>
+__global__ void k_default_qp(const void *sysp, int B, const float *qpos, const float *qvel, float *pos, float *rot,
+                             float *vel, float *ang) {
+  csys_t &S = *(csys_t *)(size_t)sysp;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int N = n_bodies<KIND>(S);
+  float qp[POB_NJ], qv[POB_NJ];
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) { qp[j] = qpos[(size_t)b * POB_NJ + j]; qv[j] = qvel[(size_t)b * POB_NJ + j]; }
+  Body bd;
+  fk(S, qp, qv, bd);
+  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  store_body(bd, pos + r3, rot + r4, vel + r3, ang + r3);
+  for (int i = POB_NDYN; i < N; ++i) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { pos[r3 + 3 * i + c] = S.frozen_pos[i][c]; vel[r3 + 3 * i + c] = 0.0f; ang[r3 + 3 * i + c] = 0.0f; }
+    rot[r4 + 4 * i] = 1.0f; rot[r4 + 4 * i + 1] = 0.0f; rot[r4 + 4 * i + 2] = 0.0f; rot[r4 + 4 * i + 3] = 0.0f;
+  }
+}
+
+// --------------------------------------------------------------------------- random
+__global__ void k_split(const uint32_t *key, int num, int first, int count, uint32_t *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t o0, o1;
+  tf_split(key[0], key[1], (uint32_t)num, (uint32_t)(first + i), o0, o1);
+  out[2 * i] = o0; out[2 * i + 1] = o1;
+}
+__global__ void k_uniform(const uint32_t *key, int n, int first, int count, float lo, float hi, float *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  out[i] = tf_uniform(key[0], key[1], (uint32_t)n, (uint32_t)(first + i), lo, hi);
+}
+// act = uniform(split(key)[1], (total, A), -1, 1)[first:first+B]
+__global__ void k_actions(const uint32_t *key, int total, int first, int B, int A, float *act) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * A) return;
+  uint32_t s0, s1;
+  tf_split(key[0], key[1], 2u, 1u, s0, s1);
+  act[i] = tf_uniform(s0, s1, (uint32_t)total * (uint32_t)A, (uint32_t)first * (uint32_t)A + (uint32_t)i, -1.0f, 1.0f);
+}
+__global__ void k_advance_key(uint32_t *key) {
+  uint32_t o0, o1;
+  tf_split(key[0], key[1], 2u, 0u, o0, o1);
+  key[0] = o0; key[1] = o1;
+}
+__global__ void k_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, float *out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * K) return;
+  const int b = t / K, k = t - b * K;
+  out[t] = obs[(size_t)b * D + idx[k]];
+}
+
+// ============================================================================ C ABI
+static thread_local char g_err[512] = "";
+static int fail(int code, const char *msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+static int hip_check(hipError_t e, const char *what) {
+  if (e == hipSuccess) return POB_OK;
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+  return POB_EHIP;
+}
+static inline dim3 grid_for(int n, int bs) { return dim3((unsigned)((n + bs - 1) / bs)); }
+
+extern "C" {
+
+int pob_abi_version(void) { return POB_ABI_VERSION; }
+const char *pob_last_error(void) { return g_err; }
+
+int pob_default_params(pob_params *p) {
+  if (!p) return fail(POB_EINVAL, "params is NULL");
+  pob::default_params(*p);
+  return POB_OK;
+}
+
+int pob_env_create(int kind, const pob_params *p, pob_env **out) {
+  if (!out) return fail(POB_EINVAL, "out is NULL");
+  *out = nullptr;
+  pob_params prm;
+  if (p) prm = *p; else pob::default_params(prm);
+  pob_env *e = new (std::nothrow) pob_env();
+  if (!e) return fail(POB_ENOMEM, "out of host memory");
+  e->params = prm;
+  if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
+  int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
+  if (rc) { delete e; return rc; }
+  rc = hip_check(hipMalloc(&e->d_scratch, 64), "hipMalloc(scratch)");
+  if (rc) { delete e; return rc; }
+  if (kind == POB_GATHER) {
+    static float tmp[3 * 4096];
+    const int n = pob::gather_grid(prm, tmp, 4096);
+    rc = hip_check(hipMalloc(&e->d_grid, sizeof(float) * 3 * n), "hipMalloc(grid)");
+    if (!rc) rc = hip_check(hipMemcpy(e->d_grid, tmp, sizeof(float) * 3 * n, hipMemcpyHostToDevice), "hipMemcpy(grid)");
+    if (rc) { (void)hipFree(e->d_scratch); delete e; return rc; }
+    e->sys.grid = e->d_grid;
+  }
+  rc = hip_check(hipMalloc(&e->d_sys, sizeof(pob_sys)), "hipMalloc(sys)");
+  if (!rc) rc = hip_check(hipMemcpy(e->d_sys, &e->sys, sizeof(pob_sys), hipMemcpyHostToDevice), "hipMemcpy(sys)");
+  if (rc) { if (e->d_grid) (void)hipFree(e->d_grid); (void)hipFree(e->d_scratch); delete e; return rc; }
+  *out = e;
+  return POB_OK;
+}
+
+void pob_env_destroy(pob_env *e) {
+  if (!e) return;
+  if (e->d_grid) (void)hipFree(e->d_grid);
+  if (e->d_scratch) (void)hipFree(e->d_scratch);
+  if (e->d_sys) (void)hipFree(e->d_sys);
+  delete e;
+}
+
+int pob_env_dims(const pob_env *e, int *n, int *d, int *a) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (n) *n = e->sys.N;
+  if (d) *d = e->sys.D;
+  if (a) *a = POB_NJ;
+  return POB_OK;
+}
+
+int pob_env_default_angle(const pob_env *e, float *out8) {
+  if (!e || !out8) return fail(POB_EINVAL, "NULL argument");
+  for (int j = 0; j < POB_NJ; ++j) out8[j] = e->sys.default_angle[j];
+  return POB_OK;
+}
+
+static int check_state(const pob_state *s, bool need_rng) {
+  if (!s) return fail(POB_EINVAL, "state is NULL");
+  if (!s->pos || !s->rot || !s->vel || !s->ang || !s->obs || !s->reward || !s->done)
+    return fail(POB_EINVAL, "state: qp/obs/reward/done pointers are required");
+  if (need_rng && !s->rng) return fail(POB_EINVAL, "state: rng pointer is required");
+  return POB_OK;
+}
+
+int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, void *stream) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
+  if (!keys) return fail(POB_EINVAL, "keys is NULL");
+  if (int rc = check_state(out, true)) return rc;
+  if (out->first_pos && (!out->first_rot || !out->first_vel || !out->first_ang || !out->first_obs))
+    return fail(POB_EINVAL, "state: first_* pointers must be all set or all NULL");
+  hipStream_t st = (hipStream_t)stream;
+  const StatePtrs p = to_ptrs(*out);
+  switch (e->sys.kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
+    default: hipLaunchKernelGGL((k_reset<POB_TAG, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
+  }
+  return hip_check(hipGetLastError(), "k_reset launch");
+}
+
+int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out, uint32_t flags,
+             int episode_length, void *stream) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
+  if (!act) return fail(POB_EINVAL, "action is NULL");
+  if (int rc = check_state(in, true)) return rc;
+  if (int rc = check_state(out, true)) return rc;
+  if ((flags & POB_F_EPISODE) && episode_length <= 0) return fail(POB_EINVAL, "episode_length must be positive");
+  if ((flags & POB_F_AUTORESET) &&
+      (!in->first_pos || !in->first_rot || !in->first_vel || !in->first_ang || !in->first_obs ||
+       !out->first_pos || !out->first_rot || !out->first_vel || !out->first_ang || !out->first_obs))
+    return fail(POB_EINVAL, "AUTORESET needs first_qp/first_obs in both states");
+  if ((flags & POB_F_EPISODE) && (!out->steps || !out->truncation)) return fail(POB_EINVAL, "EPISODE needs steps/truncation");
+  hipStream_t st = (hipStream_t)stream;
+  const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
+  switch (e->sys.kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
+    default: hipLaunchKernelGGL((k_step<POB_TAG>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
+  }
+  return hip_check(hipGetLastError(), "k_step launch");
+}
+
+int pob_reset_where_done(pob_env *e, int B, int mode, const uint32_t *gym_in, uint32_t *gym_out, const pob_state *s,
+                         void *stream) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
+  if (int rc = check_state(s, true)) return rc;
+  if (mode != POB_RESET_GYM && mode != POB_RESET_OWN) return fail(POB_EINVAL, "unknown reset mode");
+  if (mode == POB_RESET_GYM && (!gym_in || !gym_out)) return fail(POB_EINVAL, "gym mode needs gym_key_in/out");
+  hipStream_t st = (hipStream_t)stream;
+  const StatePtrs p = to_ptrs(*s);
+  const uint32_t *flag = s->any_done;
+  if (mode == POB_RESET_GYM && !flag) {
+    int rc = hip_check(hipMemsetAsync(e->d_scratch, 0, 16, st), "hipMemsetAsync");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_any_done, grid_for(B, 256), dim3(256), 0, st, s->done, B, e->d_scratch);
+    flag = e->d_scratch;
+  }
+  const int kmode = mode == POB_RESET_GYM ? RESET_GYM : RESET_OWN;
+  switch (e->sys.kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
+    default: hipLaunchKernelGGL((k_reset<POB_TAG, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
+  }
+  return hip_check(hipGetLastError(), "k_reset(where done) launch");
+}
+
+int pob_default_qp(pob_env *e, int B, const float *qpos, const float *qvel, float *pos, float *rot, float *vel,
+                   float *ang, void *stream) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
+  if (!qpos || !qvel || !pos || !rot || !vel || !ang) return fail(POB_EINVAL, "NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  switch (e->sys.kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_default_qp<POB_HEAVENHELL>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_default_qp<POB_GATHER>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
+    default: hipLaunchKernelGGL((k_default_qp<POB_TAG>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
+  }
+  return hip_check(hipGetLastError(), "k_default_qp launch");
+}
+
+int pob_random_split(const uint32_t *key, int num, int first, int count, uint32_t *out, void *stream) {
+  if (!key || !out) return fail(POB_EINVAL, "NULL argument");
+  if (num <= 0 || first < 0 || count < 0 || first + count > num) return fail(POB_EINVAL, "bad split range");
+  if (count == 0) return POB_OK;
+  hipLaunchKernelGGL(k_split, grid_for(count, 256), dim3(256), 0, (hipStream_t)stream, key, num, first, count, out);
+  return hip_check(hipGetLastError(), "k_split launch");
+}
+
+int pob_random_uniform(const uint32_t *key, int n, int first, int count, float lo, float hi, float *out, void *stream) {
+  if (!key || !out) return fail(POB_EINVAL, "NULL argument");
+  if (n <= 0 || first < 0 || count < 0 || first + count > n) return fail(POB_EINVAL, "bad uniform range");
+  if (count == 0) return POB_OK;
+  hipLaunchKernelGGL(k_uniform, grid_for(count, 256), dim3(256), 0, (hipStream_t)stream, key, n, first, count, lo, hi, out);
+  return hip_check(hipGetLastError(), "k_uniform launch");
+}
+
+int pob_random_actions(uint32_t *key_io, int total, int first, int B, int A, float *act, void *stream) {
+  if (!key_io || !act) return fail(POB_EINVAL, "NULL argument");
+  if (B <= 0 || A <= 0 || first < 0 || first + B > total) return fail(POB_EINVAL, "bad action shard");
+  if ((long long)total * A >= 4294967295LL) return fail(POB_EINVAL, "too many action elements");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_actions, grid_for(B * A, 256), dim3(256), 0, st, key_io, total, first, B, A, act);
+  hipLaunchKernelGGL(k_advance_key, dim3(1), dim3(1), 0, st, key_io);
+  return hip_check(hipGetLastError(), "k_actions launch");
+}
+
+int pob_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, float *out, void *stream) {
+  if (!obs || !idx || !out) return fail(POB_EINVAL, "NULL argument");
+  if (B <= 0 || D <= 0 || K <= 0) return fail(POB_EINVAL, "bad shape");
+  hipLaunchKernelGGL(k_obs_gather, grid_for(B * K, 256), dim3(256), 0, (hipStream_t)stream, obs, B, D, idx, K, out);
+  return hip_check(hipGetLastError(), "k_obs_gather launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// pob_math.h -- device math for the rollout kernels (gfx950).
+//
+// Every expression here has a FIXED evaluation order and the library is compiled with
+// -ffp-contract=off, so results are reproducible IEEE-754 binary32 (add/sub/mul/div/sqrt
+// correctly rounded on gfx950).  Transcendentals use explicit polynomial forms instead of
+// ocml so that the float results are a deterministic function of the inputs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define POB_D __device__ __forceinline__
+
+struct v3 { float x, y, z; };
+struct q4 { float w, x, y, z; };
+
+POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+POB_D v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+POB_D v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+POB_D v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+POB_D v3 vdivs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+POB_D float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+POB_D v3 vcross(v3 a, v3 b) {
+  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+POB_D v3 vload(const float *p) { return V(p[0], p[1], p[2]); }
+
+// brax.math.rotate(v, q) = 2 (u.v) u + (s^2 - u.u) v + 2 s (u x v)
+POB_D v3 qrot(v3 v, q4 q) {
+  v3 u = V(q.x, q.y, q.z);
+  float t = vdot(u, v);
+  float c = q.w * q.w - vdot(u, u);
+  float s2 = 2.0f * q.w;
+  v3 cr = vcross(u, v);
+  v3 r = V(2.0f * (t * u.x) + c * v.x, 2.0f * (t * u.y) + c * v.y, 2.0f * (t * u.z) + c * v.z);
+  return V(r.x + s2 * cr.x, r.y + s2 * cr.y, r.z + s2 * cr.z);
+}
+// brax.math.quat_mul
+POB_D q4 qmul(q4 u, q4 v) {
+  q4 r;
+  r.w = u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z;
+  r.x = u.w * v.x + u.x * v.w + u.y * v.z - u.z * v.y;
+  r.y = u.w * v.y - u.x * v.z + u.y * v.w + u.z * v.x;
+  r.z = u.w * v.z + u.x * v.y - u.y * v.x + u.z * v.w;
+  return r;
+}
+// quat_mul([0, a], q)
+POB_D q4 qmul_vq(v3 a, q4 q) {
+  q4 r;
+  r.w = -(a.x * q.x) - a.y * q.y - a.z * q.z;
+  r.x = a.x * q.w + a.y * q.z - a.z * q.y;
+  r.y = -(a.x * q.z) + a.y * q.w + a.z * q.x;
+  r.z = a.x * q.y - a.y * q.x + a.z * q.w;
+  return r;
+}
+POB_D q4 qinv(q4 q) { q4 r; r.w = q.w; r.x = -q.x; r.y = -q.y; r.z = -q.z; return r; }
+POB_D q4 qnormalize(q4 q) {
+  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  q4 r; r.w = q.w / n; r.x = q.x / n; r.y = q.y / n; r.z = q.z / n;
+  return r;
+}
+// acc += sign * 0.5 * d
+POB_D void qadd_half(q4 &acc, q4 d, float sign) {
+  acc.w += sign * (0.5f * d.w); acc.x += sign * (0.5f * d.x);
+  acc.y += sign * (0.5f * d.y); acc.z += sign * (0.5f * d.z);
+}
+
+// Cephes-form atanf / atan2f
+POB_D float pob_atanf(float x) {
+  float sign = 1.0f, y = 0.0f;
+  if (x < 0.0f) { sign = -1.0f; x = -x; }
+  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -(1.0f / x); }
+  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = (x - 1.0f) / (x + 1.0f); }
+  float z = x * x;
+  y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -
+            3.33329491539e-1f) * z * x + x);
+  return sign * y;
+}
+POB_D float pob_atan2f(float y, float x) {
+  if (x == 0.0f) {
+    if (y < 0.0f) return -1.5707963267948966f;
+    if (y == 0.0f) return 0.0f;
+    return 1.5707963267948966f;
+  }
+  if (y == 0.0f) return x < 0.0f ? 3.141592653589793f : 0.0f;
+  float w = 0.0f;
+  if (x < 0.0f) w = (y < 0.0f) ? -3.141592653589793f : 3.141592653589793f;
+  return w + pob_atanf(y / x);
+}
+// Cephes-form sinf/cosf (Cody-Waite reduction by pi/4)
+POB_D void pob_sincosf(float x, float *s, float *c) {
+  float sgn_s = 1.0f, sgn_c = 1.0f;
+  if (x < 0.0f) { x = -x; sgn_s = -1.0f; }
+  int j = (int)(1.27323954473516f * x);
+  float y = (float)j;
+  if (j & 1) { j += 1; y += 1.0f; }
+  j &= 7;
+  if (j > 3) { sgn_s = -sgn_s; sgn_c = -sgn_c; j -= 4; }
+  if (j > 1) sgn_c = -sgn_c;
+  float xr = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+  float z = xr * xr;
+  float ps = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * xr + xr;
+  float pc = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) *
+                 z * z - 0.5f * z + 1.0f;
+  if (j == 1 || j == 2) { *s = sgn_s * pc; *c = sgn_c * ps; }
+  else { *s = sgn_s * ps; *c = sgn_c * pc; }
+}
+
+// ------------------------------------------------------------------------- threefry
+// jax.random threefry2x32 (20 rounds), pre-partitionable scheme.
+POB_D uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+POB_D void threefry2x32(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1, uint32_t &y0,
+                        uint32_t &y1) {
+  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  uint32_t a = x0 + k0, b = x1 + k1;
+#define POB_TF_R(r) a += b; b = rotl32(b, r); b ^= a;
+  POB_TF_R(13) POB_TF_R(15) POB_TF_R(26) POB_TF_R(6)
+  a += k1; b += k2 + 1u;
+  POB_TF_R(17) POB_TF_R(29) POB_TF_R(16) POB_TF_R(24)
+  a += k2; b += k0 + 2u;
+  POB_TF_R(13) POB_TF_R(15) POB_TF_R(26) POB_TF_R(6)
+  a += k0; b += k1 + 3u;
+  POB_TF_R(17) POB_TF_R(29) POB_TF_R(16) POB_TF_R(24)
+  a += k1; b += k2 + 4u;
+  POB_TF_R(13) POB_TF_R(15) POB_TF_R(26) POB_TF_R(6)
+  a += k2; b += k0 + 5u;
+#undef POB_TF_R
+  y0 = a; y1 = b;
+}
+
+// element j of threefry_2x32(key, iota(n)) (odd n padded with a zero count)
+POB_D uint32_t tf_elem(uint32_t k0, uint32_t k1, uint32_t n, uint32_t j) {
+  const uint32_t h = (n + 1u) >> 1;
+  uint32_t y0, y1;
+  if (j < h) {
+    uint32_t x1 = j + h;
+    if (x1 >= n) x1 = 0u;
+    threefry2x32(k0, k1, j, x1, y0, y1);
+    return y0;
+  }
+  threefry2x32(k0, k1, j - h, j, y0, y1);
+  return y1;
+}
+// row i of split(key, num)
+POB_D void tf_split(uint32_t k0, uint32_t k1, uint32_t num, uint32_t i, uint32_t &o0, uint32_t &o1) {
+  o0 = tf_elem(k0, k1, 2u * num, 2u * i);
+  o1 = tf_elem(k0, k1, 2u * num, 2u * i + 1u);
+}
+POB_D float bits_to_unit(uint32_t b) { return __uint_as_float((b >> 9) | 0x3F800000u) - 1.0f; }
+// jax.random.uniform element: max(lo, f*(hi-lo)+lo)
+POB_D float tf_uniform(uint32_t k0, uint32_t k1, uint32_t n, uint32_t i, float lo, float hi) {
+  float f = bits_to_unit(tf_elem(k0, k1, n, i));
+  float v = f * (hi - lo) + lo;
+  return v > lo ? v : lo;
+}

@@ -1,0 +1,370 @@
+// pob_physics.h -- the PBD Ant step on one lane (= one environment), gfx950.
+//
+// One lane owns one env: the 9 dynamic bodies (pos, rot, vel, ang = 117 floats), the
+// substep-start copy (63), the Jacobi accumulators and the per-contact scratch all live in
+// VGPRs (fully unrolled over bodies / joints / contacts, compile-time indices only), so a
+// control step touches HBM only to load and store the state once.
+//
+// Algorithm = brax v1 System.step with dynamics_mode "pbd" as restated in DESIGN.md §3
+// (brax is not vendored: reference call sites ant_heavenhell.py:108, ant_gather.py:127,
+// ant_tag.py:109).  Op order matches oracle/pob_oracle.c expression for expression.
+#pragma once
+#include "pob_math.h"
+#include "pob_sys.h"
+
+struct Body {
+  v3 x[POB_NDYN];
+  q4 q[POB_NDYN];
+  v3 v[POB_NDYN];
+  v3 w[POB_NDYN];
+};
+
+struct Contacts {
+  // [0, 5): ground (CapsulePlane, normal +z, end point S.ground_end[k]),
+  // [5, 14): deepest wall contact of capsule i (normal n[i], end point cap_end[i][sel[i]])
+  float pen[POB_NGROUND + POB_NDYN];
+  v3 n[POB_NDYN];
+  bool sel[POB_NDYN];
+};
+
+// Hide the table pointer from loop-invariant code motion: without this the compiler
+// hoists every table value of the unrolled substep into SGPRs and spills hundreds of
+// them.  Re-laundering per joint / contact keeps each value's scalar load next to its use
+// (scalar-cache hits).
+typedef __attribute__((address_space(4))) const pob_sys csys_t;  // constant address space
+POB_D csys_t *launder(csys_t *p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// Scheduling fence between the independent joint / contact blocks: without it the machine
+// scheduler interleaves all of them for ILP and the live set blows past 512 registers.
+#define POB_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Per-lane LDS scratch, lane-minor (element e of lane t at base[e * BS + t]): conflict-free
+// ds_read/ds_write_b32.  Holds what the substep keeps live but rarely touches: the
+// substep-start pose (63 floats, read by static friction and the velocity projection) and
+// the Info.contact accumulators (54 floats, touched once per collide substep).
+struct Lds {
+  float *base;
+  int stride, t;
+  POB_D float get(int e) const { return base[e * stride + t]; }
+  POB_D void set(int e, float v) const { base[e * stride + t] = v; }
+  POB_D v3 get3(int e) const { return V(get(e), get(e + 1), get(e + 2)); }
+  POB_D void set3(int e, v3 v) const { set(e, v.x); set(e + 1, v.y); set(e + 2, v.z); }
+  POB_D q4 get4(int e) const { q4 q; q.w = get(e); q.x = get(e + 1); q.y = get(e + 2); q.z = get(e + 3); return q; }
+  POB_D void set4(int e, q4 q) const { set(e, q.w); set(e + 1, q.x); set(e + 2, q.y); set(e + 3, q.z); }
+};
+#define POB_LDS_PX(i) (7 * (i))          // prev pos (3) + prev rot (4) of body i
+#define POB_LDS_PQ(i) (7 * (i) + 3)
+#define POB_LDS_CV(i) (63 + 6 * (i))     // Info.contact vel / ang of body i
+#define POB_LDS_CA(i) (63 + 6 * (i) + 3)
+#define POB_LDS_FLOATS 117
+
+POB_D constexpr int jparent(int j) { return (j & 1) ? j : 0; }
+POB_D constexpr int jchild(int j) { return j + 1; }
+POB_D constexpr int ground_body(int g) { return 2 * g; }
+POB_D constexpr int contact_body(int k) { return k < POB_NGROUND ? 2 * k : k - POB_NGROUND; }
+
+#define SV(a) V((a)[0], (a)[1], (a)[2])
+
+// sphere (centre p, radius r) vs z-rotated box w -> penetration, world normal
+POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
+  const float c = S.wall_cos[w], s = S.wall_sin[w];
+  const v3 h = SV(S.wall_h[w]);
+  v3 d = vsub(p, SV(S.wall_c[w]));
+  float lx = d.x * c + d.y * s, ly = -(d.x * s) + d.y * c, lz = d.z;
+  float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
+  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
+  float d2 = ex * ex + ey * ey + ez * ez;
+  float pen, nx, ny, nz;
+  if (d2 > 0.0f) {
+    float dist = sqrtf(d2);
+    pen = r - dist; nx = ex / dist; ny = ey / dist; nz = ez / dist;
+  } else {
+    float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
+    nx = 0.0f; ny = 0.0f; nz = 0.0f;
+    if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
+    else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
+    else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
+  }
+  n = V(nx * c - ny * s, nx * s + ny * c, nz);
+  return pen;
+}
+
+// Contact detection of a collide substep: CapsulePlane on the torso and the four feet,
+// and for every capsule its deepest sphere-box contact over (wall, segment end).
+POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
+#pragma unroll
+  for (int g = 0; g < POB_NGROUND; ++g) {
+    csys_t &S = *launder(Sp);
+    const int i = ground_body(g);
+    v3 pe = vadd(b.x[i], qrot(SV(S.ground_end[g]), b.q[i]));
+    ct.pen[g] = S.ground_r[g] - pe.z;
+  }
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) {
+    POB_FENCE();
+    csys_t &S = *launder(Sp);
+    const int nend = (i == 0) ? 1 : 2;
+    v3 pe[2];
+#pragma unroll
+    for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[i], qrot(SV(S.cap_end[i][q]), b.q[i]));
+    float best = 0.0f;
+    v3 bn = V(0.0f, 0.0f, 0.0f);
+    bool bsel = false;
+    const float r = S.cap_r[i];
+    const int nw = S.n_walls;
+    for (int w = 0; w < nw; ++w) {
+#pragma unroll
+      for (int q = 0; q < nend; ++q) {
+        v3 n;
+        float pen = sphere_box(*launder(Sp), w, pe[q], r, n);
+        if (pen > best) { best = pen; bn = n; bsel = q == 1; }
+      }
+    }
+    ct.pen[POB_NGROUND + i] = best;
+    ct.n[i] = bn;
+    ct.sel[i] = bsel;
+  }
+}
+
+// contact k: body frame end point, world normal, radius
+POB_D void contact_geom(csys_t &S, const Contacts &ct, int k, v3 &e, v3 &n, float &r) {
+  if (k < POB_NGROUND) {
+    e = SV(S.ground_end[k]);
+    n = V(0.0f, 0.0f, 1.0f);
+    r = S.ground_r[k];
+  } else {
+    const int i = k - POB_NGROUND;
+    const v3 e0 = SV(S.cap_end[i][0]), e1 = SV(S.cap_end[i][1]);
+    e = ct.sel[i] ? e1 : e0;
+    n = ct.n[i];
+    r = S.cap_r[i];
+  }
+}
+
+POB_D void contact_position(csys_t *Sp, const Body &b, const Lds &L, const Contacts &ct,
+                            v3 (&DX)[POB_NDYN], q4 (&DQ)[POB_NDYN]) {
+#pragma unroll
+  for (int k = 0; k < POB_NGROUND + POB_NDYN; ++k) {
+    POB_FENCE();
+    const int i = contact_body(k);
+    const float pen = ct.pen[k];
+    if (pen > 0.0f) {
+      csys_t &S = *launder(Sp);
+      v3 e, n;
+      float rad;
+      contact_geom(S, ct, k, e, n, rad);
+      const float im = S.inv_mass[i];
+      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
+      v3 cp = vsub(pe, vscl(n, rad));
+      v3 rr = vsub(cp, b.x[i]);
+      v3 cn = vcross(rr, n);
+      float w = im + vdot(cn, cn);
+      float lam = pen / w;
+      v3 P = vscl(n, lam);
+      q4 dq = qmul_vq(vcross(rr, P), b.q[i]);
+      DX[i] = vadd(DX[i], vscl(P, im));
+      DQ[i].w += 0.5f * dq.w; DQ[i].x += 0.5f * dq.x; DQ[i].y += 0.5f * dq.y; DQ[i].z += 0.5f * dq.z;
+      v3 cprev = vadd(L.get3(POB_LDS_PX(i)), qrot(qrot(rr, qinv(b.q[i])), L.get4(POB_LDS_PQ(i))));
+      v3 dp = vsub(cp, cprev);
+      v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
+      float lt = sqrtf(vdot(dpt, dpt));
+      if (lt > 0.0f) {
+        v3 t = vdivs(dpt, lt);
+        v3 ctn = vcross(rr, t);
+        float wt = im + vdot(ctn, ctn);
+        float lamt = lt / wt;
+        if (lamt < S.friction * lam) {
+          v3 Pt = vscl(t, -lamt);
+          q4 dqt = qmul_vq(vcross(rr, Pt), b.q[i]);
+          DX[i] = vadd(DX[i], vscl(Pt, im));
+          DQ[i].w += 0.5f * dqt.w; DQ[i].x += 0.5f * dqt.x; DQ[i].y += 0.5f * dqt.y; DQ[i].z += 0.5f * dqt.z;
+        }
+      }
+    }
+  }
+}
+
+POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&dV)[POB_NDYN],
+                            v3 (&dW)[POB_NDYN]) {
+#pragma unroll
+  for (int k = 0; k < POB_NGROUND + POB_NDYN; ++k) {
+    POB_FENCE();
+    const int i = contact_body(k);
+    const float pen = ct.pen[k];
+    if (pen > 0.0f) {
+      csys_t &S = *launder(Sp);
+      v3 e, n;
+      float rad;
+      contact_geom(S, ct, k, e, n, rad);
+      const float im = S.inv_mass[i];
+      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
+      v3 cp = vsub(pe, vscl(n, rad));
+      v3 rr = vsub(cp, b.x[i]);
+      v3 vr = vadd(b.v[i], vcross(b.w[i], rr));
+      float vn = vdot(vr, n);
+      v3 vt = vsub(vr, vscl(n, vn));
+      float lt = sqrtf(vdot(vt, vt));
+      v3 dv = V(0.0f, 0.0f, 0.0f);
+      if (lt > 0.0f) {
+        float fr = fminf(S.friction * pen / S.h, lt);
+        dv = vscl(vt, -(fr / lt));
+      }
+      if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+      float D = sqrtf(vdot(dv, dv));
+      if (D > 0.0f) {
+        v3 dh = vdivs(dv, D);
+        v3 cd = vcross(rr, dh);
+        float w = im + vdot(cd, cd);
+        v3 P = vdivs(dv, w);
+        dV[i] = vadd(dV[i], vscl(P, im));
+        dW[i] = vadd(dW[i], vcross(rr, P));
+      }
+    }
+  }
+}
+
+POB_D void joints_position(csys_t *Sp, const Body &b, v3 (&DX)[POB_NDYN], q4 (&DQ)[POB_NDYN]) {
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) {
+    POB_FENCE();
+    csys_t &S = *launder(Sp);
+    const int p = jparent(j), c = jchild(j);
+    const float imp = S.inv_mass[p], imc = S.inv_mass[c];
+    // point-to-point constraint between the joint anchors
+    v3 rp = qrot(SV(S.off_p[j]), b.q[p]), rc = qrot(SV(S.off_c[j]), b.q[c]);
+    v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
+    float L = sqrtf(vdot(d, d));
+    if (L > 0.0f) {
+      v3 n = vdivs(d, L);
+      v3 cp = vcross(rp, n), cc = vcross(rc, n);
+      float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
+      float lam = (L / wsum) * S.s_pos;
+      v3 P = vscl(n, lam);
+      DX[p] = vadd(DX[p], vscl(P, imp));
+      qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
+      DX[c] = vsub(DX[c], vscl(P, imc));
+      qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
+    }
+    // hinge axis alignment (unit inverse inertia: w_p = w_c = 1)
+    const v3 axis = SV(S.axis[j]);
+    v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
+    v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+    qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
+    qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
+    // angle limits about the parent's hinge axis (brax math.signed_angle)
+    const v3 ref = SV(S.ref[j]);
+    v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
+    float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    float dl = 0.0f;
+    if (psi < S.lim_lo[j]) dl = psi - S.lim_lo[j];
+    else if (psi > S.lim_hi[j]) dl = psi - S.lim_hi[j];
+    v3 Pl = vscl(ap, dl * S.half_s_ang);
+    qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
+    qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
+  }
+}
+
+// One XPBD substep; COLLIDE selects the second substep of each brax PBD iteration.
+POB_D void pbd_substep(csys_t *Sp, Body &b, const float (&act)[POB_NJ], const Lds &L, const bool COLLIDE) {
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) { L.set3(POB_LDS_PX(i), b.x[i]); L.set4(POB_LDS_PQ(i), b.q[i]); }
+  // 1. acceleration level: torque actuators + joint angular damping; gravity
+  {
+    v3 dw[POB_NDYN];
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) dw[i] = V(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int j = 0; j < POB_NJ; ++j) {
+      csys_t &S = *launder(Sp);
+      const int p = jparent(j), c = jchild(j);
+      v3 a = qrot(SV(S.axis[j]), b.q[p]);
+      v3 t = vscl(a, act[j] * S.strength[j]);
+      v3 d = vscl(vsub(b.w[p], b.w[c]), S.jdamp[j]);
+      v3 tt = vadd(t, d);
+      dw[p] = vsub(dw[p], tt);
+      dw[c] = vadd(dw[c], tt);
+    }
+    csys_t &S = *launder(Sp);
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) {
+      const v3 v = b.v[i], w = b.w[i];
+      b.v[i] = V(S.lin_damp * v.x + 0.0f * S.h, S.lin_damp * v.y + 0.0f * S.h, S.lin_damp * v.z + S.gz * S.h);
+      b.w[i] = V(S.ang_damp * w.x + dw[i].x * S.h, S.ang_damp * w.y + dw[i].y * S.h,
+                 S.ang_damp * w.z + dw[i].z * S.h);
+    }
+    // 2. kinetic
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) {
+      b.x[i] = vadd(b.x[i], vscl(b.v[i], S.h));
+      q4 dq = qmul_vq(b.w[i], b.q[i]);
+      q4 q = b.q[i];
+      q.w = q.w + S.half_h * dq.w; q.x = q.x + S.half_h * dq.x;
+      q.y = q.y + S.half_h * dq.y; q.z = q.z + S.half_h * dq.z;
+      b.q[i] = qnormalize(q);
+    }
+  }
+  // 3. position projection (Jacobi: joints + contacts from the same state)
+  Contacts ct;
+  {
+    v3 DX[POB_NDYN];
+    q4 DQ[POB_NDYN];
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) { DX[i] = V(0.0f, 0.0f, 0.0f); DQ[i].w = DQ[i].x = DQ[i].y = DQ[i].z = 0.0f; }
+    joints_position(Sp, b, DX, DQ);
+    if (COLLIDE) {
+      detect(Sp, b, ct);
+      contact_position(Sp, b, L, ct, DX, DQ);
+    }
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) {
+      b.x[i] = vadd(b.x[i], DX[i]);
+      b.q[i].w += DQ[i].w; b.q[i].x += DQ[i].x; b.q[i].y += DQ[i].y; b.q[i].z += DQ[i].z;
+    }
+  }
+  // 4. velocity projection
+  {
+    csys_t &S = *launder(Sp);
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) {
+      b.q[i] = qnormalize(b.q[i]);
+      b.v[i] = vdivs(vsub(b.x[i], L.get3(POB_LDS_PX(i))), S.h);
+      q4 dq = qmul(b.q[i], qinv(L.get4(POB_LDS_PQ(i))));
+      float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
+      b.w[i] = V(sg * ((2.0f * dq.x) / S.h), sg * ((2.0f * dq.y) / S.h), sg * ((2.0f * dq.z) / S.h));
+    }
+  }
+  // 5. velocity-level contact solve, accumulated into Info.contact (LDS)
+  if (COLLIDE) {
+    v3 dV[POB_NDYN], dW[POB_NDYN];
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) { dV[i] = V(0.0f, 0.0f, 0.0f); dW[i] = V(0.0f, 0.0f, 0.0f); }
+    contact_velocity(Sp, b, ct, dV, dW);
+#pragma unroll
+    for (int i = 0; i < POB_NDYN; ++i) {
+      b.v[i] = vadd(b.v[i], dV[i]); b.w[i] = vadd(b.w[i], dW[i]);
+      L.set3(POB_LDS_CV(i), vadd(L.get3(POB_LDS_CV(i)), dV[i]));
+      L.set3(POB_LDS_CA(i), vadd(L.get3(POB_LDS_CA(i)), dW[i]));
+    }
+  }
+}
+
+// brax System.step: substeps/2 iterations of (plain substep, collide substep); the summed
+// contact impulses (Info.contact) are left in L at POB_LDS_CV / POB_LDS_CA.
+POB_D void physics_step(csys_t *Sp, Body &b, const float (&act)[POB_NJ], const Lds &L) {
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) { L.set3(POB_LDS_CV(i), V(0.0f, 0.0f, 0.0f)); L.set3(POB_LDS_CA(i), V(0.0f, 0.0f, 0.0f)); }
+  const int iters = launder(Sp)->substeps / 2;
+#pragma nounroll
+  for (int it = 0; it < 2 * iters; ++it) pbd_substep(Sp, b, act, L, (it & 1) != 0);
+}
+
+// sys.info(qp).contact at a static state
+POB_D void info_contact(csys_t *Sp, const Body &b, v3 (&cvel)[POB_NDYN], v3 (&cang)[POB_NDYN]) {
+  Contacts ct;
+  detect(Sp, b, ct);
+#pragma unroll
+  for (int i = 0; i < POB_NDYN; ++i) { cvel[i] = V(0.0f, 0.0f, 0.0f); cang[i] = V(0.0f, 0.0f, 0.0f); }
+  contact_velocity(Sp, b, ct, cvel, cang);
+}

@@ -1,0 +1,46 @@
+// pob_sys.h -- static system tables of one env instance (host-built, passed to every
+// kernel by value as a kernel argument, so the wave reads them through the scalar cache).
+//
+// Built by pob_system.cpp from the constructor kwargs exactly as brax.System(cfg) is built
+// from extend_ant_cfg(...) in the reference (ant_heavenhell.py:13-39, ant_gather.py:17-39,
+// ant_tag.py:13-25, envs/utils.py:6-119).  The ant's TOPOLOGY is compile-time (8 revolute
+// joints, parent(j) = j odd ? j : 0, child(j) = j + 1; ground contacts on bodies
+// 0,2,4,6,8); every number (offsets, axes, limits, masses, capsules, walls) is data.
+#pragma once
+#include <stdint.h>
+
+#define POB_NDYN 9      // dynamic ant bodies
+#define POB_NJ 8        // revolute joints == actuators == action dim
+#define POB_NGROUND 5   // collide_include Ant x Ground pairs
+#define POB_MAXW 8      // walls (HH T-maze: 8, arenas: 4)
+#define POB_MAXB 43     // bodies (GA: 11 + up to 32 objects)
+#define POB_MAXOBJ 32   // GA apples + bombs
+#define POB_MAXBINS 32  // GA 2 * n_bins
+
+struct pob_sys {
+  int kind, N, D, n_obj;
+  int substeps, n_walls, n_grid;
+  int ga_n_apples, ga_n_bins;
+  // integrator (dt_sub = dt / substeps)
+  float h, half_h, lin_damp, ang_damp, gz;
+  float inv_mass[POB_NDYN];
+  // joints: parent/child offsets, hinge axis and reference direction (body frame),
+  // limits (rad), angular damping, actuator strength, default angle
+  float off_p[POB_NJ][3], off_c[POB_NJ][3], axis[POB_NJ][3], ref[POB_NJ][3];
+  float lim_lo[POB_NJ], lim_hi[POB_NJ], jdamp[POB_NJ], strength[POB_NJ], default_angle[POB_NJ];
+  // one capsule per dynamic body: segment end points (body frame) and radius; body 0's
+  // segment is degenerate (a sphere: one end point)
+  float cap_end[POB_NDYN][2][3], cap_r[POB_NDYN];
+  float ground_end[POB_NGROUND][3], ground_r[POB_NGROUND];
+  // walls: box centre (world), half extents, z-rotation cos/sin
+  float wall_c[POB_MAXW][3], wall_h[POB_MAXW][3], wall_cos[POB_MAXW], wall_sin[POB_MAXW];
+  float friction, s_pos, half_s_ang;
+  // default_qp rows of the frozen bodies (index >= 9)
+  float frozen_pos[POB_MAXB][3];
+  // env parameters (float32 as the reference's jnp scalars)
+  float hh_hhp[2][2], hh_priest[2], hh_visible_radius, hh_dying_cost;
+  float ga_catch_range, ga_sensor_range, ga_half_span, ga_bin_res, ga_dying_cost, ga_waiting[3];
+  float tag_tag_radius, tag_visible_radius, tag_target_step, tag_min_spawn_distance;
+  float tag_cage_xy[2], tag_dying_cost;
+  const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env
+};

@@ -1,0 +1,207 @@
+// pob_system.cpp -- builds the static tables of one env (the brax.System(cfg) step).
+//
+// What the reference does at construction (all [ext] brax v1 unless a file is cited):
+//   * extend_ant_cfg adds walls / spheres to brax.envs.ant._SYSTEM_CONFIG
+//     (ant_heavenhell.py:13-39, ant_gather.py:17-39, ant_tag.py:13-25);
+//   * draw_t_maze / draw_arena / add_box_wall_to_body compute the wall boxes
+//     (envs/utils.py:6-28, 60-83, 87-119);
+//   * brax.System derives joint axes from the euler `rotation`, capsule end points from
+//     the collider rotation, and integrator constants from dt / substeps;
+//   * ActionRepeatWrapper multiplies dt and substeps by action_repeat (wrappers.py:16-24).
+// Config floats live in float32 protobuf fields, so they are rounded to float32 before
+// any double-precision derivation, and every derived constant is rounded once at the end.
+#include <cmath>
+#include <cstring>
+
+#include "pob_sys.h"
+#include "../../include/pob.h"
+
+namespace pob {
+
+static double f32d(double x) { return (double)(float)x; }
+
+static void d_euler_to_quat(const double e[3], double q[4]) {
+  double c1 = cos(e[0] * M_PI / 360), c2 = cos(e[1] * M_PI / 360), c3 = cos(e[2] * M_PI / 360);
+  double s1 = sin(e[0] * M_PI / 360), s2 = sin(e[1] * M_PI / 360), s3 = sin(e[2] * M_PI / 360);
+  q[0] = c1 * c2 * c3 - s1 * s2 * s3;
+  q[1] = s1 * c2 * c3 + c1 * s2 * s3;
+  q[2] = c1 * s2 * c3 - s1 * c2 * s3;
+  q[3] = c1 * c2 * s3 + s1 * s2 * c3;
+}
+static void d_rotate(const double v[3], const double q[4], double r[3]) {
+  double s = q[0], u[3] = {q[1], q[2], q[3]};
+  double t = u[0] * v[0] + u[1] * v[1] + u[2] * v[2];
+  double c = s * s - (u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  double cr[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+  for (int i = 0; i < 3; ++i) r[i] = 2 * (t * u[i]) + c * v[i] + 2 * s * cr[i];
+}
+
+// brax ant (brax.envs.ant._SYSTEM_CONFIG as serialised in notebooks/ant_tag.ipynb:449)
+static const double kMass[POB_NDYN] = {10, 1, 1, 1, 1, 1, 1, 1, 1};
+static const double kCapsule[POB_NDYN][3] = {  // radius, length, end
+    {0.25, 0.5, 1},  {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1},
+    {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1}, {0.08, 0.44284272, 0},
+    {0.08, 0.7256854, -1}, {0.08, 0.44284272, 0}, {0.08, 0.7256854, -1}};
+static const double kCapsuleRot[POB_NDYN][3] = {
+    {0, 0, 0},   {90, -45, 0},  {90, -45, 0},  {90, 45, 0},  {90, 45, 0},
+    {-90, 45, 0}, {-90, 45, 0}, {-90, -45, 0}, {-90, -45, 0}};
+static const double kJoint[POB_NJ][11] = {  // parent_offset(3) child_offset(3) rotation(3) min max
+    {0.2, 0.2, 0, -0.1, -0.1, 0, 0, -90, 0, -30, 30},
+    {0.1, 0.1, 0, -0.2, -0.2, 0, 0, 0, 135, 30, 70},
+    {-0.2, 0.2, 0, 0.1, -0.1, 0, 0, -90, 0, -30, 30},
+    {-0.1, 0.1, 0, 0.2, -0.2, 0, 0, 0, 45, -70, -30},
+    {-0.2, -0.2, 0, 0.1, 0.1, 0, 0, -90, 0, -30, 30},
+    {-0.1, -0.1, 0, 0.2, 0.2, 0, 0, 0, 135, -70, -30},
+    {0.2, -0.2, 0, -0.1, 0.1, 0, 0, -90, 0, -30, 30},
+    {0.1, -0.1, 0, -0.2, 0.2, 0, 0, 0, 45, 30, 70}};
+static const int kGroundBody[POB_NGROUND] = {0, 2, 4, 6, 8};  // collide_include Ant x Ground
+
+// envs/utils.py:6-28: box from `from` to `to` in xy, halfsize (|v|/2, width, half_height),
+// rotation.z = arccos(x_hat . v / |v|) in degrees, on the frozen Arena body (z = 0.5).
+static void add_box_wall(pob_sys &s, double fx, double fy, double tx, double ty, double half_h,
+                         double width) {
+  int w = s.n_walls++;
+  double vx = tx - fx, vy = ty - fy;
+  double len = sqrt(vx * vx + vy * vy);
+  double zr = acos((1.0 * vx + 0.0 * vy) / len) * 180.0 / M_PI;
+  double mx = f32d((fx + tx) / 2), my = f32d((fy + ty) / 2);
+  double ang = f32d(zr) * M_PI / 180.0;
+  s.wall_c[w][0] = (float)mx; s.wall_c[w][1] = (float)my; s.wall_c[w][2] = 0.5f;
+  s.wall_h[w][0] = (float)f32d(len / 2); s.wall_h[w][1] = (float)f32d(width);
+  s.wall_h[w][2] = (float)f32d(half_h);
+  s.wall_cos[w] = (float)cos(ang);
+  s.wall_sin[w] = (float)sin(ang);
+}
+
+// grid of AntGather object slots (ant_gather.py:88-91); returns count, fills xyz
+int gather_grid(const pob_params &p, float *xyz, int cap) {
+  int n = 0;
+  float cx = p.ga_cage_xy[0], cy = p.ga_cage_xy[1];
+  for (float gy = -cy; gy < cy + 1.0f; gy += 1.0f)
+    for (float gx = -cx; gx < cx + 1.0f; gx += 1.0f)
+      if (sqrtf(gx * gx + gy * gy) > p.ga_robot_object_spacing) {
+        if (n < cap) { xyz[3 * n] = gx; xyz[3 * n + 1] = gy; xyz[3 * n + 2] = 0.0f; }
+        ++n;
+      }
+  return n;
+}
+
+void default_params(pob_params &p) {
+  memset(&p, 0, sizeof(p));
+  p.hh_heaven_hell[0][0] = -5.25f; p.hh_heaven_hell[0][1] = 7.0f;
+  p.hh_heaven_hell[1][0] = 5.25f;  p.hh_heaven_hell[1][1] = 7.0f;
+  p.hh_priest[0] = 0.0f; p.hh_priest[1] = 7.0f;
+  p.hh_visible_radius = 2.0f; p.hh_dying_cost = -2.0f;
+  p.ga_n_apples = 8; p.ga_n_bombs = 8;
+  p.ga_cage_xy[0] = 6.0f; p.ga_cage_xy[1] = 6.0f;
+  p.ga_robot_object_spacing = 2.0f; p.ga_catch_range = 1.0f; p.ga_n_bins = 10;
+  p.ga_sensor_range = 6.0f; p.ga_sensor_span = 3.14159265358979323846f; p.ga_dying_cost = -10.0f;
+  p.tag_tag_radius = 1.5f; p.tag_visible_radius = 3.0f; p.tag_target_step = 0.5f;
+  p.tag_min_spawn_distance = 5.0f; p.tag_cage_xy[0] = 4.5f; p.tag_cage_xy[1] = 4.5f;
+  p.tag_dying_cost = -1.0f;
+  p.action_repeat = 1;
+  p.solver_scale_pos = 0.6f; p.solver_scale_ang = 0.2f;
+}
+
+// Returns an error message or nullptr.  grid (GA) is filled separately by the caller.
+const char *build_system(int kind, const pob_params &p, pob_sys &s) {
+  memset(&s, 0, sizeof(s));
+  if (kind < 0 || kind > 2) return "unknown env kind";
+  if (p.action_repeat < 1) return "action_repeat must be >= 1";
+  s.kind = kind;
+  const int ar = p.action_repeat;
+  const double dt = f32d(0.05) * ar;
+  const int sub = 10 * ar;
+  const double hd = dt / sub;
+  s.substeps = sub;
+  s.h = (float)hd; s.half_h = 0.5f * s.h;
+  s.lin_damp = (float)exp(0.0 * hd);
+  s.ang_damp = (float)exp(f32d(-0.05) * hd);
+  s.gz = (float)f32d(-9.8);
+  s.friction = 1.0f;
+  s.s_pos = p.solver_scale_pos;
+  s.half_s_ang = 0.5f * p.solver_scale_ang;
+  for (int i = 0; i < POB_NDYN; ++i) s.inv_mass[i] = 1.0f / (float)kMass[i];
+  for (int j = 0; j < POB_NJ; ++j) {
+    const double *J = kJoint[j];
+    for (int c = 0; c < 3; ++c) { s.off_p[j][c] = (float)J[c]; s.off_c[j][c] = (float)J[3 + c]; }
+    double q[4], ex[3] = {1, 0, 0}, ez[3] = {0, 0, 1}, a[3], r[3];
+    d_euler_to_quat(J + 6, q);
+    d_rotate(ex, q, a);
+    d_rotate(ez, q, r);
+    for (int c = 0; c < 3; ++c) { s.axis[j][c] = (float)a[c]; s.ref[j][c] = (float)r[c]; }
+    s.lim_lo[j] = (float)(J[9] * M_PI / 180.0);
+    s.lim_hi[j] = (float)(J[10] * M_PI / 180.0);
+    s.default_angle[j] = (float)((J[9] + J[10]) * M_PI / 360.0);
+    s.jdamp[j] = 20.0f; s.strength[j] = 350.0f;
+  }
+  int g = 0;
+  for (int i = 0; i < POB_NDYN; ++i) {
+    double q[4], ez[3] = {0, 0, 1}, a[3];
+    d_euler_to_quat(kCapsuleRot[i], q);
+    d_rotate(ez, q, a);
+    double r = f32d(kCapsule[i][0]), len = f32d(kCapsule[i][1]);
+    double seg = len / 2 - r;
+    int end = (int)kCapsule[i][2];
+    s.cap_r[i] = (float)r;
+    if ((i == 0) != (seg == 0.0)) return "ant topology: only the torso capsule is a sphere";
+    for (int c = 0; c < 3; ++c) {
+      s.cap_end[i][0][c] = (float)(a[c] * seg);
+      s.cap_end[i][1][c] = (float)(-a[c] * seg);
+    }
+    if (g < POB_NGROUND && kGroundBody[g] == i) {
+      double sg = (end == 0) ? 1.0 : (double)end;
+      for (int c = 0; c < 3; ++c) s.ground_end[g][c] = (float)(a[c] * seg * sg);
+      s.ground_r[g] = (float)r;
+      ++g;
+    }
+  }
+  if (kind == POB_HEAVENHELL) {
+    s.N = 14; s.D = 29 + 6 * 14 + 1;
+    double tx = fmax(p.hh_heaven_hell[0][0], fmax(p.hh_heaven_hell[1][0], p.hh_priest[0])) + 1.0;
+    double ty = fmax(p.hh_heaven_hell[0][1], fmax(p.hh_heaven_hell[1][1], p.hh_priest[1])) + 1.0;
+    const double hw = 2.0, r = 0.5;  // draw_t_maze(hallway_width=2, r=0.5), boxes not halved
+    const double P[8][2] = {{-tx - r, ty + r}, {tx + r, ty + r},      {tx + r, ty - hw - r},
+                            {hw + r, ty - hw - r}, {hw + r, -r},      {-hw - r, -r},
+                            {-hw - r, ty - hw - r}, {-tx - r, ty - hw - r}};
+    for (int i = 0; i < 8; ++i) add_box_wall(s, P[i][0], P[i][1], P[(i + 1) % 8][0], P[(i + 1) % 8][1], 0.5, r);
+    s.frozen_pos[10][0] = p.hh_priest[0]; s.frozen_pos[10][1] = p.hh_priest[1]; s.frozen_pos[10][2] = 1.0f;
+    s.frozen_pos[11][2] = 0.5f; s.frozen_pos[12][2] = 0.5f; s.frozen_pos[13][2] = 0.5f;
+    for (int k = 0; k < 2; ++k) { s.hh_hhp[k][0] = p.hh_heaven_hell[k][0]; s.hh_hhp[k][1] = p.hh_heaven_hell[k][1]; }
+    s.hh_priest[0] = p.hh_priest[0]; s.hh_priest[1] = p.hh_priest[1];
+    s.hh_visible_radius = p.hh_visible_radius; s.hh_dying_cost = p.hh_dying_cost;
+  } else if (kind == POB_GATHER) {
+    const int no = p.ga_n_apples + p.ga_n_bombs;
+    if (p.ga_n_apples < 0 || p.ga_n_bombs < 0 || no < 1 || no > POB_MAXOBJ) return "n_apples + n_bombs must be in [1, 32]";
+    if (p.ga_n_bins < 1 || 2 * p.ga_n_bins > POB_MAXBINS) return "n_bins must be in [1, 16]";
+    s.n_obj = no; s.ga_n_apples = p.ga_n_apples; s.ga_n_bins = p.ga_n_bins;
+    s.N = 11 + no; s.D = 29 + 6 * s.N + 2 * p.ga_n_bins;
+    const double x = p.ga_cage_xy[0] + 1.0, y = p.ga_cage_xy[1] + 1.0, r = 0.5 / 2;
+    const double P[4][2] = {{x + r, y + r}, {x + r, -y - r}, {-x - r, -y - r}, {-x - r, y + r}};
+    for (int i = 0; i < 4; ++i) add_box_wall(s, P[i][0], P[i][1], P[(i + 1) % 4][0], P[(i + 1) % 4][1], 0.5, r);
+    s.frozen_pos[10][2] = 0.5f;
+    for (int i = 0; i < no; ++i) s.frozen_pos[11 + i][2] = 0.25f;
+    static float tmp[3 * 4096];
+    s.n_grid = gather_grid(p, tmp, 4096);
+    if (s.n_grid < no) return "object grid smaller than n_apples + n_bombs";
+    if (s.n_grid > 1625) return "object grid too large (one threefry shuffle round needs n <= 1625)";
+    for (int c = 0; c < 3; ++c) s.ga_waiting[c] = tmp[3 * (s.n_grid - 1) + c] + p.ga_sensor_range * 2.0f;
+    s.ga_catch_range = p.ga_catch_range; s.ga_sensor_range = p.ga_sensor_range;
+    s.ga_half_span = (float)((double)p.ga_sensor_span / 2.0);
+    s.ga_bin_res = (float)((2.0 * ((double)p.ga_sensor_span / 2.0)) / p.ga_n_bins);
+    s.ga_dying_cost = p.ga_dying_cost;
+  } else {
+    s.N = 12; s.D = 29 + 6 * 12 + 2;
+    const double x = p.tag_cage_xy[0] + 1.0, y = p.tag_cage_xy[1] + 1.0, r = 0.5 / 2;
+    const double P[4][2] = {{x + r, y + r}, {x + r, -y - r}, {-x - r, -y - r}, {-x - r, y + r}};
+    for (int i = 0; i < 4; ++i) add_box_wall(s, P[i][0], P[i][1], P[(i + 1) % 4][0], P[(i + 1) % 4][1], 0.5, r);
+    s.frozen_pos[10][2] = 0.5f; s.frozen_pos[11][2] = 0.5f;
+    s.tag_tag_radius = p.tag_tag_radius; s.tag_visible_radius = p.tag_visible_radius;
+    s.tag_target_step = p.tag_target_step; s.tag_min_spawn_distance = p.tag_min_spawn_distance;
+    s.tag_cage_xy[0] = p.tag_cage_xy[0]; s.tag_cage_xy[1] = p.tag_cage_xy[1];
+    s.tag_dying_cost = p.tag_dying_cost;
+  }
+  return nullptr;
+}
+
+}  // namespace pob

@@ -1,0 +1,412 @@
+"""brax-v1-style ``Env`` / ``State`` / ``Wrapper`` surface over the HIP engine.
+
+Mirrors ``brax.envs.env`` [ext] as used by the reference (``po_brax/envs/*.py``):
+``Env.reset(rng) -> State``, ``Env.step(state, action) -> State``, ``State(qp, obs,
+reward, done, metrics, info)`` with ``qp = QP(pos, rot, vel, ang)``.  Tensors are
+torch-ROCm tensors in the reference's batch-major layout (``pos (B, N, 3)`` ...).
+
+Differences from the JAX original (by design):
+* batching is native -- ``reset`` takes keys ``(B, 2)`` (or ``(2,)`` for one env) and every
+  kernel processes the whole batch, so ``VmapWrapper`` is a pass-through;
+* the wrapper chain (ActionRepeat / Episode / AutoReset / RandomizedAutoReset) is folded
+  into flags of ONE fused step kernel instead of being traced by XLA;
+* ``step`` is functional (returns a new State, the input is untouched); ``step_`` updates
+  the state in place (the allocation-free path used by the gym wrappers and the bench).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import torch
+
+from .. import _lib
+from .._lib import lib, check
+
+F_EPISODE, F_AUTORESET, F_ZERO = _lib.F_EPISODE, _lib.F_AUTORESET, _lib.F_ZERO_STEPS_ON_DONE
+
+
+@dataclass
+class QP:
+    """brax.QP: pos (.., N, 3), rot (.., N, 4) wxyz, vel (.., N, 3), ang (.., N, 3)."""
+    pos: torch.Tensor
+    rot: torch.Tensor
+    vel: torch.Tensor
+    ang: torch.Tensor
+
+    def replace(self, **kw) -> "QP":
+        return dataclasses.replace(self, **kw)
+
+
+@dataclass
+class State:
+    """brax.envs.env.State."""
+    qp: QP
+    obs: torch.Tensor
+    reward: torch.Tensor
+    done: torch.Tensor
+    metrics: Dict[str, torch.Tensor] = field(default_factory=dict)
+    info: Dict[str, Any] = field(default_factory=dict)
+    # engine-side float32 buffers (done, hidden metrics) -- not part of the brax pytree
+    aux: Dict[str, torch.Tensor] = field(default_factory=dict, repr=False, compare=False)
+
+    def replace(self, **kw) -> "State":
+        return dataclasses.replace(self, **kw)
+
+
+class Env:
+    """API of a brax environment (brax.envs.env.Env [ext])."""
+
+    def reset(self, rng: torch.Tensor) -> State:
+        raise NotImplementedError
+
+    def step(self, state: State, action: torch.Tensor) -> State:
+        raise NotImplementedError
+
+    @property
+    def observation_size(self) -> int:
+        return self.unwrapped._D
+
+    @property
+    def action_size(self) -> int:
+        return self.unwrapped._A
+
+    @property
+    def unwrapped(self) -> "Env":
+        return self
+
+    # fused-chain hooks (overridden by wrappers)
+    def _chain_reset(self, rng, episode: bool, first: bool) -> State:
+        return self.unwrapped._reset_impl(rng, episode, first)
+
+    def _chain_step(self, state, action, flags: int, episode_length: int, inplace: bool) -> State:
+        return self.unwrapped._step_impl(state, action, flags, episode_length, inplace)
+
+    def step_(self, state: State, action: torch.Tensor) -> State:
+        """In-place step (state's buffers are overwritten and returned)."""
+        return self._chain_step(state, action, 0, 0, True)
+
+
+class Wrapper(Env):
+    """brax.envs.env.Wrapper: delegates everything to the wrapped env."""
+
+    def __init__(self, env: Env):
+        self.env = env
+
+    def reset(self, rng):
+        return self._chain_reset(rng, False, False)
+
+    def step(self, state, action):
+        return self._chain_step(state, action, 0, 0, False)
+
+    def step_(self, state, action):
+        return self._chain_step(state, action, 0, 0, True)
+
+    def _chain_reset(self, rng, episode, first):
+        return self.env._chain_reset(rng, episode, first)
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        return self.env._chain_step(state, action, flags, episode_length, inplace)
+
+    @property
+    def observation_size(self):
+        return self.env.observation_size
+
+    @property
+    def action_size(self):
+        return self.env.action_size
+
+    @property
+    def unwrapped(self):
+        return self.env.unwrapped
+
+    def __getattr__(self, name):
+        if name == "__setstate__" or name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
+
+# ----------------------------------------------------------------------- brax.System
+@dataclass
+class _Config:
+    dt: float
+    substeps: int
+
+
+class _BodyIndex:
+    def __init__(self, names):
+        self.index = {n: i for i, n in enumerate(names)}
+
+
+class System:
+    """The parts of brax.System the reference envs and wrappers touch.
+
+    ``config.dt`` / ``config.substeps`` (read by VmapGymWrapper wrappers.py:133-135 and
+    written by ActionRepeatWrapper wrappers.py:21-23), ``body.index`` (ant_*.py __init__),
+    ``num_bodies`` / ``num_joint_dof`` / ``num_actuators``, ``default_angle()`` and
+    ``default_qp(joint_angle, joint_velocity)`` (the latter runs the FK kernel).
+    """
+
+    def __init__(self, env: "PoBraxEnv", body_names):
+        self._env = env
+        self.config = _Config(dt=0.05 * env._action_repeat, substeps=10 * env._action_repeat)
+        self.body = _BodyIndex(body_names)
+        self.num_bodies = len(body_names)
+        self.num_joint_dof = 8
+        self.num_actuators = 8
+
+    def default_angle(self) -> torch.Tensor:
+        out = (C.c_float * 8)()
+        check(lib.pob_env_default_angle(self._env._handle, out))
+        return torch.tensor(list(out), dtype=torch.float32, device=self._env.device)
+
+    def default_qp(self, joint_angle=None, joint_velocity=None) -> QP:
+        e = self._env
+        qpos = self.default_angle() if joint_angle is None else torch.as_tensor(joint_angle)
+        qpos = qpos.to(e.device, torch.float32)
+        qvel = torch.zeros_like(qpos) if joint_velocity is None else torch.as_tensor(joint_velocity)
+        qvel = qvel.to(e.device, torch.float32)
+        squeeze = qpos.ndim == 1
+        qpos, qvel = qpos.reshape(-1, 8).contiguous(), qvel.reshape(-1, 8).contiguous()
+        B, N = qpos.shape[0], e._N
+        out = [torch.empty((B, N, k), dtype=torch.float32, device=e.device) for k in (3, 4, 3, 3)]
+        check(lib.pob_default_qp(e._handle, B, qpos.data_ptr(), qvel.data_ptr(),
+                                 *[o.data_ptr() for o in out], _lib.stream_handle(e.device)))
+        if squeeze:
+            out = [o[0] for o in out]
+        return QP(*out)
+
+
+# ------------------------------------------------------------------- the engine env
+class PoBraxEnv(Env):
+    """Base of AntHeavenHellEnv / AntGatherEnv / AntTagEnv (one libpob env handle)."""
+
+    kind: str = ""
+    body_names: tuple = ()
+    slot_names: tuple = ()       # metric stored in engine slot m0, m1, m2
+    reset_metrics: tuple = ()    # metric keys after reset (reference order)
+    step_metrics: tuple = ()     # metric keys after step
+    done_dtype = torch.float32
+
+    def __init__(self, device=None, **params):
+        self.device = torch.device(device if device is not None else "cuda")
+        self._params = _lib.pob_params()
+        check(lib.pob_default_params(C.byref(self._params)))
+        self._set_params(params)
+        self._action_repeat = 1
+        self._handle = None
+        self._create()
+        self.sys = System(self, self._body_names())
+
+    # subclasses map constructor kwargs onto pob_params
+    def _set_params(self, params: dict) -> None:
+        raise NotImplementedError
+
+    def _body_names(self):
+        return list(self.body_names)
+
+    def _create(self):
+        if self._handle is not None:
+            lib.pob_env_destroy(self._handle)
+            self._handle = None
+        self._params.action_repeat = self._action_repeat
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.pob_env_create(_lib.KINDS[self.kind], C.byref(self._params), C.byref(h)))
+        self._handle = h
+        n, d, a = C.c_int(), C.c_int(), C.c_int()
+        check(lib.pob_env_dims(self._handle, C.byref(n), C.byref(d), C.byref(a)))
+        self._N, self._D, self._A = n.value, d.value, a.value
+
+    def _set_action_repeat(self, action_repeat: int) -> None:
+        """ActionRepeatWrapper (wrappers.py:16-24): dt and substeps scale by action_repeat."""
+        self._action_repeat *= int(action_repeat)
+        self._create()
+        self.sys.config.dt = 0.05 * self._action_repeat
+        self.sys.config.substeps = 10 * self._action_repeat
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None:
+            try:
+                lib.pob_env_destroy(h)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ buffers
+    def _empty(self, B: int, episode: bool, first: bool) -> dict:
+        f = dict(dtype=torch.float32, device=self.device)
+        N, D = self._N, self._D
+        b = dict(pos=torch.empty((B, N, 3), **f), rot=torch.empty((B, N, 4), **f),
+                 vel=torch.empty((B, N, 3), **f), ang=torch.empty((B, N, 3), **f),
+                 obs=torch.empty((B, D), **f), reward=torch.empty((B,), **f),
+                 done=torch.empty((B,), **f), m0=torch.empty((B,), **f), m1=torch.empty((B,), **f),
+                 m2=torch.empty((B,), **f),
+                 rng=torch.empty((B, 2), dtype=torch.uint32, device=self.device))
+        if episode:
+            b["steps"] = torch.empty((B,), **f)
+            b["truncation"] = torch.empty((B,), **f)
+        if first:
+            b.update(first_pos=torch.empty((B, N, 3), **f), first_rot=torch.empty((B, N, 4), **f),
+                     first_vel=torch.empty((B, N, 3), **f), first_ang=torch.empty((B, N, 3), **f),
+                     first_obs=torch.empty((B, D), **f))
+        return b
+
+    @staticmethod
+    def _cstate(b: dict) -> _lib.pob_state:
+        s = _lib.pob_state()
+        for name, _ in _lib.pob_state._fields_:
+            t = b.get(name)
+            if t is not None:
+                setattr(s, name, t.data_ptr())
+        return s
+
+    def _bufs_of(self, state: State) -> dict:
+        """Engine buffers of a State (reusing its float32 aux buffers when present)."""
+        a = state.aux
+        b = dict(pos=state.qp.pos, rot=state.qp.rot, vel=state.qp.vel, ang=state.qp.ang,
+                 obs=state.obs, reward=state.reward,
+                 done=a.get("done", state.done.to(torch.float32)),
+                 rng=state.info["rng"])
+        for k in range(3):
+            name = self.slot_names[k] if k < len(self.slot_names) else None
+            t = a.get(f"m{k}")
+            if t is None and name in state.metrics:
+                t = state.metrics[name].to(torch.float32).contiguous()
+            b[f"m{k}"] = t
+        if "steps" in state.info:
+            b["steps"] = state.info["steps"]
+            b["truncation"] = a.get("truncation", state.info["truncation"].to(torch.float32))
+        if "first_qp" in state.info:
+            fq = state.info["first_qp"]
+            b.update(first_pos=fq.pos, first_rot=fq.rot, first_vel=fq.vel, first_ang=fq.ang,
+                     first_obs=state.info["first_obs"])
+        if "any_done" in a:
+            b["any_done"] = a["any_done"]
+        for k, t in b.items():
+            if t is not None and not t.is_contiguous():
+                raise ValueError(f"state tensor {k} must be contiguous")
+        return b
+
+    def _state_of(self, b: dict, after_step: bool, squeeze: bool) -> State:
+        names = self.step_metrics if after_step else self.reset_metrics
+        metrics = {name: b[f"m{self.slot_names.index(name)}"] for name in names}
+        metrics = self._metric_dtypes(metrics, after_step)
+        done = b["done"]
+        if after_step and self.done_dtype is not torch.float32:
+            done = done != 0
+        info = {"rng": b["rng"]}
+        aux = {"done": b["done"]}
+        for k in range(3):
+            aux[f"m{k}"] = b[f"m{k}"]
+        if "steps" in b:
+            info["steps"] = b["steps"]
+            trunc = b["truncation"]
+            aux["truncation"] = trunc
+            if after_step and self.done_dtype is not torch.float32:
+                trunc = trunc.to(torch.int32)  # 1 - bool -> int32 in EpisodeWrapper
+            info["truncation"] = trunc
+        if "first_pos" in b:
+            info["first_qp"] = QP(b["first_pos"], b["first_rot"], b["first_vel"], b["first_ang"])
+            info["first_obs"] = b["first_obs"]
+        st = State(QP(b["pos"], b["rot"], b["vel"], b["ang"]), b["obs"], b["reward"], done,
+                   metrics, info, aux)
+        if squeeze:
+            st = _squeeze_state(st)
+        return st
+
+    def _metric_dtypes(self, metrics, after_step):
+        return metrics
+
+    # ------------------------------------------------------------------ API
+    def reset(self, rng) -> State:
+        return self._reset_impl(rng, False, False)
+
+    def step(self, state: State, action) -> State:
+        return self._step_impl(state, action, 0, 0, False)
+
+    def _keys(self, rng) -> tuple:
+        rng = as_key(rng).to(self.device).contiguous()
+        squeeze = rng.ndim == 1
+        rng = rng.reshape(-1, 2).contiguous()
+        return rng, squeeze
+
+    def _reset_impl(self, rng, episode: bool, first: bool) -> State:
+        keys, squeeze = self._keys(rng)
+        B = keys.shape[0]
+        b = self._empty(B, episode, first)
+        cs = self._cstate(b)
+        check(lib.pob_reset(self._handle, B, keys.data_ptr(), C.byref(cs),
+                            _lib.stream_handle(self.device)))
+        return self._state_of(b, False, squeeze)
+
+    def _step_impl(self, state: State, action, flags: int, episode_length: int, inplace: bool) -> State:
+        squeeze = state.obs.ndim == 1
+        if squeeze:
+            state = _unsqueeze_state(state)
+        act = torch.as_tensor(action, device=self.device)
+        if act.dtype != torch.float32:
+            act = act.to(torch.float32)
+        act = act.reshape(-1, self._A).contiguous()
+        bin_ = self._bufs_of(state)
+        B = bin_["pos"].shape[0]
+        if act.shape[0] != B:
+            raise ValueError(f"action batch {act.shape[0]} != state batch {B}")
+        if (flags & F_EPISODE) and "steps" not in bin_:
+            raise ValueError("EpisodeWrapper.step needs a state from EpisodeWrapper.reset")
+        if (flags & F_AUTORESET) and "first_pos" not in bin_:
+            raise ValueError("AutoResetWrapper.step needs a state from AutoResetWrapper.reset")
+        if inplace:
+            bout = bin_
+            for k in ("m0", "m1", "m2"):
+                if bout.get(k) is None:
+                    bout[k] = torch.empty((B,), dtype=torch.float32, device=self.device)
+        else:
+            bout = self._empty(B, "steps" in bin_, False)
+            if "first_pos" in bin_:  # immutable: shared, not copied
+                for k in ("first_pos", "first_rot", "first_vel", "first_ang", "first_obs"):
+                    bout[k] = bin_[k]
+        ci, co = self._cstate(bin_), self._cstate(bout)
+        check(lib.pob_step(self._handle, B, C.byref(ci), act.data_ptr(), C.byref(co), flags,
+                           int(episode_length), _lib.stream_handle(self.device)))
+        return self._state_of(bout, True, squeeze)
+
+    # helpers for the gym / randomized-autoreset wrappers
+    def _reset_where_done(self, state: State, mode: int, gym_in=None, gym_out=None) -> None:
+        b = self._bufs_of(state)
+        cs = self._cstate(b)
+        check(lib.pob_reset_where_done(self._handle, b["pos"].shape[0], mode, _lib.ptr(gym_in),
+                                       _lib.ptr(gym_out), C.byref(cs), _lib.stream_handle(self.device)))
+
+
+def as_key(rng) -> torch.Tensor:
+    """Keys as a uint32 tensor (accepts uint32 tensors, numpy arrays and int sequences)."""
+    if isinstance(rng, torch.Tensor) and rng.dtype == torch.uint32:
+        return rng
+    if isinstance(rng, torch.Tensor):
+        rng = rng.detach().cpu().numpy()
+    import numpy as np
+    arr = np.asarray(rng)
+    if arr.dtype.kind == "f":
+        raise TypeError("PRNG keys must be integers (uint32 pairs)")
+    return torch.from_numpy(np.ascontiguousarray(arr.astype(np.uint64).astype(np.uint32)))
+
+
+def _squeeze_state(s: State) -> State:
+    sq = lambda t: t[0] if isinstance(t, torch.Tensor) else t  # noqa: E731
+    qp = QP(sq(s.qp.pos), sq(s.qp.rot), sq(s.qp.vel), sq(s.qp.ang))
+    info = {k: (QP(*(sq(x) for x in (v.pos, v.rot, v.vel, v.ang))) if isinstance(v, QP) else sq(v))
+            for k, v in s.info.items()}
+    return State(qp, sq(s.obs), sq(s.reward), sq(s.done), {k: sq(v) for k, v in s.metrics.items()}, info,
+                 {k: v for k, v in s.aux.items()})
+
+
+def _unsqueeze_state(s: State) -> State:
+    us = lambda t: t.unsqueeze(0) if isinstance(t, torch.Tensor) else t  # noqa: E731
+    qp = QP(us(s.qp.pos), us(s.qp.rot), us(s.qp.vel), us(s.qp.ang))
+    info = {k: (QP(*(us(x) for x in (v.pos, v.rot, v.vel, v.ang))) if isinstance(v, QP) else us(v))
+            for k, v in s.info.items()}
+    return State(qp, us(s.obs), us(s.reward), us(s.done), {k: us(v) for k, v in s.metrics.items()}, info,
+                 {k: v for k, v in s.aux.items()})

@@ -1,0 +1,349 @@
+"""Wrappers of ``po_brax/envs/wrappers.py`` and the brax wrappers it builds on.
+
+The wrapper objects do not run anything themselves: they fold into flags of the one fused
+step kernel (``pob_step``) and into the masked reset kernel (``pob_reset_where_done``), so a
+wrapped step is still ONE device launch (two for the autoresetting gym/randomized
+wrappers) and never synchronises the host:
+
+==========================================  =============================================
+reference                                    here
+==========================================  =============================================
+ActionRepeatWrapper  wrappers.py:16-24       rebuilds the engine with dt, substeps x ar
+brax EpisodeWrapper [ext]                     POB_F_EPISODE (steps, truncation, time limit)
+brax VmapWrapper [ext] / VectorWrapper :13    pass-through (batching is native)
+brax AutoResetWrapper [ext] / alias :27       POB_F_AUTORESET (first_qp / first_obs)
+RandomizedAutoResetWrapperNaive :30-52        POB_F_ZERO_STEPS_ON_DONE + reset(info.rng)
+RandomizedAutoResetWrapperOnTerminal :55-80   same outputs as Naive (cond only skips work)
+RandomizedAutoResetWrapperCached :83-123      host step counter refreshes first_qp/obs
+VmapGymWrapper :126-172                       gym VectorEnv API over device tensors
+AutoresetVmapGymWrapper :240-262              device-side any(done) + gym-key reset
+AutoresetGymWrapper :232-237                  single env, full reset on done
+EvalGymWrapper :175-229                       device-side episode statistics
+brax EvalWrapper [ext]                        device-side episode metrics
+==========================================  =============================================
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from .. import jumpy as jp
+from .env import Env, State, Wrapper, QP, F_EPISODE, F_AUTORESET, F_ZERO
+
+
+class ActionRepeatWrapper(Wrapper):
+    """Just change action duration (wrappers.py:16-24): dt and substeps x action_repeat."""
+
+    def __init__(self, env: Env, action_repeat: int):
+        super().__init__(env)
+        if hasattr(self.unwrapped, "_set_action_repeat"):
+            self.unwrapped._set_action_repeat(action_repeat)
+        self.action_repeat = action_repeat
+
+
+class EpisodeWrapper(Wrapper):
+    """brax EpisodeWrapper: info['steps'] += 1, done at episode_length, info['truncation']."""
+
+    def __init__(self, env: Env, episode_length: int, action_repeat: int = 1):
+        super().__init__(env)
+        if action_repeat != 1:
+            raise NotImplementedError("EpisodeWrapper(action_repeat != 1): use ActionRepeatWrapper "
+                                      "(po_brax.envs.create passes 1, __init__.py:62)")
+        if episode_length <= 0:
+            raise ValueError("episode_length must be positive")
+        self.episode_length = int(episode_length)
+        self.action_repeat = action_repeat
+
+    def _chain_reset(self, rng, episode, first):
+        return self.env._chain_reset(rng, True, first)
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        if flags & F_EPISODE:
+            raise NotImplementedError("nested EpisodeWrapper")
+        return self.env._chain_step(state, action, flags | F_EPISODE, self.episode_length, inplace)
+
+
+class VmapWrapper(Wrapper):
+    """brax VmapWrapper: batching is native to the engine -- a pass-through."""
+
+
+VectorWrapper = VmapWrapper  # wrappers.py:13
+
+
+class AutoResetWrapper(Wrapper):
+    """brax AutoResetWrapper: reset done envs to info['first_qp'] / info['first_obs']."""
+
+    def _chain_reset(self, rng, episode, first):
+        return self.env._chain_reset(rng, episode, True)
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        if flags & F_EPISODE:
+            raise NotImplementedError("EpisodeWrapper outside AutoResetWrapper is not supported")
+        return self.env._chain_step(state, action, flags | F_AUTORESET, episode_length, inplace)
+
+
+class RandomizedAutoResetWrapperNaive(Wrapper):
+    """wrappers.py:30-52: re-sample ``reset(state.info['rng'])`` for envs that are done."""
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        if flags & F_EPISODE:
+            raise NotImplementedError("EpisodeWrapper outside the autoreset wrapper is not supported")
+        s = self.env._chain_step(state, action, flags | F_ZERO, episode_length, inplace)
+        self.unwrapped._reset_where_done(s, _lib.RESET_OWN)
+        return s
+
+
+class RandomizedAutoResetWrapperOnTerminal(RandomizedAutoResetWrapperNaive):
+    """wrappers.py:55-80: identical outputs (the cond only skips work when nothing is done;
+    the masked reset kernel skips every env that is not done anyway)."""
+
+
+class RandomizedAutoResetWrapperCached(Wrapper):
+    """wrappers.py:83-123: first_qp / first_obs refreshed from reset(split(rng)[1]) every
+    ``n_steps_between_updates`` calls of ``step`` (a host-side counter, as in the reference)."""
+
+    def __init__(self, env: Env, n_steps_between_updates: int = 200):
+        super().__init__(env)
+        self.n_steps_between_updates = n_steps_between_updates
+        self.steps = 0
+
+    def _chain_reset(self, rng, episode, first):
+        return self.env._chain_reset(rng, episode, True)
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        if flags & F_EPISODE:
+            raise NotImplementedError("EpisodeWrapper outside the autoreset wrapper is not supported")
+        self.steps += 1
+        if self.steps % self.n_steps_between_updates == 0:
+            rng = state.info["rng"]
+            ks = jp.random_split_batch(rng, 2)  # (B, 2, 2)
+            fresh = self.env._chain_reset(ks[:, 1].contiguous(), False, False)
+            fq = state.info["first_qp"]
+            for dst, src in ((fq.pos, fresh.qp.pos), (fq.rot, fresh.qp.rot), (fq.vel, fresh.qp.vel),
+                             (fq.ang, fresh.qp.ang), (state.info["first_obs"], fresh.obs)):
+                dst.copy_(src)
+            rng.copy_(ks[:, 0])
+        return self.env._chain_step(state, action, flags | F_AUTORESET, episode_length, inplace)
+
+
+class EvalWrapper(Wrapper):
+    """brax EvalWrapper: per-env running episode metrics and completed-episode totals."""
+
+    def _chain_reset(self, rng, episode, first):
+        s = self.env._chain_reset(rng, episode, first)
+        s.metrics["reward"] = s.reward
+        cur = {k: torch.zeros_like(v, dtype=torch.float32) for k, v in s.metrics.items()}
+        s.info["eval_metrics"] = {
+            "current_episode_metrics": cur,
+            "completed_episodes_metrics": {k: torch.zeros((), device=v.device) for k, v in cur.items()},
+            "completed_episodes": torch.zeros((), device=s.reward.device),
+            "completed_episodes_steps": torch.zeros((), device=s.reward.device),
+        }
+        return s
+
+    def _chain_step(self, state, action, flags, episode_length, inplace):
+        em = state.info.pop("eval_metrics")
+        ns = self.env._chain_step(state, action, flags, episode_length, inplace)
+        state.info["eval_metrics"] = em
+        ns.metrics["reward"] = ns.reward
+        done = ns.aux["done"] if "done" in ns.aux else ns.done.to(torch.float32)
+        cur = {k: em["current_episode_metrics"][k] + ns.metrics[k].to(torch.float32)
+               for k in em["current_episode_metrics"] if k in ns.metrics}
+        comp = {k: em["completed_episodes_metrics"][k] + (cur[k] * done).sum() for k in cur}
+        steps = ns.info.get("steps")
+        nem = {
+            "current_episode_metrics": {k: v * (1.0 - done) for k, v in cur.items()},
+            "completed_episodes_metrics": comp,
+            "completed_episodes": em["completed_episodes"] + done.sum(),
+            "completed_episodes_steps": em["completed_episodes_steps"]
+            + ((steps * done).sum() if steps is not None else 0.0),
+        }
+        ns.info["eval_metrics"] = nem
+        return ns
+
+
+# --------------------------------------------------------------------------- gym side
+class Box:
+    """Minimal gym.spaces.Box (gym is not a dependency of the engine)."""
+
+    def __init__(self, low, high, shape=None, dtype="float32", device="cpu"):
+        self.low, self.high = np.asarray(low, dtype=dtype), np.asarray(high, dtype=dtype)
+        self.shape = tuple(shape if shape is not None else self.low.shape)
+        self.dtype = np.dtype(dtype)
+        self._device = device
+        self._gen = torch.Generator(device="cpu").manual_seed(0)
+
+    def sample(self) -> torch.Tensor:
+        lo, hi = torch.as_tensor(self.low), torch.as_tensor(self.high)
+        u = torch.rand(self.shape, generator=self._gen, dtype=torch.float32)
+        lo = torch.where(torch.isfinite(lo), lo, torch.full_like(lo, -1.0))
+        hi = torch.where(torch.isfinite(hi), hi, torch.full_like(hi, 1.0))
+        return (lo + u * (hi - lo)).to(self._device)
+
+    def __repr__(self):
+        return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+
+class VmapGymWrapper:
+    """wrappers.py:126-172: gym VectorEnv API for a batched env (device tensors in/out)."""
+
+    def __init__(self, env: Env, batch_size: int, seed: int = 0, backend: Optional[str] = None):
+        self._env = env
+        self.metadata = {"render.modes": ["human", "rgb_array"],
+                         "video.frames_per_second": 1 / self._env.sys.config.dt}
+        self.num_envs = int(batch_size)
+        self.backend = backend
+        self.device = env.unwrapped.device
+        self._state = None
+        self.seed(seed)
+        D, A = self._env.observation_size, self._env.action_size
+        self.single_observation_space = Box(-np.inf * np.ones(D), np.inf * np.ones(D), device=self.device)
+        self.observation_space = Box(-np.inf * np.ones((self.num_envs, D)), np.inf * np.ones((self.num_envs, D)),
+                                     device=self.device)
+        self.single_action_space = Box(-np.ones(A), np.ones(A), device=self.device)
+        self.action_space = Box(-np.ones((self.num_envs, A)), np.ones((self.num_envs, A)), device=self.device)
+
+    def seed(self, seed: int = 0):
+        self._key = jp.random_prngkey(seed, device=self.device)
+
+    def _reset(self, key):
+        keys = jp.random_split(key, self.num_envs + 1)
+        state = self._env._chain_reset(keys[1:].contiguous(), False, False)
+        return state, state.obs, keys[0].contiguous()
+
+    def reset(self):
+        self._state, obs, self._key = self._reset(self._key)
+        return obs
+
+    def step(self, action):
+        self._state = self._env._chain_step(self._state, action, 0, 0, True)
+        s = self._state
+        return s.obs, s.reward, s.done, s.metrics
+
+    def render(self, mode="human"):
+        raise NotImplementedError("rendering is out of scope for the accelerated path")
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self._env, name)
+
+
+class AutoresetVmapGymWrapper(VmapGymWrapper):
+    """wrappers.py:240-262, with the ``if done.any()`` decided on the device: the step
+    kernel ORs into an any-done word, the masked reset kernel re-samples the done envs from
+    ``split(gym_key, B+1)[1:]`` and advances the gym key only when something was done."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self._any = torch.zeros(4, dtype=torch.uint32, device=self.device)
+        self._key2 = torch.empty(2, dtype=torch.uint32, device=self.device)
+
+    def step(self, action):
+        s = self._state
+        self._any.zero_()
+        s.aux["any_done"] = self._any
+        self._state = s = self._env._chain_step(s, action, 0, 0, True)
+        s.aux["any_done"] = self._any
+        self._env.unwrapped._reset_where_done(s, _lib.RESET_GYM, self._key, self._key2)
+        self._key, self._key2 = self._key2, self._key
+        return s.obs, s.reward, s.done, s.metrics
+
+
+class AutoresetGymWrapper:
+    """wrappers.py:232-237 (brax GymWrapper for one env): full reset when done."""
+
+    def __init__(self, env: Env, seed: int = 0, backend: Optional[str] = None):
+        self._env = env
+        self.device = env.unwrapped.device
+        self.metadata = {"render.modes": ["human", "rgb_array"],
+                         "video.frames_per_second": 1 / env.sys.config.dt}
+        self.backend = backend
+        self._state = None
+        D, A = env.observation_size, env.action_size
+        self.observation_space = Box(-np.inf * np.ones(D), np.inf * np.ones(D), device=self.device)
+        self.action_space = Box(-np.ones(A), np.ones(A), device=self.device)
+        self.seed(seed)
+
+    def seed(self, seed: int = 0):
+        self._key = jp.random_prngkey(seed, device=self.device)
+
+    def _reset(self, key):
+        k = jp.random_split(key, 2)
+        state = self._env._chain_reset(k[1].contiguous(), False, False)
+        return state, state.obs, k[0].contiguous()
+
+    def reset(self):
+        self._state, obs, self._key = self._reset(self._key)
+        return obs
+
+    def step(self, action):
+        self._state = self._env._chain_step(self._state, action, 0, 0, False)
+        s = self._state
+        obs, reward, done, info = s.obs, s.reward, s.done, s.metrics
+        if bool(done):  # host sync, as the reference's `if done:`
+            self._state, obs, self._key = self._reset(self._key)
+        return obs, reward, done, info
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self._env, name)
+
+
+class EvalGymWrapper:
+    """wrappers.py:175-229: episode return / discounted return / length statistics, kept as
+    device-side sums (no per-step host sync); ``get_stats`` = nanmean over completed
+    episodes, as the reference's queues seeded with NaN."""
+
+    def __init__(self, env, discount: float = 1.0):
+        self.env = env
+        self._discount = float(discount)
+        self.num_envs = getattr(env, "num_envs", 1)
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
+    def reset(self, **kwargs):
+        o = self.env.reset(**kwargs)
+        like = torch.atleast_1d(o[..., -1])
+        dev = like.device
+        self.episode_returns = torch.zeros_like(like, dtype=torch.float32)
+        self.discounted_episode_returns = torch.zeros_like(like, dtype=torch.float32)
+        self.episode_lengths = torch.zeros_like(like, dtype=torch.int64)
+        self.current_discount = torch.ones_like(like, dtype=torch.float32)
+        self._sum = torch.zeros(3, dtype=torch.float64, device=dev)   # return, disc. return, length
+        self._count = torch.zeros((), dtype=torch.float64, device=dev)
+        return o
+
+    def step(self, action):
+        o, r, d, info = self.env.step(action)
+        r = torch.atleast_1d(r).to(torch.float32)
+        df = torch.atleast_1d(d).to(torch.float32)
+        self.episode_returns += r
+        self.episode_lengths += 1
+        self.discounted_episode_returns += r * self.current_discount
+        self.current_discount *= self._discount
+        self._sum[0] += (self.episode_returns * df).sum().double()
+        self._sum[1] += (self.discounted_episode_returns * df).sum().double()
+        self._sum[2] += (self.episode_lengths.to(torch.float32) * df).sum().double()
+        self._count += df.sum().double()
+        keep = 1.0 - df
+        self.episode_returns *= keep
+        self.discounted_episode_returns *= keep
+        self.episode_lengths *= keep.to(torch.int64)
+        self.current_discount = self.current_discount * keep + df
+        return o, r, d, info
+
+    def get_stats(self):
+        c = float(self._count)
+        mean = (self._sum / self._count).cpu().numpy() if c > 0 else np.full(3, math.nan)
+        return {"charts/mean_episodic_return": np.array(mean[0]),
+                "charts/mean_discounted_episodic_return": np.array(mean[1]),
+                "charts/mean_episodic_length": np.array(mean[2])}

@@ -1,0 +1,304 @@
+"""GPU parity: the HIP kernels (through libpob.so's C ABI) vs the CPU oracle.
+
+Bar (BASELINE.json north star): bit-exact on integer / key / done / goal / pickup fields,
+within 1e-5 relative on float qp state.  The engine and the oracle follow the same op
+order with IEEE float32 arithmetic, so most float fields are expected bit-exact too; the
+float comparison below uses the stated tolerance and the exactness is reported.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import orc
+import pob_np as P
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+NAMES = ["ant_heavenhell", "ant_gather", "ant_tag"]
+RTOL, ATOL = 1e-5, 1e-6
+
+
+def _np(t):
+    t = t.detach().cpu()
+    if t.dtype == torch.bool:
+        t = t.to(torch.float32)
+    return t.numpy()
+
+
+def close(a, b, what, rtol=RTOL, atol=ATOL):
+    a = _np(a) if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    np.testing.assert_allclose(a.astype(np.float64), b.astype(np.float64), rtol=rtol, atol=atol, err_msg=what)
+    return bool(np.array_equal(a.astype(np.float32), b.astype(np.float32)))
+
+
+def _envs():
+    from po_brax_amd import envs
+    return envs
+
+
+def _keys(B, seed=0):
+    return P.split(P.prngkey(seed), B + 1)[1:]
+
+
+def _state_np(s):
+    """GPU State -> oracle state dict (reference layout)."""
+    d = dict(pos=_np(s.qp.pos), rot=_np(s.qp.rot), vel=_np(s.qp.vel), ang=_np(s.qp.ang), obs=_np(s.obs),
+             reward=_np(s.reward), done=_np(s.aux["done"]), rng=_np(s.info["rng"]).astype(np.uint32))
+    for k in range(3):
+        d[f"m{k}"] = _np(s.aux[f"m{k}"])
+    if "steps" in s.info:
+        d["steps"] = _np(s.info["steps"])
+        d["truncation"] = _np(s.aux["truncation"])
+    else:
+        d["steps"] = np.zeros_like(d["reward"]); d["truncation"] = np.zeros_like(d["reward"])
+    if "first_qp" in s.info:
+        fq = s.info["first_qp"]
+        d.update(first_pos=_np(fq.pos), first_rot=_np(fq.rot), first_vel=_np(fq.vel), first_ang=_np(fq.ang),
+                 first_obs=_np(s.info["first_obs"]))
+    return {k: np.ascontiguousarray(v) for k, v in d.items()}
+
+
+def compare_states(g, o, what, exact_report=None):
+    gs = _state_np(g)
+    exact = True
+    for k in ("pos", "rot", "vel", "ang", "obs", "reward", "m0", "m1", "m2", "steps", "truncation"):
+        exact &= close(gs[k], o[k], f"{what}: {k}")
+    np.testing.assert_array_equal(gs["done"], o["done"], err_msg=f"{what}: done")
+    np.testing.assert_array_equal(gs["rng"], o["rng"], err_msg=f"{what}: rng")
+    if exact_report is not None:
+        exact_report.append((what, exact))
+    return exact
+
+
+# ------------------------------------------------------------------------ RNG kernels
+def test_threefry_kernels_match_kats():
+    from po_brax_amd import jumpy
+    kat = json.load(open(os.path.join(HERE, "golden", "threefry_kat.json")))
+    assert _np(jumpy.random_split(jumpy.random_prngkey(0))).tolist() == kat["public"]["split_PRNGKey0"]
+    assert _np(jumpy.random_split(jumpy.random_prngkey(42))).tolist() == kat["public"]["split_PRNGKey42"]
+    assert _np(jumpy.random_split(jumpy.random_prngkey(7), 65)).tolist() == kat["restated"]["split_PRNGKey7_65"]
+    u = jumpy.random_uniform(jumpy.random_prngkey(0), (8,), -0.1, 0.1)
+    np.testing.assert_array_equal(_np(u), np.array(kat["restated"]["uniform_PRNGKey0_8"], np.float32))
+    u = jumpy.random_uniform(jumpy.random_prngkey(3), (7,), -1.0, 1.0)
+    np.testing.assert_array_equal(_np(u), np.array(kat["restated"]["uniform_PRNGKey3_7"], np.float32))
+
+
+def test_sharded_actions_and_keys():
+    from po_brax_amd import jumpy
+    from po_brax_amd.sharding import shard_keys, shard_range
+    total, world = 1000, 3
+    key = jumpy.random_prngkey(5)
+    full = P.split(P.prngkey(5), total + 1)[1:]
+    for r in range(world):
+        lo, hi = shard_range(total, world, r)
+        np.testing.assert_array_equal(_np(shard_keys(key, total, world, r)), full[lo:hi])
+    k = jumpy.random_prngkey(11)
+    kn = P.prngkey(11)
+    for step in range(3):
+        kn, sub = P.split(kn)
+        ref = P.uniform(sub, (total, 8), -1, 1)
+        for r in range(world):
+            lo, hi = shard_range(total, world, r)
+            kk = k.clone()
+            act = torch.empty((hi - lo, 8), dtype=torch.float32, device="cuda")
+            jumpy.random_actions_(kk, total, lo, act)
+            np.testing.assert_array_equal(_np(act), ref[lo:hi])
+        jumpy.random_actions_(k, total, 0, torch.empty((total, 8), device="cuda"))
+        np.testing.assert_array_equal(_np(k), kn)
+
+
+# -------------------------------------------------------------------------- kinematics
+def test_default_qp_reproduces_notebook_frame0():
+    traj = json.load(open(os.path.join(HERE, "golden", "ant_tag_notebook_trajectory.json")))
+    ks = P.np_split(P.np_prngkey(0), 2)
+    ant_xy = P.np_uniform(ks[1], (2,), -4.5, 4.5)
+    qpos = (P.default_angle() + P.np_uniform(ks[1], (8,), -.1, .1)).astype(np.float32)
+    env = _envs().AntTagEnv()
+    qp = env.sys.default_qp(torch.from_numpy(qpos), torch.zeros(8))
+    pos = _np(qp.pos).astype(np.float64)
+    pos[:9, :2] += ant_xy
+    np.testing.assert_allclose(pos[:9], np.array(traj["pos"][0])[:9], atol=3e-6, rtol=0)
+    np.testing.assert_allclose(_np(qp.rot)[:9], np.array(traj["rot"][0])[:9], atol=3e-6, rtol=0)
+    o = orc.OracleEnv("ant_tag")
+    opos, orot, ovel, oang = o.default_qp(qpos, np.zeros(8, np.float32))
+    np.testing.assert_array_equal(_np(qp.pos), opos)
+    np.testing.assert_array_equal(_np(qp.rot), orot)
+
+
+# ------------------------------------------------------------------------------ reset
+@pytest.mark.parametrize("name", NAMES)
+def test_reset_parity(name):
+    B = 512
+    keys = _keys(B)
+    env = _envs().create(name, batch_size=B)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name).reset(keys, first=True)
+    compare_states(s, o, f"{name} reset")
+    fq = s.info["first_qp"]
+    np.testing.assert_array_equal(_np(fq.pos), _np(s.qp.pos))
+
+
+# ------------------------------------------------------------------------------- step
+@pytest.mark.parametrize("name", NAMES)
+def test_step_parity_per_step(name):
+    """30 steps; every step the oracle restarts from the GPU's state (one-step parity)."""
+    B, T = 256, 30
+    envs = _envs()
+    env = envs.create(name, batch_size=B, episode_length=20)
+    s = env.reset(torch.from_numpy(_keys(B, 1)).cuda())
+    o = orc.OracleEnv(name)
+    rng = np.random.default_rng(0)
+    report = []
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        so = o.step(_state_np(s), act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=20)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} step {t}", report)
+    n_exact = sum(e for _, e in report)
+    print(f"{name}: {n_exact}/{len(report)} steps bit-exact on every float field")
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_trajectory_parity_free_running(name):
+    """Both engines run 25 steps independently from the same reset (stronger than per-step:
+    any float divergence would compound through the contact dynamics)."""
+    B, T = 128, 25
+    env = _envs().create(name, batch_size=B, episode_length=1000)
+    keys = _keys(B, 2)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name)
+    so = o.reset(keys, first=True)
+    rng = np.random.default_rng(4)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        s = env.step_(s, torch.from_numpy(act).cuda())
+        so = o.step(so, act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=1000, inplace=True)
+    compare_states(s, so, f"{name} free-running t={T}")
+
+
+def test_functional_and_inplace_agree():
+    B = 128
+    env = _envs().create("ant_heavenhell", batch_size=B)
+    keys = torch.from_numpy(_keys(B)).cuda()
+    s1 = env.reset(keys)
+    s2 = env.reset(keys)
+    act = torch.rand((B, 8), device="cuda") * 2 - 1
+    a = env.step(s1, act)
+    pos_before = s1.qp.pos.clone()
+    b = env.step_(s2, act)
+    assert torch.equal(a.qp.pos, b.qp.pos) and torch.equal(a.obs, b.obs)
+    assert torch.equal(s1.qp.pos, pos_before)  # functional step leaves its input intact
+
+
+# ------------------------------------------------------------------------- autoreset
+@pytest.mark.parametrize("name", NAMES)
+def test_gym_autoreset_parity(name):
+    """AutoresetVmapGymWrapper (wrappers.py:240-262) with the device-side any(done)."""
+    B, T = 96, 25
+    envs = _envs()
+    g = envs.create_gym_env(name, batch_size=B, seed=3, episode_length=7)
+    obs = g.reset()
+    o = orc.OracleEnv(name)
+    key = P.prngkey(3)
+    ks = P.split(key, B + 1)
+    so, gkey = o.reset(ks[1:]), ks[0].copy()
+    np.testing.assert_array_equal(_np(obs), so["obs"])
+    rng = np.random.default_rng(1)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        obs, rew, done, info = g.step(torch.from_numpy(act).cuda())
+        so = o.step(so, act, flags=orc.F_EPISODE, episode_length=7, inplace=True)
+        np.testing.assert_array_equal(_np(done), so["done"], err_msg=f"t={t}")
+        o.gym_autoreset(so, gkey)
+        close(obs, so["obs"], f"{name} gym obs t={t}")
+        close(g._state.qp.pos, so["pos"], f"{name} gym pos t={t}")
+        np.testing.assert_array_equal(_np(g._key), gkey, err_msg=f"gym key t={t}")
+        np.testing.assert_array_equal(_np(g._state.info["steps"]), so["steps"])
+
+
+def test_randomized_autoreset_naive():
+    """RandomizedAutoResetWrapperNaive (wrappers.py:30-52): reset(info.rng) where done."""
+    B = 64
+    envs = _envs()
+    name = "ant_tag"
+    env = envs.wrappers.RandomizedAutoResetWrapperNaive(envs.create(name, batch_size=B, auto_reset=False,
+                                                                    episode_length=5))
+    s = env.reset(torch.from_numpy(_keys(B)).cuda())
+    o = orc.OracleEnv(name)
+    rng = np.random.default_rng(2)
+    for t in range(8):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        prev = _state_np(s)
+        if t > 0:
+            prev["steps"] = np.where(prev["done"] != 0, 0, prev["steps"]).astype(np.float32)
+        so = o.step(prev, act, flags=orc.F_EPISODE, episode_length=5)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        # reset the done envs from their (post-step) info['rng']
+        done = so["done"] != 0
+        if done.any():
+            fresh = o.reset(so["rng"][done])
+            for k in ("pos", "rot", "vel", "ang", "obs"):
+                so[k][done] = fresh[k]
+        close(s.qp.pos, so["pos"], f"naive pos t={t}")
+        close(s.obs, so["obs"], f"naive obs t={t}")
+
+
+# ---------------------------------------------------------------------- misc surface
+def test_obs_mask_gather():
+    from po_brax_amd import standard_observability_masks as M
+    obs = torch.randn((1000, 87), device="cuda")
+    for idx in (M.POSITION["ant"], M.VELOCITY["ant"], M.CFRC["ant"]):
+        got = M.apply_mask(obs, idx)
+        assert torch.equal(got, obs[:, torch.as_tensor(idx, device="cuda")])
+    o2 = torch.randn((64, 114), device="cuda")
+    idx = M.po_env_mask("ant_heavenhell", cfrc=False)
+    assert torch.equal(M.apply_mask(o2, idx), o2[:, torch.as_tensor(idx, device="cuda")])
+
+
+def test_registry_errors():
+    envs = _envs()
+    with pytest.raises(KeyError):
+        envs.create("no_such_env")
+    with pytest.raises(ValueError):
+        envs.create_gym_env("ant_heavenhell", batch_size=-1)
+    with pytest.raises(NotImplementedError):
+        envs.create("humanoid")
+
+
+def test_unbatched_env_api():
+    """Un-vmapped brax usage: reset(key (2,)) -> unbatched shapes; step works on them."""
+    envs = _envs()
+    env = envs.AntHeavenHellEnv()
+    s = env.reset(torch.tensor([0, 0], dtype=torch.uint32))
+    assert s.qp.pos.shape == (14, 3) and s.obs.shape == (114,) and s.reward.shape == ()
+    s2 = env.step(s, torch.zeros(8))
+    assert s2.obs.shape == (114,) and "hits" in s2.metrics
+    o = orc.OracleEnv("ant_heavenhell")
+    so = o.reset(np.zeros((1, 2), np.uint32))
+    np.testing.assert_array_equal(_np(s.obs), so["obs"][0])
+
+
+def test_large_batch_properties():
+    """HH at the headline batch (65 536): finite, unit quaternions, done/reward logic."""
+    B, T = 65536, 20
+    env = _envs().create("ant_heavenhell", batch_size=B, episode_length=1000)
+    from po_brax_amd import jumpy
+    key = jumpy.random_prngkey(0)
+    keys = jumpy.random_split(key, B + 1)[1:].contiguous()
+    s = env.reset(keys)
+    act = torch.empty((B, 8), device="cuda")
+    for _ in range(T):
+        jumpy.random_actions_(key, B, 0, act)
+        s = env.step_(s, act)
+    torch.cuda.synchronize()
+    assert torch.isfinite(s.obs).all() and torch.isfinite(s.qp.pos).all()
+    qn = s.qp.rot[:, :9].norm(dim=-1)
+    assert torch.allclose(qn, torch.ones_like(qn), atol=1e-5)
+    r, d = s.reward, s.done
+    assert bool(((r != 0) <= (d != 0)).all())  # every non-zero reward ends the episode (HH)
+    assert set(torch.unique(r).tolist()) <= {-2.0, -1.0, 0.0, 1.0}
