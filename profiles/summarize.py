@@ -1,0 +1,56 @@
+"""Summarise a gpurun_out/<tag>/ rocprofv3 directory into profiles/<tag>_summary.md.
+
+Usage: python profiles/summarize.py gpurun_out/prof_r1 profiles/r1
+Copies the kernel-stats CSV and writes per-dispatch means of every PMC counter for the
+step kernel, plus the derived HBM numbers (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM
+for wide coalesced reads -- our loads are narrow, so both raw and doubled are listed).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def main(src, dst_prefix):
+    os.makedirs(os.path.dirname(dst_prefix), exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), dst_prefix + "_kernel_stats.csv")
+    lines = [f"# rocprofv3 summary ({os.path.basename(src)})", ""]
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))))
+    lines.append("| kernel | calls | avg us | % |")
+    lines.append("|---|---|---|---|")
+    for r in stats[:8]:
+        lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.2f} |")
+    lines.append("")
+    counters = collections.defaultdict(list)
+    for d in sorted(os.listdir(src)):
+        p = os.path.join(src, d, f"{d}_counter_collection.csv")
+        if d.startswith("pmc") and os.path.exists(p):
+            for r in csv.DictReader(open(p)):
+                if "k_step" in r["Kernel_Name"]:
+                    counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    counters["_grid"] = [float(r["Grid_Size"])]
+                    counters["_vgpr"] = [float(r["VGPR_Count"])]
+                    counters["_agpr"] = [float(r["Accum_VGPR_Count"])]
+                    counters["_lds"] = [float(r["LDS_Block_Size"])]
+    lines.append("k_step per-dispatch counter means:")
+    lines.append("")
+    for k, v in sorted(counters.items()):
+        lines.append(f"- {k}: {sum(v)/len(v):.6g}")
+    if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+        f = sum(counters["FETCH_SIZE"]) / len(counters["FETCH_SIZE"]) * 1024
+        w = sum(counters["WRITE_SIZE"]) / len(counters["WRITE_SIZE"]) * 1024
+        lines.append("")
+        lines.append(f"- HBM bytes per launch: FETCH {f/1e6:.2f} MB (x2 gfx950 correction {2*f/1e6:.2f} MB), "
+                     f"WRITE {w/1e6:.2f} MB")
+    for j in ("trace.bench.json",):
+        p = os.path.join(src, j)
+        if os.path.exists(p) and os.path.getsize(p):
+            lines += ["", "bench line of the profiled run:", "", "```", open(p).read().strip(), "```"]
+    open(dst_prefix + "_summary.md", "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
