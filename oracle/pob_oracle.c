@@ -63,7 +63,7 @@ static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
 static inline v3 vadd(v3 a, v3 b) { FL(3); return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 static inline v3 vsub(v3 a, v3 b) { FL(3); return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline v3 vscl(v3 a, float s) { FL(3); return V(a.x * s, a.y * s, a.z * s); }
-static inline v3 vdivs(v3 a, float s) { FL(3); return V(a.x / s, a.y / s, a.z / s); }
+static inline v3 vdivs(v3 a, float s) { FL(4); float inv = 1.0f / s; return V(a.x * inv, a.y * inv, a.z * inv); }
 static inline float vdot(v3 a, v3 b) { FL(5); return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline v3 vcross(v3 a, v3 b) {
   FL(9);
@@ -102,9 +102,10 @@ static inline q4 qmul_vq(v3 a, q4 q) {
 }
 static inline q4 qinv(q4 q) { q4 r = {q.w, -q.x, -q.y, -q.z}; return r; }
 static inline q4 qnormalize(q4 q) {
-  FL(12);
+  FL(13);
   float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
-  q4 r = {q.w / n, q.x / n, q.y / n, q.z / n};
+  float inv = 1.0f / n;
+  q4 r = {q.w * inv, q.x * inv, q.y * inv, q.z * inv};
   return r;
 }
 
@@ -238,7 +239,7 @@ void orc_choice_idx(const uint32_t key[2], int n, int k, int *out) {
 struct orc_env {
   int kind, N, D, n_obj;
   /* integrator */
-  float h, half_h, lin_damp, ang_damp, g[3];
+  float h, half_h, inv_h, lin_damp, ang_damp, g[3];
   int substeps;
   float mass[NDYN], inv_mass[NDYN];
   /* joints (ant tree; parent(j) = j odd ? j : 0, child(j) = j+1) */
@@ -338,7 +339,7 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
   double dt = f32d(0.05) * ar; int sub = 10 * ar; /* wrappers.py:21-23 */
   double hd = dt / sub;
   e->substeps = sub;
-  e->h = (float)hd; e->half_h = 0.5f * e->h;
+  e->h = (float)hd; e->half_h = 0.5f * e->h; e->inv_h = (float)(1.0 / hd);
   e->lin_damp = (float)exp(0.0 * hd);
   e->ang_damp = (float)exp(f32d(-0.05) * hd);
   e->g[0] = 0.0f; e->g[1] = 0.0f; e->g[2] = (float)f32d(-9.8);
@@ -590,7 +591,7 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
     v3 dv = V(0.0f, 0.0f, 0.0f);
     if (lt > 0.0f) {
       FL(4);
-      float fr = fminf(e->friction * pen / e->h, lt);
+      float fr = fminf(e->friction * pen * e->inv_h, lt);
       dv = vscl(vt, -(fr / lt));
     }
     if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
@@ -704,11 +705,11 @@ static void pbd_substep(const orc_env *e, body_t *b, const float *act, int colli
   /* 4. velocity projection */
   for (int i = 0; i < NDYN; ++i) {
     b->q[i] = qnormalize(b->q[i]);
-    b->v[i] = vdivs(vsub(b->x[i], prev.x[i]), e->h);
+    b->v[i] = vscl(vsub(b->x[i], prev.x[i]), e->inv_h);
     q4 dq = qmul(b->q[i], qinv(prev.q[i]));
     float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
     FL(9);
-    b->w[i] = V(sg * ((2.0f * dq.x) / e->h), sg * ((2.0f * dq.y) / e->h), sg * ((2.0f * dq.z) / e->h));
+    b->w[i] = V(sg * ((2.0f * dq.x) * e->inv_h), sg * ((2.0f * dq.y) * e->inv_h), sg * ((2.0f * dq.z) * e->inv_h));
   }
   /* 5. velocity-level contact solve */
   if (collide) {

@@ -17,7 +17,7 @@ POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return 
 POB_D v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 POB_D v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 POB_D v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
-POB_D v3 vdivs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+POB_D v3 vdivs(v3 a, float s) { float inv = 1.0f / s; return V(a.x * inv, a.y * inv, a.z * inv); }
 POB_D float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 POB_D v3 vcross(v3 a, v3 b) {
   return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -55,7 +55,8 @@ POB_D q4 qmul_vq(v3 a, q4 q) {
 POB_D q4 qinv(q4 q) { q4 r; r.w = q.w; r.x = -q.x; r.y = -q.y; r.z = -q.z; return r; }
 POB_D q4 qnormalize(q4 q) {
   float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
-  q4 r; r.w = q.w / n; r.x = q.x / n; r.y = q.y / n; r.z = q.z / n;
+  float inv = 1.0f / n;
+  q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
   return r;
 }
 // acc += sign * 0.5 * d

@@ -101,6 +101,23 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
     v3 pe = vadd(b.x[i], qrot(SV(S.ground_end[g]), b.q[i]));
     ct.pen[g] = S.ground_r[g] - pe.z;
   }
+  // wave-uniform broadphase: bit w set iff some lane's body-centre AABB meets wall w's grown box
+  uint32_t near_mask = 0u;
+  {
+    v3 mn = b.x[0], mx = b.x[0];
+#pragma unroll
+    for (int i = 1; i < POB_NDYN; ++i) {
+      mn = V(fminf(mn.x, b.x[i].x), fminf(mn.y, b.x[i].y), fminf(mn.z, b.x[i].z));
+      mx = V(fmaxf(mx.x, b.x[i].x), fmaxf(mx.y, b.x[i].y), fmaxf(mx.z, b.x[i].z));
+    }
+    csys_t &S = *launder(Sp);
+    const int nw = S.n_walls;
+    for (int w = 0; w < nw; ++w) {
+      const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
+                        mx.y >= S.wall_lo[w][1] && mn.z <= S.wall_hi[w][2] && mx.z >= S.wall_lo[w][2];
+      if (__any(near)) near_mask |= 1u << w;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < POB_NDYN; ++i) {
     POB_FENCE();
@@ -115,6 +132,7 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
     const float r = S.cap_r[i];
     const int nw = S.n_walls;
     for (int w = 0; w < nw; ++w) {
+      if (!(near_mask & (1u << w))) continue;  // uniform: no lane can touch wall w
 #pragma unroll
       for (int q = 0; q < nend; ++q) {
         v3 n;
@@ -208,7 +226,7 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       float lt = sqrtf(vdot(vt, vt));
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
-        float fr = fminf(S.friction * pen / S.h, lt);
+        float fr = fminf(S.friction * pen * S.inv_h, lt);
         dv = vscl(vt, -(fr / lt));
       }
       if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
@@ -329,10 +347,10 @@ POB_D void pbd_substep(csys_t *Sp, Body &b, const float (&act)[POB_NJ], const Ld
 #pragma unroll
     for (int i = 0; i < POB_NDYN; ++i) {
       b.q[i] = qnormalize(b.q[i]);
-      b.v[i] = vdivs(vsub(b.x[i], L.get3(POB_LDS_PX(i))), S.h);
+      b.v[i] = vscl(vsub(b.x[i], L.get3(POB_LDS_PX(i))), S.inv_h);
       q4 dq = qmul(b.q[i], qinv(L.get4(POB_LDS_PQ(i))));
       float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
-      b.w[i] = V(sg * ((2.0f * dq.x) / S.h), sg * ((2.0f * dq.y) / S.h), sg * ((2.0f * dq.z) / S.h));
+      b.w[i] = V(sg * ((2.0f * dq.x) * S.inv_h), sg * ((2.0f * dq.y) * S.inv_h), sg * ((2.0f * dq.z) * S.inv_h));
     }
   }
   // 5. velocity-level contact solve, accumulated into Info.contact (LDS)

@@ -22,7 +22,7 @@ struct pob_sys {
   int substeps, n_walls, n_grid;
   int ga_n_apples, ga_n_bins;
   // integrator (dt_sub = dt / substeps)
-  float h, half_h, lin_damp, ang_damp, gz;
+  float h, half_h, inv_h, lin_damp, ang_damp, gz;
   float inv_mass[POB_NDYN];
   // joints: parent/child offsets, hinge axis and reference direction (body frame),
   // limits (rad), angular damping, actuator strength, default angle
@@ -34,6 +34,10 @@ struct pob_sys {
   float ground_end[POB_NGROUND][3], ground_r[POB_NGROUND];
   // walls: box centre (world), half extents, z-rotation cos/sin
   float wall_c[POB_MAXW][3], wall_h[POB_MAXW][3], wall_cos[POB_MAXW], wall_sin[POB_MAXW];
+  // broadphase: world AABB of each wall grown by (capsule reach + radius + margin); a
+  // wave skips a wall when no lane's body centres fall inside it (exact: every culled
+  // sphere-box pair has penetration < 0, so the deepest-contact search is unchanged)
+  float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
   float friction, s_pos, half_s_ang;
   // default_qp rows of the frozen bodies (index >= 9)
   float frozen_pos[POB_MAXB][3];

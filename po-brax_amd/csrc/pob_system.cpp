@@ -114,7 +114,7 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
   const int sub = 10 * ar;
   const double hd = dt / sub;
   s.substeps = sub;
-  s.h = (float)hd; s.half_h = 0.5f * s.h;
+  s.h = (float)hd; s.half_h = 0.5f * s.h; s.inv_h = (float)(1.0 / hd);
   s.lin_damp = (float)exp(0.0 * hd);
   s.ang_damp = (float)exp(f32d(-0.05) * hd);
   s.gz = (float)f32d(-9.8);
@@ -200,6 +200,24 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     s.tag_target_step = p.tag_target_step; s.tag_min_spawn_distance = p.tag_min_spawn_distance;
     s.tag_cage_xy[0] = p.tag_cage_xy[0]; s.tag_cage_xy[1] = p.tag_cage_xy[1];
     s.tag_dying_cost = p.tag_dying_cost;
+  }
+  // broadphase boxes: wall AABB + the largest distance from a body centre to any point of
+  // its capsule (|end| + r) + 1e-3 margin (>> float rounding of the sphere-box distance)
+  double reach = 0.0;
+  for (int i = 0; i < POB_NDYN; ++i)
+    for (int q = 0; q < 2; ++q) {
+      const float *e = s.cap_end[i][q];
+      reach = fmax(reach, sqrt((double)e[0] * e[0] + (double)e[1] * e[1] + (double)e[2] * e[2]) + s.cap_r[i]);
+    }
+  reach += 1e-3;
+  for (int w = 0; w < s.n_walls; ++w) {
+    const double c = fabs((double)s.wall_cos[w]), sn = fabs((double)s.wall_sin[w]);
+    const double ex[3] = {c * s.wall_h[w][0] + sn * s.wall_h[w][1], sn * s.wall_h[w][0] + c * s.wall_h[w][1],
+                          (double)s.wall_h[w][2]};
+    for (int k = 0; k < 3; ++k) {
+      s.wall_lo[w][k] = (float)(s.wall_c[w][k] - ex[k] - reach);
+      s.wall_hi[w][k] = (float)(s.wall_c[w][k] + ex[k] + reach);
+    }
   }
   return nullptr;
 }
