@@ -12,11 +12,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 
 #include "../../include/pob.h"
+#include "pob_pair.h"
 #include "pob_physics.h"
 
 namespace pob {
@@ -32,6 +34,7 @@ struct pob_env {
   float *d_grid = nullptr;
   uint32_t *d_scratch = nullptr;  // any-done word for pob_reset_where_done without a flag
   int device = 0;
+  int lanes_per_env = 2;  // k_step_pair (default) or k_step (POB_STEP_LANES=1)
 };
 
 // ---------------------------------------------------------------------------- state
@@ -134,6 +137,104 @@ POB_D void ga_reading_one(csys_t &S, int k, float ox, float oy, float dist, floa
   if (slot >= 0 && slot < 2 * S.ga_n_bins) o_rd[slot] = inten;
 }
 
+struct TaskOut {
+  float reward, done, trunc, steps, m0, m1, m2;
+  uint32_t rng0, rng1;
+};
+
+// Per-env POMDP logic after the physics (env.step minus System.step) + EpisodeWrapper:
+// reward / done / metrics / rng, the task part of the obs, and the task bodies' rows.
+// HH ant_heavenhell.py:106-123, GA ant_gather.py:125-150 (+ readings :152-181),
+// TAG ant_tag.py:107-146; EpisodeWrapper.step [ext].
+template <int KIND>
+POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r3, const int N, const v3 x0,
+                     const q4 q0, float *opos, float *o, const uint32_t flags, const int L, TaskOut &t) {
+  const float tz = x0.z;
+  float dead = tz < 0.2f ? 1.0f : 0.0f;
+  dead = tz > 1.0f ? 1.0f : dead;
+  float reward, done;
+  float steps = t.steps, m0 = t.m0, m1 = t.m1, m2 = t.m2;
+  uint32_t rng0 = t.rng0, rng1 = t.rng1;
+  const int base = 29 + 6 * N;
+  if (KIND == POB_HEAVENHELL) {
+    // ant_heavenhell.py:106-123
+    reward = dead > 0.0f ? S.hh_dying_cost : 0.0f;
+    const float *ip = in.pos + r3;
+    bool in0 = dist2d(ip[33], ip[34], x0.x, x0.y) <= S.hh_visible_radius;  // Target (11)
+    bool in1 = dist2d(ip[36], ip[37], x0.x, x0.y) <= S.hh_visible_radius;  // Hell (12)
+    bool in2 = dist2d(ip[30], ip[31], x0.x, x0.y) <= S.hh_visible_radius;  // Priest (10)
+    if (in0) reward = 1.0f;
+    if (in1) reward = -1.0f;
+    done = reward != 0.0f ? 1.0f : 0.0f;
+    const float tx = ip[33];
+    const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
+    o[base] = in2 ? sgn : 0.0f;
+    m2 = done;  // metrics['hits']
+  } else if (KIND == POB_GATHER) {
+    // ant_gather.py:125-150 (obs from pre-relocation positions)
+    float *rd = o + base;
+    ga_readings_begin(S, rd);
+    const float ori = ga_orientation(q0);
+    const float *ip = in.pos + r3;
+    int na_hit = 0, nb_hit = 0;
+    bool any_a = false, any_b = false, all_wait = true;
+    for (int k = 0; k < S.n_obj; ++k) {
+      const int row = 3 * (11 + k);
+      const float ox = ip[row], oy = ip[row + 1], oz = ip[row + 2];
+      const float dk = dist2d(x0.x, x0.y, ox, oy);
+      ga_reading_one(S, k, ox, oy, dk, ori, rd);
+      const bool c = dk <= S.ga_catch_range;
+      float nx = ox, ny = oy, nz = oz;
+      if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
+      opos[row] = nx; opos[row + 1] = ny; opos[row + 2] = nz;
+      if (k < S.ga_n_apples) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
+      all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
+    }
+    reward = dead > 0.0f ? S.ga_dying_cost : 0.0f;
+    if (any_a && dead == 0.0f) reward = 1.0f;
+    if (any_b && dead == 0.0f) reward = -1.0f;
+    done = all_wait ? 1.0f : dead;
+    m0 = (float)na_hit; m1 = (float)nb_hit;
+  } else {
+    // ant_tag.py:107-127, adversary _step_target :129-146
+    reward = dead > 0.0f ? S.tag_dying_cost : 0.0f;
+    uint32_t n0, n1, c0, c1;
+    tf_split(rng0, rng1, 2u, 0u, n0, n1);
+    tf_split(rng0, rng1, 2u, 1u, c0, c1);
+    uint32_t k20, k21;  // randint(rng1, (), 0, 4) = bits(split(rng1)[1]) % 4
+    tf_split(c0, c1, 2u, 1u, k20, k21);
+    const int ch = (int)(tf_elem(k20, k21, 1u, 0u) % 4u);
+    const float *ip = in.pos + r3;
+    const float ax = x0.x, ay = x0.y, tx = ip[30], ty = ip[31];
+    float vx = ax - tx, vy = ay - ty;
+    const float nrm = sqrtf(vx * vx + vy * vy);
+    vx = vx / nrm; vy = vy / nrm;
+    float cx, cy;
+    if (ch == 0) { cx = vy * 1.0f; cy = vx * -1.0f; }
+    else if (ch == 1) { cx = vy * -1.0f; cy = vx * 1.0f; }
+    else if (ch == 2) { cx = -vx; cy = -vy; }
+    else { cx = 0.0f; cy = 0.0f; }
+    float nx = cx * S.tag_target_step + tx, ny = cy * S.tag_target_step + ty;
+    if (fabsf(nx) > S.tag_cage_xy[0] || fabsf(ny) > S.tag_cage_xy[1]) { nx = tx; ny = ty; }
+    opos[30] = nx; opos[31] = ny; opos[32] = 1.0f;
+    rng0 = n0; rng1 = n1;
+    const bool vis = dist2d(nx, ny, ax, ay) <= S.tag_visible_radius;
+    o[base] = vis ? nx : 0.0f; o[base + 1] = vis ? ny : 0.0f;
+    const float tag = dist2d(ax, ay, nx, ny) <= S.tag_tag_radius ? 1.0f : 0.0f;
+    m0 = tag;
+    if (tag > 0.0f) reward = 1.0f;
+    done = (dead != 0.0f || tag != 0.0f) ? 1.0f : 0.0f;
+  }
+  float trunc = in.truncation ? in.truncation[b] : 0.0f;
+  if (flags & POB_F_EPISODE) {  // brax EpisodeWrapper.step [ext]
+    steps = steps + 1.0f;
+    trunc = steps >= (float)L ? 1.0f - done : 0.0f;
+    done = steps >= (float)L ? 1.0f : done;
+  }
+  t.reward = reward; t.done = done; t.trunc = trunc; t.steps = steps;
+  t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
+}
+
 // ------------------------------------------------------------------------------ step
 // Fused step: brax AutoResetWrapper(VmapWrapper(EpisodeWrapper(ActionRepeat(env)))).step
 // (envs/__init__.py:59-70) with env.step = ant_heavenhell.py:106-123 /
@@ -183,87 +284,13 @@ __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, con
     }
     store_body(bd, opos, orot, ovel, oang);
 
-    const float tz = bd.x[0].z;
-    float dead = tz < 0.2f ? 1.0f : 0.0f;
-    dead = tz > 1.0f ? 1.0f : dead;
-    float reward;
     write_obs_common(S, N, bd, cv, ca, o);
-    const int base = 29 + 6 * N;
-    if (KIND == POB_HEAVENHELL) {
-      // ant_heavenhell.py:106-123
-      reward = dead > 0.0f ? S.hh_dying_cost : 0.0f;
-      const float *ip = in.pos + r3;
-      bool in0 = dist2d(ip[33], ip[34], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Target (11)
-      bool in1 = dist2d(ip[36], ip[37], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Hell (12)
-      bool in2 = dist2d(ip[30], ip[31], bd.x[0].x, bd.x[0].y) <= S.hh_visible_radius;  // Priest (10)
-      if (in0) reward = 1.0f;
-      if (in1) reward = -1.0f;
-      done = reward != 0.0f ? 1.0f : 0.0f;
-      const float tx = ip[33];
-      const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
-      o[base] = in2 ? sgn : 0.0f;
-      m2 = done;  // metrics['hits']
-    } else if (KIND == POB_GATHER) {
-      // ant_gather.py:125-150 (obs from pre-relocation positions)
-      float *rd = o + base;
-      ga_readings_begin(S, rd);
-      const float ori = ga_orientation(bd.q[0]);
-      const float *ip = in.pos + r3;
-      int na_hit = 0, nb_hit = 0;
-      bool any_a = false, any_b = false, all_wait = true;
-      for (int k = 0; k < S.n_obj; ++k) {
-        const int row = 3 * (11 + k);
-        const float ox = ip[row], oy = ip[row + 1], oz = ip[row + 2];
-        const float dk = dist2d(bd.x[0].x, bd.x[0].y, ox, oy);
-        ga_reading_one(S, k, ox, oy, dk, ori, rd);
-        const bool c = dk <= S.ga_catch_range;
-        float nx = ox, ny = oy, nz = oz;
-        if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
-        opos[row] = nx; opos[row + 1] = ny; opos[row + 2] = nz;
-        if (k < S.ga_n_apples) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
-        all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
-      }
-      reward = dead > 0.0f ? S.ga_dying_cost : 0.0f;
-      if (any_a && dead == 0.0f) reward = 1.0f;
-      if (any_b && dead == 0.0f) reward = -1.0f;
-      done = all_wait ? 1.0f : dead;
-      m0 = (float)na_hit; m1 = (float)nb_hit;
-    } else {
-      // ant_tag.py:107-127, adversary _step_target :129-146
-      reward = dead > 0.0f ? S.tag_dying_cost : 0.0f;
-      uint32_t n0, n1, c0, c1;
-      tf_split(rng0, rng1, 2u, 0u, n0, n1);
-      tf_split(rng0, rng1, 2u, 1u, c0, c1);
-      uint32_t k20, k21;  // randint(rng1, (), 0, 4) = bits(split(rng1)[1]) % 4
-      tf_split(c0, c1, 2u, 1u, k20, k21);
-      const int ch = (int)(tf_elem(k20, k21, 1u, 0u) % 4u);
-      const float *ip = in.pos + r3;
-      const float ax = bd.x[0].x, ay = bd.x[0].y, tx = ip[30], ty = ip[31];
-      float vx = ax - tx, vy = ay - ty;
-      const float nrm = sqrtf(vx * vx + vy * vy);
-      vx = vx / nrm; vy = vy / nrm;
-      float cx, cy;
-      if (ch == 0) { cx = vy * 1.0f; cy = vx * -1.0f; }
-      else if (ch == 1) { cx = vy * -1.0f; cy = vx * 1.0f; }
-      else if (ch == 2) { cx = -vx; cy = -vy; }
-      else { cx = 0.0f; cy = 0.0f; }
-      float nx = cx * S.tag_target_step + tx, ny = cy * S.tag_target_step + ty;
-      if (fabsf(nx) > S.tag_cage_xy[0] || fabsf(ny) > S.tag_cage_xy[1]) { nx = tx; ny = ty; }
-      opos[30] = nx; opos[31] = ny; opos[32] = 1.0f;
-      rng0 = n0; rng1 = n1;
-      const bool vis = dist2d(nx, ny, ax, ay) <= S.tag_visible_radius;
-      o[base] = vis ? nx : 0.0f; o[base + 1] = vis ? ny : 0.0f;
-      const float tag = dist2d(ax, ay, nx, ny) <= S.tag_tag_radius ? 1.0f : 0.0f;
-      m0 = tag;
-      if (tag > 0.0f) reward = 1.0f;
-      done = (dead != 0.0f || tag != 0.0f) ? 1.0f : 0.0f;
-    }
-    float trunc = in.truncation ? in.truncation[b] : 0.0f;
-    if (flags & POB_F_EPISODE) {  // brax EpisodeWrapper.step [ext]
-      steps = steps + 1.0f;
-      trunc = steps >= (float)L ? 1.0f - done : 0.0f;
-      done = steps >= (float)L ? 1.0f : done;
-    }
+    TaskOut t;
+    t.steps = steps; t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
+    task_step<KIND>(S, in, b, r3, N, bd.x[0], bd.q[0], opos, o, flags, L, t);
+    done = t.done;
+    const float reward = t.reward, trunc = t.trunc;
+    steps = t.steps; m0 = t.m0; m1 = t.m1; m2 = t.m2; rng0 = t.rng0; rng1 = t.rng1;
     if ((flags & POB_F_AUTORESET) && done != 0.0f) {  // brax AutoResetWrapper.step [ext]
       for (int k = 0; k < 3 * N; ++k) {
         opos[k] = in.first_pos[r3 + k]; ovel[k] = in.first_vel[r3 + k]; oang[k] = in.first_ang[r3 + k];
@@ -291,6 +318,160 @@ __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, con
   }
   if (out.any_done) {
     const unsigned long long m = __ballot(done != 0.0f);
+    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
+  }
+}
+
+
+// ------------------------------------------------------------------ step, lane pairs
+// Same fused step with TWO lanes per env (pob_pair.h): lane h owns the torso (replica) and
+// bodies 4h+1..4h+4.  2 waves / SIMD (VGPR+AGPR <= 256, 65 LDS floats / lane).  Lane 0
+// runs the per-env POMDP tail; lane 1 writes its bodies' rows, joints and cfrc rows.
+template <int KIND>
+__global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const int B, const StatePtrs in,
+                                                      const float *__restrict__ act, const StatePtrs out,
+                                                      const uint32_t flags, const int L) {
+  __shared__ float lds[PL_FLOATS * 256];
+  csys_t *Sp = (csys_t *)(size_t)sysp;
+  csys_t &S = *Sp;
+  const Lds Ls{lds, 256, (int)threadIdx.x};
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gt >> 1;
+  const bool h = (gt & 1) != 0;
+  float done = 0.0f;
+  if (b < B) {
+    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+    HBody bd;
+#pragma unroll
+    for (int l = 0; l < PNB; ++l) {
+      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
+      bd.x[l] = vload(in.pos + r3 + 3 * g);
+      const float *rq = in.rot + r4 + 4 * g;
+      bd.q[l].w = rq[0]; bd.q[l].x = rq[1]; bd.q[l].y = rq[2]; bd.q[l].z = rq[3];
+      bd.v[l] = vload(in.vel + r3 + 3 * g);
+      bd.w[l] = vload(in.ang + r3 + 3 * g);
+    }
+    float a[PNJ];
+#pragma unroll
+    for (int jl = 0; jl < PNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + jl + (h ? 4 : 0)];
+
+#pragma unroll
+    for (int l = 0; l < PNB; ++l) { Ls.set3(PL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(PL_CA(l), V(0.0f, 0.0f, 0.0f)); }
+    const int iters = launder(Sp)->substeps / 2;
+#pragma nounroll
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep(Sp, bd, a, Ls, h, (it & 1) != 0);
+
+    float *opos = out.pos + r3, *orot = out.rot + r4, *ovel = out.vel + r3, *oang = out.ang + r3;
+    float *o = out.obs + (size_t)b * D;
+    // joint angle / velocity obs of this lane's joints (a3)
+#pragma unroll
+    for (int jl = 0; jl < PNJ; ++jl) {
+      const int p = jparent(jl), c = jchild(jl);
+      v3 ap = qrot(HSV(h, S.axis[jl], S.axis[jl + 4]), bd.q[p]);
+      const v3 ref = HSV(h, S.ref[jl], S.ref[jl + 4]);
+      v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
+      const int j = jl + (h ? 4 : 0);
+      o[7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      o[21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
+    }
+    // cfrc rows: lane 0 rows 0..4, lane 1 rows 5..8 and the zero rows of frozen bodies
+#pragma unroll
+    for (int l = 0; l < PNB; ++l) {
+      if (l == 0 && h) continue;
+      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
+      const v3 cv = Ls.get3(PL_CV(l)), ca = Ls.get3(PL_CA(l));
+      o[29 + 3 * g] = clip1(cv.x); o[30 + 3 * g] = clip1(cv.y); o[31 + 3 * g] = clip1(cv.z);
+      o[29 + 3 * N + 3 * g] = clip1(ca.x); o[30 + 3 * N + 3 * g] = clip1(ca.y); o[31 + 3 * N + 3 * g] = clip1(ca.z);
+    }
+    if (h) {
+      for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { o[29 + k] = 0.0f; o[29 + 3 * N + k] = 0.0f; }
+    }
+    TaskOut t;
+    if (!h) {
+      o[0] = bd.x[0].x; o[1] = bd.x[0].y; o[2] = bd.x[0].z;
+      o[3] = bd.q[0].w; o[4] = bd.q[0].x; o[5] = bd.q[0].y; o[6] = bd.q[0].z;
+      o[15] = bd.v[0].x; o[16] = bd.v[0].y; o[17] = bd.v[0].z;
+      o[18] = bd.w[0].x; o[19] = bd.w[0].y; o[20] = bd.w[0].z;
+      if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
+        for (int i = POB_NDYN; i < N; ++i) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            opos[3 * i + c] = in.pos[r3 + 3 * i + c];
+            ovel[3 * i + c] = in.vel[r3 + 3 * i + c];
+            oang[3 * i + c] = in.ang[r3 + 3 * i + c];
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) orot[4 * i + c] = in.rot[r4 + 4 * i + c];
+        }
+      }
+      float steps = in.steps ? in.steps[b] : 0.0f;
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
+      t.steps = steps;
+      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+      task_step<KIND>(S, in, b, r3, N, bd.x[0], bd.q[0], opos, o, flags, L, t);
+      done = t.done;
+    }
+    const float done_partner = pair_swap(done);  // all lanes of the pair active here
+    done = h ? done_partner : done;
+    const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+    // dynamic body rows: computed state, or first_qp when the AutoResetWrapper resets
+#pragma unroll
+    for (int l = 0; l < PNB; ++l) {
+      if (l == 0 && h) continue;
+      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
+      if (reset_rows) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          opos[3 * g + c] = in.first_pos[r3 + 3 * g + c];
+          ovel[3 * g + c] = in.first_vel[r3 + 3 * g + c];
+          oang[3 * g + c] = in.first_ang[r3 + 3 * g + c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) orot[4 * g + c] = in.first_rot[r4 + 4 * g + c];
+      } else {
+        opos[3 * g] = bd.x[l].x; opos[3 * g + 1] = bd.x[l].y; opos[3 * g + 2] = bd.x[l].z;
+        orot[4 * g] = bd.q[l].w; orot[4 * g + 1] = bd.q[l].x; orot[4 * g + 2] = bd.q[l].y; orot[4 * g + 3] = bd.q[l].z;
+        ovel[3 * g] = bd.v[l].x; ovel[3 * g + 1] = bd.v[l].y; ovel[3 * g + 2] = bd.v[l].z;
+        oang[3 * g] = bd.w[l].x; oang[3 * g + 1] = bd.w[l].y; oang[3 * g + 2] = bd.w[l].z;
+      }
+    }
+    if (!h) {
+      if (reset_rows) {  // frozen rows + obs from first_qp / first_obs
+        for (int k = 3 * POB_NDYN; k < 3 * N; ++k) {
+          opos[k] = in.first_pos[r3 + k]; ovel[k] = in.first_vel[r3 + k]; oang[k] = in.first_ang[r3 + k];
+        }
+        for (int k = 4 * POB_NDYN; k < 4 * N; ++k) orot[k] = in.first_rot[r4 + k];
+      }
+      if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+        for (int k = 0; k < 3 * N; ++k) {
+          out.first_pos[r3 + k] = in.first_pos[r3 + k]; out.first_vel[r3 + k] = in.first_vel[r3 + k];
+          out.first_ang[r3 + k] = in.first_ang[r3 + k];
+        }
+        for (int k = 0; k < 4 * N; ++k) out.first_rot[r4 + k] = in.first_rot[r4 + k];
+        for (int k = 0; k < D; ++k) out.first_obs[(size_t)b * D + k] = in.first_obs[(size_t)b * D + k];
+      }
+      out.reward[b] = t.reward;
+      out.done[b] = t.done;
+      if (out.steps) out.steps[b] = t.steps;
+      if (out.truncation) out.truncation[b] = t.trunc;
+      if (out.m0) out.m0[b] = t.m0;
+      if (out.m1) out.m1[b] = t.m1;
+      if (out.m2) out.m2[b] = t.m2;
+      out.rng[2 * b] = t.rng0;
+      out.rng[2 * b + 1] = t.rng1;
+    }
+  }
+  // obs row of a reset env: both lanes' obs writes are done (same wave, program order);
+  // lane 0 overwrites the whole row with first_obs
+  if (b < B && !h && (flags & POB_F_AUTORESET) && done != 0.0f) {
+    const int D = obs_dim<KIND>(S);
+    float *o = out.obs + (size_t)b * D;
+    for (int k = 0; k < D; ++k) o[k] = in.first_obs[(size_t)b * D + k];
+  }
+  if (out.any_done) {
+    const unsigned long long m = __ballot(!h && done != 0.0f);
     if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
   }
 }
@@ -592,6 +773,7 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   pob_env *e = new (std::nothrow) pob_env();
   if (!e) return fail(POB_ENOMEM, "out of host memory");
   e->params = prm;
+  if (const char *v = getenv("POB_STEP_LANES")) e->lanes_per_env = atoi(v) == 1 ? 1 : 2;
   if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
   int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
   if (rc) { delete e; return rc; }
@@ -674,10 +856,20 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   if ((flags & POB_F_EPISODE) && (!out->steps || !out->truncation)) return fail(POB_EINVAL, "EPISODE needs steps/truncation");
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
-  switch (e->sys.kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
-    default: hipLaunchKernelGGL((k_step<POB_TAG>), grid_for(B, 256), dim3(256), 0, st, (const void *)e->d_sys, B, pi, act, po, flags, episode_length); break;
+  const void *sp = (const void *)e->d_sys;
+  if (e->lanes_per_env == 2) {
+    const dim3 g = grid_for(2 * B, 256);
+    switch (e->sys.kind) {
+      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_pair<POB_HEAVENHELL>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      case POB_GATHER: hipLaunchKernelGGL((k_step_pair<POB_GATHER>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      default: hipLaunchKernelGGL((k_step_pair<POB_TAG>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+    }
+  } else {
+    switch (e->sys.kind) {
+      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      default: hipLaunchKernelGGL((k_step<POB_TAG>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+    }
   }
   return hip_check(hipGetLastError(), "k_step launch");
 }
