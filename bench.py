@@ -33,15 +33,22 @@ import torch.distributed as dist  # noqa: E402
 #           steps, truncation, 3 metrics, rng (2)
 #   writes: qp (117 f) + task bodies + obs (D) + reward, done, steps, truncation,
 #           3 metrics, rng (2)
-_TASK_READ = {"ant_heavenhell": 6, "ant_gather": 48, "ant_tag": 2}
-_TASK_WRITE = {"ant_heavenhell": 0, "ant_gather": 48, "ant_tag": 3}
-_OBS = {"ant_heavenhell": 114, "ant_gather": 211, "ant_tag": 103}
+_TASK_READ = {"ant_heavenhell": 6, "ant_gather": 48, "ant_tag": 2, "ant": 0}
+_TASK_WRITE = {"ant_heavenhell": 0, "ant_gather": 48, "ant_tag": 3, "ant": 0}
+_OBS = {"ant_heavenhell": 114, "ant_gather": 211, "ant_tag": 103, "ant": 87}
+MIXED = ("ant_heavenhell", "ant_gather", "ant_tag")  # --env mixed (BASELINE.json config 5)
 
 
-def bytes_per_env_step(name: str) -> int:
-    reads = 117 + _TASK_READ[name] + 8 + 1 + 1 + 1 + 3 + 2
-    writes = 117 + _TASK_WRITE[name] + _OBS[name] + 1 + 1 + 1 + 1 + 3 + 2
-    return 4 * (reads + writes)
+def bytes_per_env_step(name: str, qp_bytes: int = 4) -> int:
+    """qp elements (dynamic bodies + task bodies' positions) at qp_bytes, the rest float32."""
+    qp = (117 + _TASK_READ[name]) + (117 + _TASK_WRITE[name])
+    rest = (8 + 1 + 1 + 1 + 3 + 2) + (_OBS[name] + 1 + 1 + 1 + 1 + 3 + 2)
+    return qp_bytes * qp + 4 * rest
+
+
+def mixed_sizes(B: int):
+    base, rem = divmod(B, len(MIXED))
+    return [base + (1 if i < rem else 0) for i in range(len(MIXED))]
 
 
 def main() -> int:
@@ -49,7 +56,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--env", default="ant_heavenhell", choices=sorted(_OBS))
+    ap.add_argument("--env", default="ant_heavenhell", choices=sorted(_OBS) + ["mixed"],
+                    help="'mixed' = HH + GA + TAG batches (B split 3 ways) in one launch per step")
+    ap.add_argument("--qp-dtype", default="f32", choices=["f32", "f16"],
+                    help="qp storage (f16 = binary16 qp, float32 arithmetic)")
     ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--episode-length", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
@@ -75,9 +85,19 @@ def main() -> int:
     B = args.batch
     total = B * world
     lo, hi = shard_range(total, world, rank)
-    env = envs.create(args.env, batch_size=B, episode_length=args.episode_length, device=dev)
+    qp_dtype = torch.float16 if args.qp_dtype == "f16" else torch.float32
     key = jumpy.random_prngkey(0, device=dev)
-    state = env.reset(shard_keys(key, total, world, rank))
+    if args.env == "mixed":
+        # rank r owns global envs [lo, hi); within it the kinds follow one another
+        env = envs.create_mixed(MIXED, episode_length=args.episode_length, device=dev, qp_dtype=qp_dtype)
+        sizes = mixed_sizes(B)
+        keys = shard_keys(key, total, world, rank)
+        env.batch_sizes = sizes
+        state = [e.reset(keys[o:o + b].contiguous()) for e, o, b in zip(env.envs, env.offsets(), sizes)]
+    else:
+        env = envs.create(args.env, batch_size=B, episode_length=args.episode_length, device=dev,
+                          qp_dtype=qp_dtype)
+        state = env.reset(shard_keys(key, total, world, rank))
     act_key = jumpy.random_split(key, total + 1)[0].contiguous()  # VmapGymWrapper: key <- keys[0]
 
     T = args.warmup + args.steps
@@ -122,17 +142,18 @@ def main() -> int:
     wall, gpu_ms = float(elapsed[0]), float(elapsed[1])
     ms_per_step = 1e3 * wall / args.steps
     value = total * args.steps / wall
-    finite = bool(torch.isfinite(state.obs).all())
+    obs_last = torch.cat([s.obs.reshape(-1) for s in state]) if args.env == "mixed" else state.obs
+    finite = bool(torch.isfinite(obs_last).all())
 
     gather_ms = None
     if args.gather_obs and world > 1:
         from po_brax_amd.sharding import gather_obs
-        gather_obs(state.obs)
+        gather_obs(obs_last)
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
         for _ in range(5):
-            gather_obs(state.obs)
+            gather_obs(obs_last)
         torch.cuda.synchronize()
         gather_ms = 1e3 * (time.perf_counter() - g0) / 5
 
@@ -145,10 +166,12 @@ def main() -> int:
     # roofline of the dominant kernel (k_step): algorithmic bytes and FLOPs per launch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     kern_ms = sum(per) / len(per)
-    bpe = bytes_per_env_step(args.env)
+    qb = 2 if args.qp_dtype == "f16" else 4
+    kinds = list(zip(MIXED, mixed_sizes(B))) if args.env == "mixed" else [(args.env, B)]
+    bpe = sum(bytes_per_env_step(n, qb) * b for n, b in kinds) / B
     try:
         import orc  # test-infrastructure oracle: FLOP count of the restated algorithm only
-        fpe = orc.flops_per_env_step(args.env, B=64, steps=10)
+        fpe = sum(orc.flops_per_env_step(n, B=64, steps=10) * b for n, b in kinds) / B
     except Exception as ex:  # pragma: no cover
         print(f"flop count unavailable: {ex}", file=sys.stderr)
         fpe = float("nan")
@@ -157,15 +180,16 @@ def main() -> int:
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": 157.3, "unit": "TFLOP/s",
         "frac": round(tflops / 157.3, 5), "traffic": None,
-        "kernel": f"k_step<{args.env}>", "kernel_ms": round(kern_ms, 4),
-        "flops_per_env_step": round(fpe, 1), "bytes_per_env_step": bpe,
+        "kernel": "k_step_mixed" if args.env == "mixed" else f"k_step_pair<{args.env}>",
+        "kernel_ms": round(kern_ms, 4),
+        "flops_per_env_step": round(fpe, 1), "bytes_per_env_step": round(bpe, 1),
         "hbm": {"achieved": round(hbm_gbs, 2), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(hbm_gbs / 8000.0, 6)},
     }
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(args.env, args.cpu_seconds)
+        cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, args.cpu_seconds)
 
     line = {
         "metric": f"env-steps/sec {args.env} batch {B}/GPU",
@@ -174,9 +198,10 @@ def main() -> int:
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.env} B={B}/GPU, create(batch_size=B, episode_length="
                                f"{args.episode_length}) autoreset chain, PBD 10 substeps, random "
-                               "uniform(-1,1) actions (threefry)",
+                               "uniform(-1,1) actions (threefry)"
+                               + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else ""),
                    "env": args.env, "global_batch": total, "episode_length": args.episode_length,
-                   "parallelism": f"env-shard x{world}"},
+                   "qp_storage": args.qp_dtype, "parallelism": f"env-shard x{world}"},
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         "roofline": roofline, "cpu_baseline": cpu, "obs_finite": finite,
     }

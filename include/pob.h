@@ -7,6 +7,8 @@
  *   pob_env_create      AntHeavenHellEnv.__init__  po_brax/envs/ant_heavenhell.py:51-73
  *                       AntGatherEnv.__init__      po_brax/envs/ant_gather.py:59-91
  *                       AntTagEnv.__init__         po_brax/envs/ant_tag.py:38-61
+ *                       stock brax Ant             po_brax/envs/__init__.py:30 ('ant' ->
+ *                                                  brax.envs.ant.Ant, brax <= 0.0.12) [ext]
  *                       (+ brax.System(cfg) [ext], ActionRepeatWrapper wrappers.py:16-24)
  *   pob_reset           Env.reset: ant_heavenhell.py:75-103, ant_gather.py:93-123,
  *                       ant_tag.py:63-105 ; EpisodeWrapper.reset / AutoResetWrapper.reset
@@ -15,6 +17,8 @@
  *                       ant_tag.py:107-181, incl. brax System.step [ext] and the
  *                       Episode/AutoReset/RandomizedAutoReset wrappers (__init__.py:59-70,
  *                       wrappers.py:30-123)
+ *   pob_step_mixed      several of the above Env.step calls (different env kinds, one
+ *                       batch each) fused into ONE kernel launch (BASELINE.json config 5)
  *   pob_reset_where_done AutoresetVmapGymWrapper.step tail wrappers.py:245-262 and
  *                       RandomizedAutoResetWrapperNaive/OnTerminal wrappers.py:30-80
  *   pob_default_qp      System.default_qp(joint_angle, joint_velocity) [ext], called at
@@ -40,9 +44,14 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 1
+#define POB_ABI_VERSION 2
 
-enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2 };
+enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
+
+/* storage type of the qp tensors (pos/rot/vel/ang and first_qp); compute is float32 */
+enum pob_qp_storage { POB_QP_F32 = 0, POB_QP_F16 = 1 };
+
+#define POB_MIX_MAX 4 /* envs per pob_step_mixed launch */
 
 enum pob_status {
   POB_OK = 0,
@@ -81,9 +90,11 @@ typedef struct pob_params {
   float tag_dying_cost;               /* :44 */
   int action_repeat;                  /* ActionRepeatWrapper wrappers.py:16-24 */
   float solver_scale_pos, solver_scale_ang; /* PBD joint solver scales */
+  int qp_storage;                     /* pob_qp_storage (engine extension; default F32) */
 } pob_params;
 
-/* Env state: device pointers, batch-major.  Optional members may be NULL. */
+/* Env state: device pointers, batch-major.  Optional members may be NULL.  With
+ * qp_storage == POB_QP_F16 the qp and first_qp pointers address IEEE binary16 arrays. */
 typedef struct pob_state {
   float *pos, *rot, *vel, *ang; /* qp */
   float *obs;
@@ -109,6 +120,12 @@ int pob_env_default_angle(const pob_env *env, float *out8);
 int pob_reset(pob_env *env, int B, const uint32_t *keys, const pob_state *out, void *stream);
 int pob_step(pob_env *env, int B, const pob_state *in, const float *act, const pob_state *out,
              uint32_t flags, int episode_length, void *stream);
+/* One launch stepping n (<= POB_MIX_MAX) envs, env k over its own batch B[k] with its own
+ * state / action buffers; same semantics per env as pob_step.  All envs must live on the
+ * same device and share qp_storage. */
+int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *in,
+                   const float *const *act, const pob_state *out, uint32_t flags,
+                   int episode_length, void *stream);
 int pob_reset_where_done(pob_env *env, int B, int mode, const uint32_t *gym_key_in,
                          uint32_t *gym_key_out, const pob_state *s, void *stream);
 int pob_default_qp(pob_env *env, int B, const float *qpos, const float *qvel, float *pos, float *rot,

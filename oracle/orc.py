@@ -13,7 +13,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libpob_oracle.so")
-KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2}
+KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 F_EPISODE, F_AUTORESET = 1, 2
 
 

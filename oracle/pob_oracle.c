@@ -257,6 +257,8 @@ struct orc_env {
   orc_params p;
   /* GA */
   int n_grid; float grid[400][3]; float waiting[3];
+  /* stock ant: control dt (sys.config.dt as a float32 proto field) */
+  float ctrl_dt;
 };
 
 void orc_default_params(orc_params *p) {
@@ -338,6 +340,7 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
   int ar = p.action_repeat > 0 ? p.action_repeat : 1;
   double dt = f32d(0.05) * ar; int sub = 10 * ar; /* wrappers.py:21-23 */
   double hd = dt / sub;
+  e->ctrl_dt = (float)dt;
   e->substeps = sub;
   e->h = (float)hd; e->half_h = 0.5f * e->h; e->inv_h = (float)(1.0 / hd);
   e->lin_damp = (float)exp(0.0 * hd);
@@ -415,6 +418,10 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
       }
     e->n_grid = n;
     for (int c = 0; c < 3; ++c) e->waiting[c] = e->grid[n - 1][c] + p.ga_sensor_range * 2.0f;
+  } else if (kind == ORC_ANT) {
+    /* stock brax ant (brax <= 0.0.12 envs/ant.py, registered at po_brax/envs/__init__.py:30):
+     * bodies 0-8 + Ground, no arena; obs 13 qpos + 14 qvel + 60 cfrc = 87 */
+    e->N = 10; e->D = 87;
   } else {
     e->N = 12; e->D = 29 + 2 * 3 * 12 + 2;
     double x = p.tag_cage_xy[0] + 1.0, y = p.tag_cage_xy[1] + 1.0, r = 0.5 / 2;
@@ -783,11 +790,14 @@ static void angle_vel(const orc_env *e, const body_t *b, float *angle, float *av
   }
 }
 
-/* the 29 + 6N shared prefix (ant_*.py _get_obs) */
-static void obs_common(const orc_env *e, const body_t *b, const v3 *cvel, const v3 *cang, float *o) {
+/* the 29 + 6N shared prefix (ant_*.py _get_obs).  With sh = -2 it is the stock ant's
+ * 27 + 6N layout (brax envs/ant.py _get_obs: qp.pos[0, 2:] keeps only the torso z). */
+static void obs_common(const orc_env *e, const body_t *b, const v3 *cvel, const v3 *cang, float *o0, int sh) {
   float ja[NJ], jv[NJ];
   angle_vel(e, b, ja, jv);
-  o[0] = b->x[0].x; o[1] = b->x[0].y; o[2] = b->x[0].z;
+  float *o = o0 + sh;
+  if (sh == 0) { o[0] = b->x[0].x; o[1] = b->x[0].y; }
+  o[2] = b->x[0].z;
   o[3] = b->q[0].w; o[4] = b->q[0].x; o[5] = b->q[0].y; o[6] = b->q[0].z;
   for (int j = 0; j < NJ; ++j) o[7 + j] = ja[j];
   o[15] = b->v[0].x; o[16] = b->v[0].y; o[17] = b->v[0].z;
@@ -833,7 +843,8 @@ static void ga_readings(const orc_env *e, const float *pos, q4 rot0, const float
 /* per-env observation for the current env kind */
 static void env_obs(const orc_env *e, const body_t *b, const float *pos, const v3 *cvel, const v3 *cang,
                     float flag, const float *dists, float *o) {
-  obs_common(e, b, cvel, cang, o);
+  if (e->kind == ORC_ANT) { obs_common(e, b, cvel, cang, o, -2); return; }
+  obs_common(e, b, cvel, cang, o, 0);
   int base = 29 + 6 * e->N;
   if (e->kind == ORC_HH) {
     float tx = pos[3 * 11];
@@ -853,7 +864,7 @@ static void reset_one(const orc_env *e, const uint32_t key[2], float *pos, float
                       float *ang, float *obs, uint32_t *rng_out) {
   const float lo1 = -0.1f, hi1 = 0.1f;
   uint32_t ks[10];
-  int nsplit = e->kind == ORC_GA ? 4 : 5;
+  int nsplit = e->kind == ORC_GA ? 4 : (e->kind == ORC_ANT ? 3 : 5); /* ant.py: split(rng, 3) */
   orc_split(key, nsplit, ks);
   float noise[NJ], qpos[NJ], qvel[NJ];
   orc_uniform(ks + 2, NJ, &lo1, &hi1, 1, noise);
@@ -884,6 +895,8 @@ static void reset_one(const orc_env *e, const uint32_t key[2], float *pos, float
     for (int k = 0; k < no; ++k)
       dists[k] = dist2d(pos[0], pos[1], pos[3 * (11 + k)], pos[3 * (11 + k) + 1]);
     rng_out[0] = key[0]; rng_out[1] = key[1]; /* ant_gather.py:106 keeps the input key */
+  } else if (e->kind == ORC_ANT) {
+    rng_out[0] = ks[0]; rng_out[1] = ks[1]; /* not part of the stock ant's State */
   } else {
     float lo[2] = {-e->p.tag_cage_xy[0], -e->p.tag_cage_xy[1]};
     float hi[2] = {e->p.tag_cage_xy[0], e->p.tag_cage_xy[1]}, axy[2], txy[2];
@@ -949,6 +962,7 @@ static void step_one(const orc_env *e, int b, const orc_state *in, const float *
   if (flags & ORC_F_AUTORESET) { if (prev_done != 0.0f) steps = 0.0f; }
 
   body_t bd; load_body(e, pos, rot, vel, ang, &bd);
+  const float x_before = bd.x[0].x;
   v3 cv[NDYN], ca[NDYN];
   physics_step(e, &bd, act + (size_t)b * NJ, cv, ca);
   store_body(&bd, pos, rot, vel, ang);
@@ -987,6 +1001,25 @@ static void step_one(const orc_env *e, int b, const orc_state *in, const float *
     if (any_b && dead == 0.0f) reward = -1.0f;
     done = all_wait ? 1.0f : dead;
     m0 = (float)na_hit; m1 = (float)nb_hit;
+  } else if (e->kind == ORC_ANT) {
+    /* brax envs/ant.py step (brax <= 0.0.12) [ext, recalled]: forward velocity reward,
+     * .5 * sum(act^2) control cost, .5e-3 * sum(clip(contact.vel)^2), survive 1; done on
+     * torso height.  Sums run in row-major element order (parity unpinned vs XLA). */
+    const float *a = act + (size_t)b * NJ;
+    float sa = 0.0f;
+    for (int j = 0; j < NJ; ++j) sa = sa + a[j] * a[j];
+    const float ctrl = 0.5f * sa;
+    float sc = 0.0f;
+    for (int i = 0; i < NDYN; ++i) {
+      float cx = clip1(cv[i].x), cy = clip1(cv[i].y), cz = clip1(cv[i].z);
+      sc = sc + cx * cx; sc = sc + cy * cy; sc = sc + cz * cz;
+    }
+    const float contact = 0.0005f * sc;
+    const float forward = (bd.x[0].x - x_before) / e->ctrl_dt;
+    reward = ((forward - ctrl) - contact) + 1.0f;
+    done = dead;
+    env_obs(e, &bd, pos, cv, ca, 0.0f, NULL, obs);
+    m0 = ctrl; m1 = contact; m2 = forward;
   } else {
     reward = dead > 0.0f ? e->p.tag_dying_cost : 0.0f;
     /* _step_target (ant_tag.py:129-146) */

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-enum { ORC_HH = 0, ORC_GA = 1, ORC_TAG = 2 };
+enum { ORC_HH = 0, ORC_GA = 1, ORC_TAG = 2, ORC_ANT = 3 };
 
 typedef struct orc_params {
   /* AntHeavenHell (ant_heavenhell.py:51-56) */

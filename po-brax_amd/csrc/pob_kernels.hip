@@ -1,20 +1,25 @@
 // pob_kernels.hip -- fused rollout kernels + the C ABI of libpob.so (include/pob.h).
 //
-// Kernels (one lane = one environment; 64-env wavefront tiles; batch-major HBM layout):
-//   k_step<KIND>     physics (PBD) + per-env POMDP logic + obs + Episode/AutoReset wrappers
-//   k_reset<KIND>    threefry keys -> joint noise -> forward kinematics -> env placement
+// Kernels (batch-major HBM layout; qp stored as float32 or binary16, computed in float32):
+//   k_step_pair<KIND,QT> physics (PBD) + per-env POMDP logic + obs + Episode/AutoReset
+//                    wrappers, TWO lanes per environment (pob_pair.h) -- the default
+//   k_step_mixed<QT> the same body for up to POB_MIX_MAX envs of different kinds in ONE
+//                    launch (block ranges select the env; the task tail dispatches on kind)
+//   k_step<KIND>     one lane per environment (POB_STEP_LANES=1; float32 qp only)
+//   k_reset<KIND,BS,QT> threefry keys -> joint noise -> forward kinematics -> env placement
 //                    (HH goal swap / GA top-16-of-156 choice / TAG rejection loop) ->
 //                    sys.info contact -> obs; also the masked "reset where done" variants
 //   k_default_qp     System.default_qp(joint_angle, joint_velocity)
 //   k_split/k_uniform/k_actions/k_advance_key   jax.random on device
 //   k_obs_gather     standard_observability_masks column gather
 // Reference anchors are given per function; DESIGN.md has the data layout and roofline.
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <new>
 
 #include "../../include/pob.h"
@@ -37,7 +42,13 @@ struct pob_env {
   int lanes_per_env = 2;  // k_step_pair (default) or k_step (POB_STEP_LANES=1)
 };
 
+#define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
+
 // ---------------------------------------------------------------------------- state
+#define POB_STATE_FIELDS(X)                                                                    \
+  X(pos) X(rot) X(vel) X(ang) X(obs) X(reward) X(done) X(steps) X(truncation) X(m0) X(m1) X(m2) \
+  X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done)
+
 struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
   uint32_t *rng;
@@ -46,22 +57,53 @@ struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
 };
 static StatePtrs to_ptrs(const pob_state &s) {
   StatePtrs p;
-  p.pos = s.pos; p.rot = s.rot; p.vel = s.vel; p.ang = s.ang; p.obs = s.obs;
-  p.reward = s.reward; p.done = s.done; p.steps = s.steps; p.truncation = s.truncation;
-  p.m0 = s.m0; p.m1 = s.m1; p.m2 = s.m2; p.rng = s.rng;
-  p.first_pos = s.first_pos; p.first_rot = s.first_rot; p.first_vel = s.first_vel;
-  p.first_ang = s.first_ang; p.first_obs = s.first_obs; p.any_done = s.any_done;
+#define POB_CP(f) p.f = s.f;
+  POB_STATE_FIELDS(POB_CP)
+#undef POB_CP
   return p;
+}
+
+// qp storage: element i of a qp array (pos/rot/vel/ang, first_*) in float32 or binary16.
+// The float32 -> binary16 conversion is round-to-nearest-even (v_cvt_f16_f32), the same
+// rounding numpy's astype(float16) applies to the oracle's float32 results.
+template <typename QT> struct Q;
+template <> struct Q<float> {
+  static POB_D float ld(const float *p, size_t i) { return p[i]; }
+  static POB_D void st(float *p, size_t i, float v) { p[i] = v; }
+};
+template <> struct Q<__half> {
+  static POB_D float ld(const float *p, size_t i) { return __half2float(reinterpret_cast<const __half *>(p)[i]); }
+  static POB_D void st(float *p, size_t i, float v) { reinterpret_cast<__half *>(p)[i] = __float2half_rn(v); }
+};
+template <typename QT> POB_D v3 ld3(const float *p, size_t i) {
+  return V(Q<QT>::ld(p, i), Q<QT>::ld(p, i + 1), Q<QT>::ld(p, i + 2));
+}
+template <typename QT> POB_D void st3(float *p, size_t i, v3 v) {
+  Q<QT>::st(p, i, v.x); Q<QT>::st(p, i + 1, v.y); Q<QT>::st(p, i + 2, v.z);
+}
+template <typename QT> POB_D q4 ld4(const float *p, size_t i) {
+  q4 q; q.w = Q<QT>::ld(p, i); q.x = Q<QT>::ld(p, i + 1); q.y = Q<QT>::ld(p, i + 2); q.z = Q<QT>::ld(p, i + 3);
+  return q;
+}
+template <typename QT> POB_D void st4(float *p, size_t i, q4 q) {
+  Q<QT>::st(p, i, q.w); Q<QT>::st(p, i + 1, q.x); Q<QT>::st(p, i + 2, q.y); Q<QT>::st(p, i + 3, q.z);
+}
+// copy n qp elements (exact in either storage)
+template <typename QT> POB_D void cpq(float *dst, const float *src, size_t i, int n) {
+  for (int k = 0; k < n; ++k) Q<QT>::st(dst, i + k, Q<QT>::ld(src, i + k));
 }
 
 template <int KIND>
 POB_D int n_bodies(csys_t &S) {
-  return KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : S.N);
+  return KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : (KIND == POB_ANT ? 10 : S.N));
 }
 template <int KIND>
 POB_D int obs_dim(csys_t &S) {
-  return KIND == POB_HEAVENHELL ? 114 : (KIND == POB_TAG ? 103 : S.D);
+  return KIND == POB_HEAVENHELL ? 114 : (KIND == POB_TAG ? 103 : (KIND == POB_ANT ? 87 : S.D));
 }
+// obs header shift: the stock ant keeps only the torso z of qp.pos[0] (brax envs/ant.py
+// _get_obs: qp.pos[0, 2:]), so its layout is the po-env layout moved left by 2
+POB_D constexpr int obs_shift(int kind) { return kind == POB_ANT ? -2 : 0; }
 
 POB_D void load_body(const float *pos, const float *rot, const float *vel, const float *ang, Body &b) {
 #pragma unroll
@@ -72,13 +114,14 @@ POB_D void load_body(const float *pos, const float *rot, const float *vel, const
     b.w[i] = V(ang[3 * i], ang[3 * i + 1], ang[3 * i + 2]);
   }
 }
-POB_D void store_body(const Body &b, float *pos, float *rot, float *vel, float *ang) {
+template <typename QT>
+POB_D void store_body(const Body &b, float *pos, float *rot, float *vel, float *ang, size_t r3, size_t r4) {
 #pragma unroll
   for (int i = 0; i < POB_NDYN; ++i) {
-    pos[3 * i] = b.x[i].x; pos[3 * i + 1] = b.x[i].y; pos[3 * i + 2] = b.x[i].z;
-    rot[4 * i] = b.q[i].w; rot[4 * i + 1] = b.q[i].x; rot[4 * i + 2] = b.q[i].y; rot[4 * i + 3] = b.q[i].z;
-    vel[3 * i] = b.v[i].x; vel[3 * i + 1] = b.v[i].y; vel[3 * i + 2] = b.v[i].z;
-    ang[3 * i] = b.w[i].x; ang[3 * i + 1] = b.w[i].y; ang[3 * i + 2] = b.w[i].z;
+    st3<QT>(pos, r3 + 3 * i, b.x[i]);
+    st4<QT>(rot, r4 + 4 * i, b.q[i]);
+    st3<QT>(vel, r3 + 3 * i, b.v[i]);
+    st3<QT>(ang, r3 + 3 * i, b.w[i]);
   }
 }
 
@@ -91,29 +134,31 @@ POB_D float dist2d(float ax, float ay, float bx, float by) {
 // _get_obs prefix shared by the three envs (ant_heavenhell.py:125-158,
 // ant_gather.py:183-213, ant_tag.py:148-181): torso pos(3) rot(4) joint angles(8)
 // torso vel(3) ang(3) joint vels(8) clip(contact.vel) (N*3) clip(contact.ang) (N*3).
-// Joint angle/vel = sys.joints[0].angle_vel (a3).
+// Joint angle/vel = sys.joints[0].angle_vel (a3).  sh = -2: stock ant (torso z only).
 POB_D void write_obs_common(csys_t &S, int N, const Body &b, const v3 (&cv)[POB_NDYN],
-                            const v3 (&ca)[POB_NDYN], float *o) {
-  o[0] = b.x[0].x; o[1] = b.x[0].y; o[2] = b.x[0].z;
-  o[3] = b.q[0].w; o[4] = b.q[0].x; o[5] = b.q[0].y; o[6] = b.q[0].z;
+                            const v3 (&ca)[POB_NDYN], float *row, const int sh) {
+  if (sh == 0) { row[0] = b.x[0].x; row[1] = b.x[0].y; }
+  row[sh + 2] = b.x[0].z;
+  row[sh + 3] = b.q[0].w; row[sh + 4] = b.q[0].x; row[sh + 5] = b.q[0].y; row[sh + 6] = b.q[0].z;
 #pragma unroll
   for (int j = 0; j < POB_NJ; ++j) {
     const int p = jparent(j), c = jchild(j);
     v3 ap = qrot(SV(S.axis[j]), b.q[p]);
     const v3 ref = SV(S.ref[j]);
     v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
-    o[7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-    o[21 + j] = vdot(vsub(b.w[c], b.w[p]), ap);
+    row[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    row[sh + 21 + j] = vdot(vsub(b.w[c], b.w[p]), ap);
   }
-  o[15] = b.v[0].x; o[16] = b.v[0].y; o[17] = b.v[0].z;
-  o[18] = b.w[0].x; o[19] = b.w[0].y; o[20] = b.w[0].z;
+  row[sh + 15] = b.v[0].x; row[sh + 16] = b.v[0].y; row[sh + 17] = b.v[0].z;
+  row[sh + 18] = b.w[0].x; row[sh + 19] = b.w[0].y; row[sh + 20] = b.w[0].z;
+  float *o = row + (29 + sh);
 #pragma unroll
   for (int i = 0; i < POB_NDYN; ++i) {
-    o[29 + 3 * i] = clip1(cv[i].x); o[30 + 3 * i] = clip1(cv[i].y); o[31 + 3 * i] = clip1(cv[i].z);
-    o[29 + 3 * N + 3 * i] = clip1(ca[i].x); o[30 + 3 * N + 3 * i] = clip1(ca[i].y);
-    o[31 + 3 * N + 3 * i] = clip1(ca[i].z);
+    o[3 * i] = clip1(cv[i].x); o[1 + 3 * i] = clip1(cv[i].y); o[2 + 3 * i] = clip1(cv[i].z);
+    o[3 * N + 3 * i] = clip1(ca[i].x); o[1 + 3 * N + 3 * i] = clip1(ca[i].y);
+    o[2 + 3 * N + 3 * i] = clip1(ca[i].z);
   }
-  for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { o[29 + k] = 0.0f; o[29 + 3 * N + k] = 0.0f; }
+  for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { o[k] = 0.0f; o[3 * N + k] = 0.0f; }
 }
 
 // ant_gather.py:152-181 sensor readings, written straight into the obs row.  Scatter
@@ -137,18 +182,36 @@ POB_D void ga_reading_one(csys_t &S, int k, float ox, float oy, float dist, floa
   if (slot >= 0 && slot < 2 * S.ga_n_bins) o_rd[slot] = inten;
 }
 
+// stock ant costs (brax envs/ant.py step [ext]): .5 * sum(action^2) and
+// .5e-3 * sum(clip(contact.vel, -1, 1)^2), summed in row-major element order (the frozen
+// Ground row adds exact zeros and is skipped)
+POB_D float ant_ctrl_cost(const float *a8) {
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < POB_NJ; ++j) s = s + a8[j] * a8[j];
+  return 0.5f * s;
+}
+POB_D float ant_contact_add(float s, v3 c) {
+  const float cx = clip1(c.x), cy = clip1(c.y), cz = clip1(c.z);
+  s = s + cx * cx; s = s + cy * cy; s = s + cz * cz;
+  return s;
+}
+
 struct TaskOut {
   float reward, done, trunc, steps, m0, m1, m2;
   uint32_t rng0, rng1;
+  float xb, ctrl, contact;  // stock ant inputs: torso x before the step, costs
 };
 
 // Per-env POMDP logic after the physics (env.step minus System.step) + EpisodeWrapper:
 // reward / done / metrics / rng, the task part of the obs, and the task bodies' rows.
 // HH ant_heavenhell.py:106-123, GA ant_gather.py:125-150 (+ readings :152-181),
-// TAG ant_tag.py:107-146; EpisodeWrapper.step [ext].
-template <int KIND>
+// TAG ant_tag.py:107-146, stock ant brax envs/ant.py step [ext]; EpisodeWrapper.step [ext].
+// `pos` is the qp.pos array (QT storage), r3 the env's row offset, `o` its obs row.
+template <int KIND, typename QT>
 POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r3, const int N, const v3 x0,
                      const q4 q0, float *opos, float *o, const uint32_t flags, const int L, TaskOut &t) {
+  using QQ = Q<QT>;
   const float tz = x0.z;
   float dead = tz < 0.2f ? 1.0f : 0.0f;
   dead = tz > 1.0f ? 1.0f : dead;
@@ -159,14 +222,14 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
   if (KIND == POB_HEAVENHELL) {
     // ant_heavenhell.py:106-123
     reward = dead > 0.0f ? S.hh_dying_cost : 0.0f;
-    const float *ip = in.pos + r3;
-    bool in0 = dist2d(ip[33], ip[34], x0.x, x0.y) <= S.hh_visible_radius;  // Target (11)
-    bool in1 = dist2d(ip[36], ip[37], x0.x, x0.y) <= S.hh_visible_radius;  // Hell (12)
-    bool in2 = dist2d(ip[30], ip[31], x0.x, x0.y) <= S.hh_visible_radius;  // Priest (10)
+    const float *ip = in.pos;
+    bool in0 = dist2d(QQ::ld(ip, r3 + 33), QQ::ld(ip, r3 + 34), x0.x, x0.y) <= S.hh_visible_radius;  // Target
+    bool in1 = dist2d(QQ::ld(ip, r3 + 36), QQ::ld(ip, r3 + 37), x0.x, x0.y) <= S.hh_visible_radius;  // Hell
+    bool in2 = dist2d(QQ::ld(ip, r3 + 30), QQ::ld(ip, r3 + 31), x0.x, x0.y) <= S.hh_visible_radius;  // Priest
     if (in0) reward = 1.0f;
     if (in1) reward = -1.0f;
     done = reward != 0.0f ? 1.0f : 0.0f;
-    const float tx = ip[33];
+    const float tx = QQ::ld(ip, r3 + 33);
     const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
     o[base] = in2 ? sgn : 0.0f;
     m2 = done;  // metrics['hits']
@@ -175,18 +238,17 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     float *rd = o + base;
     ga_readings_begin(S, rd);
     const float ori = ga_orientation(q0);
-    const float *ip = in.pos + r3;
     int na_hit = 0, nb_hit = 0;
     bool any_a = false, any_b = false, all_wait = true;
     for (int k = 0; k < S.n_obj; ++k) {
-      const int row = 3 * (11 + k);
-      const float ox = ip[row], oy = ip[row + 1], oz = ip[row + 2];
+      const size_t row = r3 + 3 * (11 + k);
+      const float ox = QQ::ld(in.pos, row), oy = QQ::ld(in.pos, row + 1), oz = QQ::ld(in.pos, row + 2);
       const float dk = dist2d(x0.x, x0.y, ox, oy);
       ga_reading_one(S, k, ox, oy, dk, ori, rd);
       const bool c = dk <= S.ga_catch_range;
       float nx = ox, ny = oy, nz = oz;
       if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
-      opos[row] = nx; opos[row + 1] = ny; opos[row + 2] = nz;
+      QQ::st(opos, row, nx); QQ::st(opos, row + 1, ny); QQ::st(opos, row + 2, nz);
       if (k < S.ga_n_apples) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
       all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
     }
@@ -195,6 +257,12 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     if (any_b && dead == 0.0f) reward = -1.0f;
     done = all_wait ? 1.0f : dead;
     m0 = (float)na_hit; m1 = (float)nb_hit;
+  } else if (KIND == POB_ANT) {
+    // brax envs/ant.py step (brax <= 0.0.12) [ext]
+    const float forward = (x0.x - t.xb) / S.ctrl_dt;
+    reward = ((forward - t.ctrl) - t.contact) + 1.0f;
+    done = dead;
+    m0 = t.ctrl; m1 = t.contact; m2 = forward;  // reward_ctrl_cost / _contact_cost / _forward
   } else {
     // ant_tag.py:107-127, adversary _step_target :129-146
     reward = dead > 0.0f ? S.tag_dying_cost : 0.0f;
@@ -204,8 +272,7 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     uint32_t k20, k21;  // randint(rng1, (), 0, 4) = bits(split(rng1)[1]) % 4
     tf_split(c0, c1, 2u, 1u, k20, k21);
     const int ch = (int)(tf_elem(k20, k21, 1u, 0u) % 4u);
-    const float *ip = in.pos + r3;
-    const float ax = x0.x, ay = x0.y, tx = ip[30], ty = ip[31];
+    const float ax = x0.x, ay = x0.y, tx = QQ::ld(in.pos, r3 + 30), ty = QQ::ld(in.pos, r3 + 31);
     float vx = ax - tx, vy = ay - ty;
     const float nrm = sqrtf(vx * vx + vy * vy);
     vx = vx / nrm; vy = vy / nrm;
@@ -216,7 +283,7 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     else { cx = 0.0f; cy = 0.0f; }
     float nx = cx * S.tag_target_step + tx, ny = cy * S.tag_target_step + ty;
     if (fabsf(nx) > S.tag_cage_xy[0] || fabsf(ny) > S.tag_cage_xy[1]) { nx = tx; ny = ty; }
-    opos[30] = nx; opos[31] = ny; opos[32] = 1.0f;
+    QQ::st(opos, r3 + 30, nx); QQ::st(opos, r3 + 31, ny); QQ::st(opos, r3 + 32, 1.0f);
     rng0 = n0; rng1 = n1;
     const bool vis = dist2d(nx, ny, ax, ay) <= S.tag_visible_radius;
     o[base] = vis ? nx : 0.0f; o[base + 1] = vis ? ny : 0.0f;
@@ -235,10 +302,23 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
   t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
 }
 
+// task tail of a fixed kind, or (POB_MIXED) of the kind recorded in the env's table
+template <int KIND, typename QT>
+POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const int b, const size_t r3, const int N,
+                         const v3 x0, const q4 q0, float *opos, float *o, const uint32_t flags, const int L,
+                         TaskOut &t) {
+  if (KIND != POB_MIXED) { task_step<KIND, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t); return; }
+  if (kind == POB_HEAVENHELL) task_step<POB_HEAVENHELL, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
+  else if (kind == POB_GATHER) task_step<POB_GATHER, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
+  else if (kind == POB_TAG) task_step<POB_TAG, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
+  else task_step<POB_ANT, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
+}
+
 // ------------------------------------------------------------------------------ step
 // Fused step: brax AutoResetWrapper(VmapWrapper(EpisodeWrapper(ActionRepeat(env)))).step
 // (envs/__init__.py:59-70) with env.step = ant_heavenhell.py:106-123 /
 // ant_gather.py:125-150 / ant_tag.py:107-127 and System.step = physics_step().
+// One lane per env; float32 qp.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, const StatePtrs in,
                                               const float *__restrict__ act, const StatePtrs out,
@@ -262,6 +342,7 @@ __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, con
     if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && prev_done != 0.0f) steps = 0.0f;
     float m0 = in.m0 ? in.m0[b] : 0.0f, m1 = in.m1 ? in.m1[b] : 0.0f, m2 = in.m2 ? in.m2[b] : 0.0f;
     uint32_t rng0 = in.rng[2 * b], rng1 = in.rng[2 * b + 1];
+    const float xb = bd.x[0].x;
 
     physics_step(Sp, bd, a, Ls);
     v3 cv[POB_NDYN], ca[POB_NDYN];
@@ -282,12 +363,20 @@ __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, con
         for (int c = 0; c < 4; ++c) orot[4 * i + c] = in.rot[r4 + 4 * i + c];
       }
     }
-    store_body(bd, opos, orot, ovel, oang);
+    store_body<float>(bd, out.pos, out.rot, out.vel, out.ang, r3, r4);
 
-    write_obs_common(S, N, bd, cv, ca, o);
+    write_obs_common(S, N, bd, cv, ca, o, obs_shift(KIND));
     TaskOut t;
     t.steps = steps; t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
-    task_step<KIND>(S, in, b, r3, N, bd.x[0], bd.q[0], opos, o, flags, L, t);
+    t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
+    if (KIND == POB_ANT) {
+      t.ctrl = ant_ctrl_cost(a);
+      float sc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < POB_NDYN; ++i) sc = ant_contact_add(sc, cv[i]);
+      t.contact = 0.0005f * sc;
+    }
+    task_step<KIND, float>(S, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
     done = t.done;
     const float reward = t.reward, trunc = t.trunc;
     steps = t.steps; m0 = t.m0; m1 = t.m1; m2 = t.m2; rng0 = t.rng0; rng1 = t.rng1;
@@ -327,31 +416,30 @@ __global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, con
 // Same fused step with TWO lanes per env (pob_pair.h): lane h owns the torso (replica) and
 // bodies 4h+1..4h+4.  2 waves / SIMD (VGPR+AGPR <= 256, 65 LDS floats / lane).  Lane 0
 // runs the per-env POMDP tail; lane 1 writes its bodies' rows, joints and cfrc rows.
-template <int KIND>
-__global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const int B, const StatePtrs in,
-                                                      const float *__restrict__ act, const StatePtrs out,
-                                                      const uint32_t flags, const int L) {
-  __shared__ float lds[PL_FLOATS * 256];
-  csys_t *Sp = (csys_t *)(size_t)sysp;
+// gt = the pair-lane index within this env batch (2 b + h).
+template <int KIND, typename QT>
+POB_D void step_pair_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
+                          const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds) {
   csys_t &S = *Sp;
   const Lds Ls{lds, 256, (int)threadIdx.x};
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = gt >> 1;
   const bool h = (gt & 1) != 0;
   float done = 0.0f;
+  const int kind = KIND != POB_MIXED ? KIND : S.kind;
   if (b < B) {
     const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+    const int sh = obs_shift(kind);
     const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
     HBody bd;
 #pragma unroll
     for (int l = 0; l < PNB; ++l) {
       const int g = l == 0 ? 0 : l + (h ? 4 : 0);
-      bd.x[l] = vload(in.pos + r3 + 3 * g);
-      const float *rq = in.rot + r4 + 4 * g;
-      bd.q[l].w = rq[0]; bd.q[l].x = rq[1]; bd.q[l].y = rq[2]; bd.q[l].z = rq[3];
-      bd.v[l] = vload(in.vel + r3 + 3 * g);
-      bd.w[l] = vload(in.ang + r3 + 3 * g);
+      bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
+      bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
+      bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
+      bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
     }
+    const float xb = bd.x[0].x;
     float a[PNJ];
 #pragma unroll
     for (int jl = 0; jl < PNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + jl + (h ? 4 : 0)];
@@ -362,7 +450,6 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
 #pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) hpbd_substep(Sp, bd, a, Ls, h, (it & 1) != 0);
 
-    float *opos = out.pos + r3, *orot = out.rot + r4, *ovel = out.vel + r3, *oang = out.ang + r3;
     float *o = out.obs + (size_t)b * D;
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
@@ -372,37 +459,35 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
       const v3 ref = HSV(h, S.ref[jl], S.ref[jl + 4]);
       v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
       const int j = jl + (h ? 4 : 0);
-      o[7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-      o[21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
+      o[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      o[sh + 21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
     }
     // cfrc rows: lane 0 rows 0..4, lane 1 rows 5..8 and the zero rows of frozen bodies
+    float *oc = o + (29 + sh);
 #pragma unroll
     for (int l = 0; l < PNB; ++l) {
       if (l == 0 && h) continue;
       const int g = l == 0 ? 0 : l + (h ? 4 : 0);
       const v3 cv = Ls.get3(PL_CV(l)), ca = Ls.get3(PL_CA(l));
-      o[29 + 3 * g] = clip1(cv.x); o[30 + 3 * g] = clip1(cv.y); o[31 + 3 * g] = clip1(cv.z);
-      o[29 + 3 * N + 3 * g] = clip1(ca.x); o[30 + 3 * N + 3 * g] = clip1(ca.y); o[31 + 3 * N + 3 * g] = clip1(ca.z);
+      oc[3 * g] = clip1(cv.x); oc[1 + 3 * g] = clip1(cv.y); oc[2 + 3 * g] = clip1(cv.z);
+      oc[3 * N + 3 * g] = clip1(ca.x); oc[1 + 3 * N + 3 * g] = clip1(ca.y); oc[2 + 3 * N + 3 * g] = clip1(ca.z);
     }
     if (h) {
-      for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { o[29 + k] = 0.0f; o[29 + 3 * N + k] = 0.0f; }
+      for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { oc[k] = 0.0f; oc[3 * N + k] = 0.0f; }
     }
     TaskOut t;
     if (!h) {
-      o[0] = bd.x[0].x; o[1] = bd.x[0].y; o[2] = bd.x[0].z;
-      o[3] = bd.q[0].w; o[4] = bd.q[0].x; o[5] = bd.q[0].y; o[6] = bd.q[0].z;
-      o[15] = bd.v[0].x; o[16] = bd.v[0].y; o[17] = bd.v[0].z;
-      o[18] = bd.w[0].x; o[19] = bd.w[0].y; o[20] = bd.w[0].z;
+      if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
+      o[sh + 2] = bd.x[0].z;
+      o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
+      o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
+      o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
       if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
         for (int i = POB_NDYN; i < N; ++i) {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            opos[3 * i + c] = in.pos[r3 + 3 * i + c];
-            ovel[3 * i + c] = in.vel[r3 + 3 * i + c];
-            oang[3 * i + c] = in.ang[r3 + 3 * i + c];
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) orot[4 * i + c] = in.rot[r4 + 4 * i + c];
+          cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+          cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+          cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+          cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
         }
       }
       float steps = in.steps ? in.steps[b] : 0.0f;
@@ -410,7 +495,18 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
       t.steps = steps;
       t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
       t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
-      task_step<KIND>(S, in, b, r3, N, bd.x[0], bd.q[0], opos, o, flags, L, t);
+      t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
+      if (kind == POB_ANT) {
+        // full action row and contact rows 0..4 (own slots) then 5..8 (partner's slots)
+        t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
+        float sc = 0.0f;
+#pragma unroll
+        for (int l = 0; l < PNB; ++l) sc = ant_contact_add(sc, Ls.get3(PL_CV(l)));
+#pragma unroll
+        for (int l = 1; l < PNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(PL_CV(l), (int)threadIdx.x + 1));
+        t.contact = 0.0005f * sc;
+      }
+      task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
       done = t.done;
     }
     const float done_partner = pair_swap(done);  // all lanes of the pair active here
@@ -422,34 +518,29 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
       if (l == 0 && h) continue;
       const int g = l == 0 ? 0 : l + (h ? 4 : 0);
       if (reset_rows) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          opos[3 * g + c] = in.first_pos[r3 + 3 * g + c];
-          ovel[3 * g + c] = in.first_vel[r3 + 3 * g + c];
-          oang[3 * g + c] = in.first_ang[r3 + 3 * g + c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) orot[4 * g + c] = in.first_rot[r4 + 4 * g + c];
+        cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
+        cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
+        cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
+        cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
       } else {
-        opos[3 * g] = bd.x[l].x; opos[3 * g + 1] = bd.x[l].y; opos[3 * g + 2] = bd.x[l].z;
-        orot[4 * g] = bd.q[l].w; orot[4 * g + 1] = bd.q[l].x; orot[4 * g + 2] = bd.q[l].y; orot[4 * g + 3] = bd.q[l].z;
-        ovel[3 * g] = bd.v[l].x; ovel[3 * g + 1] = bd.v[l].y; ovel[3 * g + 2] = bd.v[l].z;
-        oang[3 * g] = bd.w[l].x; oang[3 * g + 1] = bd.w[l].y; oang[3 * g + 2] = bd.w[l].z;
+        st3<QT>(out.pos, r3 + 3 * g, bd.x[l]);
+        st4<QT>(out.rot, r4 + 4 * g, bd.q[l]);
+        st3<QT>(out.vel, r3 + 3 * g, bd.v[l]);
+        st3<QT>(out.ang, r3 + 3 * g, bd.w[l]);
       }
     }
     if (!h) {
-      if (reset_rows) {  // frozen rows + obs from first_qp / first_obs
-        for (int k = 3 * POB_NDYN; k < 3 * N; ++k) {
-          opos[k] = in.first_pos[r3 + k]; ovel[k] = in.first_vel[r3 + k]; oang[k] = in.first_ang[r3 + k];
-        }
-        for (int k = 4 * POB_NDYN; k < 4 * N; ++k) orot[k] = in.first_rot[r4 + k];
+      if (reset_rows) {  // frozen rows from first_qp
+        cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
       }
       if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-        for (int k = 0; k < 3 * N; ++k) {
-          out.first_pos[r3 + k] = in.first_pos[r3 + k]; out.first_vel[r3 + k] = in.first_vel[r3 + k];
-          out.first_ang[r3 + k] = in.first_ang[r3 + k];
-        }
-        for (int k = 0; k < 4 * N; ++k) out.first_rot[r4 + k] = in.first_rot[r4 + k];
+        cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
+        cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
+        cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
+        cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
         for (int k = 0; k < D; ++k) out.first_obs[(size_t)b * D + k] = in.first_obs[(size_t)b * D + k];
       }
       out.reward[b] = t.reward;
@@ -474,6 +565,67 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
     const unsigned long long m = __ballot(!h && done != 0.0f);
     if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
   }
+}
+
+template <int KIND, typename QT>
+__global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const int B, const StatePtrs in,
+                                                      const float *__restrict__ act, const StatePtrs out,
+                                                      const uint32_t flags, const int L) {
+  __shared__ float lds[PL_FLOATS * 256];
+  step_pair_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds);
+}
+
+// Mixed launch: segment k owns blocks [blk0_k, blk0_{k+1}); the segment index is
+// block-uniform, so every selected table pointer / state pointer stays scalar.
+struct MixSeg {
+  const void *sysp;
+  const float *act;
+  StatePtrs in, out;
+  int B, blk0;
+};
+struct MixArgs {
+  MixSeg s[POB_MIX_MAX];
+  int n;
+};
+static_assert(POB_MIX_MAX == 4, "pick_state selects among 4 segments");
+
+// force a (block-uniform) pointer into SGPRs: the table pointer feeds scalar loads
+POB_D const void *uniform_ptr(const void *p) {
+  const uint64_t v = (uint64_t)(size_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void *)(size_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <typename QT>
+__global__ __launch_bounds__(256, 2) void k_step_mixed(const MixArgs A, const uint32_t flags, const int L) {
+  __shared__ float lds[PL_FLOATS * 256];
+  const int bx = (int)blockIdx.x;
+  int seg = 0;
+#pragma unroll
+  for (int k = 1; k < POB_MIX_MAX; ++k)
+    if (k < A.n && bx >= A.s[k].blk0) seg = k;
+  seg = __builtin_amdgcn_readfirstlane(seg);
+#define POB_PICK(f) (seg == 0 ? A.s[0].f : (seg == 1 ? A.s[1].f : (seg == 2 ? A.s[2].f : A.s[3].f)))
+  StatePtrs in, out;
+#define POB_SEL(f) in.f = A.s[0].in.f; out.f = A.s[0].out.f;
+  POB_STATE_FIELDS(POB_SEL)
+#undef POB_SEL
+#pragma unroll
+  for (int k = 1; k < POB_MIX_MAX; ++k) {
+    if (seg == k) {
+#define POB_SEL(f) in.f = A.s[k].in.f; out.f = A.s[k].out.f;
+      POB_STATE_FIELDS(POB_SEL)
+#undef POB_SEL
+    }
+  }
+  const void *sysp = uniform_ptr(POB_PICK(sysp));
+  const float *act = POB_PICK(act);
+  const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
+#undef POB_PICK
+  step_pair_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                (bx - blk0) * 256 + (int)threadIdx.x, lds);
 }
 
 // ----------------------------------------------------------------------------- reset
@@ -536,12 +688,16 @@ POB_D void choice_topk(uint32_t k0, uint32_t k1, int n, int K, uint32_t *lds_key
   }
 }
 
-// Env.reset for one lane.  Writes qp rows (all N), obs; returns the new info['rng'].
-template <int KIND, int BS>
-POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *rot, float *vel,
-                      float *ang, float *o, uint32_t &rng0, uint32_t &rng1, uint32_t *lds_key, int *lds_idx) {
+// Env.reset for one lane.  Writes the qp rows (all N, QT storage) at r3/r4 and the obs
+// row (computed from the float32 state); returns the new info['rng'].
+template <int KIND, int BS, typename QT>
+POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *rot, float *vel, float *ang,
+                      const size_t r3, const size_t r4, float *o, uint32_t &rng0, uint32_t &rng1,
+                      uint32_t *lds_key, int *lds_idx) {
+  using QQ = Q<QT>;
   const int N = n_bodies<KIND>(S);
-  const uint32_t ns = KIND == POB_GATHER ? 4u : 5u;  // random_split(rng, 5 | 4)
+  // random_split(rng, 5) (HH, TAG) | 4 (GA) | 3 (stock ant, brax envs/ant.py reset)
+  const uint32_t ns = KIND == POB_GATHER ? 4u : (KIND == POB_ANT ? 3u : 5u);
   uint32_t r[5][2];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -557,36 +713,39 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
   Body bd;
   fk(S, qpos, qvel, bd);
   // frozen rows: default_qp values
+  const q4 qid = {1.0f, 0.0f, 0.0f, 0.0f};
   for (int i = POB_NDYN; i < N; ++i) {
-    pos[3 * i] = S.frozen_pos[i][0]; pos[3 * i + 1] = S.frozen_pos[i][1]; pos[3 * i + 2] = S.frozen_pos[i][2];
-    rot[4 * i] = 1.0f; rot[4 * i + 1] = 0.0f; rot[4 * i + 2] = 0.0f; rot[4 * i + 3] = 0.0f;
-    vel[3 * i] = 0.0f; vel[3 * i + 1] = 0.0f; vel[3 * i + 2] = 0.0f;
-    ang[3 * i] = 0.0f; ang[3 * i + 1] = 0.0f; ang[3 * i + 2] = 0.0f;
+    st3<QT>(pos, r3 + 3 * i, SV(S.frozen_pos[i]));
+    st4<QT>(rot, r4 + 4 * i, qid);
+    st3<QT>(vel, r3 + 3 * i, V(0.0f, 0.0f, 0.0f));
+    st3<QT>(ang, r3 + 3 * i, V(0.0f, 0.0f, 0.0f));
   }
+  float tx = 0.0f, ty = 0.0f;  // TAG target (obs uses the float32 values)
   if (KIND == POB_HEAVENHELL) {
     // ant_heavenhell.py:87-103
     const float ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, -0.5f, 0.5f);
     const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, 0.5f, 1.5f);
 #pragma unroll
     for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
-    pos[27] = pos[27] + ax; pos[28] = pos[28] + ay;  // Ground is in ant_indices
+    QQ::st(pos, r3 + 27, S.frozen_pos[9][0] + ax);  // Ground is in ant_indices
+    QQ::st(pos, r3 + 28, S.frozen_pos[9][1] + ay);
     uint32_t s0, s1, y0, y1;  // choice(rng3, hhp[:2], 2, replace=False)
     tf_split(r[3][0], r[3][1], 2u, 1u, s0, s1);
     threefry2x32(s0, s1, 0u, 1u, y0, y1);
     const int first = (y1 < y0) ? 1 : 0;
-    pos[33] = S.hh_hhp[first][0]; pos[34] = S.hh_hhp[first][1]; pos[35] = 1.0f;
-    pos[36] = S.hh_hhp[1 - first][0]; pos[37] = S.hh_hhp[1 - first][1]; pos[38] = 1.0f;
+    st3<QT>(pos, r3 + 33, V(S.hh_hhp[first][0], S.hh_hhp[first][1], 1.0f));
+    st3<QT>(pos, r3 + 36, V(S.hh_hhp[1 - first][0], S.hh_hhp[1 - first][1], 1.0f));
     rng0 = r[0][0]; rng1 = r[0][1];
   } else if (KIND == POB_GATHER) {
     // ant_gather.py:109-123
     choice_topk<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, lds_key, lds_idx);
     for (int k = 0; k < S.n_obj; ++k) {
       const int g = lds_idx[k * BS + threadIdx.x];
-      pos[3 * (11 + k)] = S.grid[3 * g];
-      pos[3 * (11 + k) + 1] = S.grid[3 * g + 1];
-      pos[3 * (11 + k) + 2] = k < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
+      st3<QT>(pos, r3 + 3 * (11 + k), V(S.grid[3 * g], S.grid[3 * g + 1], k < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2]));
     }
     rng0 = k0; rng1 = k1;  // ant_gather.py:106 stores the input key
+  } else if (KIND == POB_ANT) {
+    rng0 = r[0][0]; rng1 = r[0][1];  // (not part of the stock ant's State)
   } else {
     // ant_tag.py:63-105
     const float lo0 = -S.tag_cage_xy[0], lo1 = -S.tag_cage_xy[1];
@@ -594,10 +753,11 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
     const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, lo1, S.tag_cage_xy[1]);
 #pragma unroll
     for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
-    pos[27] = pos[27] + ax; pos[28] = pos[28] + ay;
+    QQ::st(pos, r3 + 27, S.frozen_pos[9][0] + ax);
+    QQ::st(pos, r3 + 28, S.frozen_pos[9][1] + ay);
     uint32_t q0 = r[4][0], q1 = r[4][1];
-    float tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
-    float ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
+    tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
+    ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
     for (int it = 0; it < 100000 && dist2d(tx, ty, ax, ay) <= S.tag_min_spawn_distance; ++it) {
       uint32_t n0, n1;
       tf_split(q0, q1, 2u, 1u, n0, n1);
@@ -605,13 +765,13 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
       tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
       ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
     }
-    pos[30] = tx; pos[31] = ty; pos[32] = 0.5f;
+    st3<QT>(pos, r3 + 30, V(tx, ty, 0.5f));
     rng0 = r[0][0]; rng1 = r[0][1];
   }
-  store_body(bd, pos, rot, vel, ang);
+  store_body<QT>(bd, pos, rot, vel, ang, r3, r4);
   v3 cv[POB_NDYN], ca[POB_NDYN];
   info_contact(&S, bd, cv, ca);
-  write_obs_common(S, N, bd, cv, ca, o);
+  write_obs_common(S, N, bd, cv, ca, o, obs_shift(KIND));
   const int base = 29 + 6 * N;
   if (KIND == POB_HEAVENHELL) {
     o[base] = 0.0f;  // priest_in_range = 0 at reset
@@ -620,17 +780,17 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
     ga_readings_begin(S, rd);
     const float ori = ga_orientation(bd.q[0]);
     for (int k = 0; k < S.n_obj; ++k) {
-      const float ox = pos[3 * (11 + k)], oy = pos[3 * (11 + k) + 1];
+      const int g = lds_idx[k * BS + threadIdx.x];
+      const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
       ga_reading_one(S, k, ox, oy, dist2d(bd.x[0].x, bd.x[0].y, ox, oy), ori, rd);
     }
-  } else {
-    const float tx = pos[30], ty = pos[31];
+  } else if (KIND == POB_TAG) {
     const bool vis = dist2d(tx, ty, bd.x[0].x, bd.x[0].y) <= S.tag_visible_radius;
     o[base] = vis ? tx : 0.0f; o[base + 1] = vis ? ty : 0.0f;
   }
 }
 
-template <int KIND, int BS>
+template <int KIND, int BS, typename QT>
 __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, const int mode,
                                               const uint32_t *__restrict__ keys, const uint32_t *gym_in,
                                               uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s) {
@@ -658,8 +818,8 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
   uint32_t rng0, rng1;
-  reset_lane<KIND, BS>(S, k0, k1, s.pos + r3, s.rot + r4, s.vel + r3, s.ang + r3, s.obs + (size_t)b * D,
-                       rng0, rng1, lds_key, lds_idx);
+  reset_lane<KIND, BS, QT>(S, k0, k1, s.pos, s.rot, s.vel, s.ang, r3, r4, s.obs + (size_t)b * D, rng0, rng1,
+                           lds_key, lds_idx);
   if (mode == RESET_FULL) {
     s.rng[2 * b] = rng0; s.rng[2 * b + 1] = rng1;
     s.reward[b] = 0.0f; s.done[b] = 0.0f;
@@ -669,10 +829,10 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     if (s.m1) s.m1[b] = 0.0f;
     if (s.m2) s.m2[b] = 0.0f;
     if (s.first_pos) {
-      for (int k = 0; k < 3 * N; ++k) {
-        s.first_pos[r3 + k] = s.pos[r3 + k]; s.first_vel[r3 + k] = s.vel[r3 + k]; s.first_ang[r3 + k] = s.ang[r3 + k];
-      }
-      for (int k = 0; k < 4 * N; ++k) s.first_rot[r4 + k] = s.rot[r4 + k];
+      cpq<QT>(s.first_pos, s.pos, r3, 3 * N);
+      cpq<QT>(s.first_vel, s.vel, r3, 3 * N);
+      cpq<QT>(s.first_ang, s.ang, r3, 3 * N);
+      cpq<QT>(s.first_rot, s.rot, r4, 4 * N);
       for (int k = 0; k < D; ++k) s.first_obs[(size_t)b * D + k] = s.obs[(size_t)b * D + k];
     }
   } else if (mode == RESET_GYM) {
@@ -700,7 +860,7 @@ __global__ void k_default_qp(const void *sysp, int B, const float *qpos, const f
   Body bd;
   fk(S, qp, qv, bd);
   const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
-  store_body(bd, pos + r3, rot + r4, vel + r3, ang + r3);
+  store_body<float>(bd, pos, rot, vel, ang, r3, r4);
   for (int i = POB_NDYN; i < N; ++i) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) { pos[r3 + 3 * i + c] = S.frozen_pos[i][c]; vel[r3 + 3 * i + c] = 0.0f; ang[r3 + 3 * i + c] = 0.0f; }
@@ -754,6 +914,28 @@ static int hip_check(hipError_t e, const char *what) {
 }
 static inline dim3 grid_for(int n, int bs) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
+// host-side launch helpers (kind / storage dispatch)
+template <typename QT>
+static void launch_reset(int kind, dim3 g, hipStream_t st, const void *sp, int B, int mode, const uint32_t *keys,
+                         const uint32_t *gin, uint32_t *gout, const uint32_t *flag, const StatePtrs &p) {
+  switch (kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
+    case POB_TAG: hipLaunchKernelGGL((k_reset<POB_TAG, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
+    default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
+  }
+}
+template <typename QT>
+static void launch_step_pair(int kind, dim3 g, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
+  switch (kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_pair<POB_HEAVENHELL, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_pair<POB_GATHER, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_pair<POB_TAG, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_pair<POB_ANT, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+  }
+}
+
 extern "C" {
 
 int pob_abi_version(void) { return POB_ABI_VERSION; }
@@ -775,6 +957,10 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   e->params = prm;
   if (const char *v = getenv("POB_STEP_LANES")) e->lanes_per_env = atoi(v) == 1 ? 1 : 2;
   if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
+  if (e->sys.qp_f16 && e->lanes_per_env != 2) {
+    delete e;
+    return fail(POB_EINVAL, "binary16 qp storage needs the two-lane step kernel (unset POB_STEP_LANES)");
+  }
   int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
   if (rc) { delete e; return rc; }
   rc = hip_check(hipMalloc(&e->d_scratch, 64), "hipMalloc(scratch)");
@@ -833,16 +1019,15 @@ int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, voi
     return fail(POB_EINVAL, "state: first_* pointers must be all set or all NULL");
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs p = to_ptrs(*out);
-  switch (e->sys.kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
-    default: hipLaunchKernelGGL((k_reset<POB_TAG, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, (int)RESET_FULL, keys, nullptr, nullptr, nullptr, p); break;
-  }
+  if (e->sys.qp_f16)
+    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
+  else
+    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
   return hip_check(hipGetLastError(), "k_reset launch");
 }
 
-int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out, uint32_t flags,
-             int episode_length, void *stream) {
+static int check_step(const pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out,
+                      uint32_t flags, int episode_length) {
   if (!e) return fail(POB_EINVAL, "env is NULL");
   if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
   if (!act) return fail(POB_EINVAL, "action is NULL");
@@ -854,24 +1039,56 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
        !out->first_pos || !out->first_rot || !out->first_vel || !out->first_ang || !out->first_obs))
     return fail(POB_EINVAL, "AUTORESET needs first_qp/first_obs in both states");
   if ((flags & POB_F_EPISODE) && (!out->steps || !out->truncation)) return fail(POB_EINVAL, "EPISODE needs steps/truncation");
+  return POB_OK;
+}
+
+int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out, uint32_t flags,
+             int episode_length, void *stream) {
+  if (int rc = check_step(e, B, in, act, out, flags, episode_length)) return rc;
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
   if (e->lanes_per_env == 2) {
     const dim3 g = grid_for(2 * B, 256);
-    switch (e->sys.kind) {
-      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_pair<POB_HEAVENHELL>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      case POB_GATHER: hipLaunchKernelGGL((k_step_pair<POB_GATHER>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      default: hipLaunchKernelGGL((k_step_pair<POB_TAG>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-    }
+    if (e->sys.qp_f16) launch_step_pair<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
+    else launch_step_pair<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
   } else {
+    const dim3 g = grid_for(B, 256);
     switch (e->sys.kind) {
-      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      default: hipLaunchKernelGGL((k_step<POB_TAG>), grid_for(B, 256), dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      case POB_TAG: hipLaunchKernelGGL((k_step<POB_TAG>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
+      default: hipLaunchKernelGGL((k_step<POB_ANT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
     }
   }
   return hip_check(hipGetLastError(), "k_step launch");
+}
+
+int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *in, const float *const *act,
+                   const pob_state *out, uint32_t flags, int episode_length, void *stream) {
+  if (n < 1 || n > POB_MIX_MAX) return fail(POB_EINVAL, "mixed step: 1 <= n <= POB_MIX_MAX envs");
+  if (!envs || !B || !in || !act || !out) return fail(POB_EINVAL, "NULL argument");
+  MixArgs A;
+  memset(&A, 0, sizeof(A));
+  A.n = n;
+  long long blk = 0;
+  for (int k = 0; k < n; ++k) {
+    const pob_env *e = envs[k];
+    if (int rc = check_step(e, B[k], &in[k], act[k], &out[k], flags, episode_length)) return rc;
+    if (e->lanes_per_env != 2) return fail(POB_EINVAL, "mixed step needs the two-lane step kernel");
+    if (e->sys.qp_f16 != envs[0]->sys.qp_f16) return fail(POB_EINVAL, "mixed step: envs must share qp_storage");
+    if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
+    MixSeg &s = A.s[k];
+    s.sysp = e->d_sys; s.act = act[k]; s.in = to_ptrs(in[k]); s.out = to_ptrs(out[k]);
+    s.B = B[k]; s.blk0 = (int)blk;
+    blk += (2LL * B[k] + 255) / 256;
+    if (blk > INT_MAX) return fail(POB_EINVAL, "mixed step: batch too large");
+  }
+  for (int k = n; k < POB_MIX_MAX; ++k) { A.s[k] = A.s[n - 1]; A.s[k].blk0 = INT_MAX; }
+  hipStream_t st = (hipStream_t)stream;
+  if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half>), dim3((unsigned)blk), dim3(256), 0, st, A, flags, episode_length);
+  else hipLaunchKernelGGL((k_step_mixed<float>), dim3((unsigned)blk), dim3(256), 0, st, A, flags, episode_length);
+  return hip_check(hipGetLastError(), "k_step_mixed launch");
 }
 
 int pob_reset_where_done(pob_env *e, int B, int mode, const uint32_t *gym_in, uint32_t *gym_out, const pob_state *s,
@@ -891,11 +1108,10 @@ int pob_reset_where_done(pob_env *e, int B, int mode, const uint32_t *gym_in, ui
     flag = e->d_scratch;
   }
   const int kmode = mode == POB_RESET_GYM ? RESET_GYM : RESET_OWN;
-  switch (e->sys.kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
-    default: hipLaunchKernelGGL((k_reset<POB_TAG, 64>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p); break;
-  }
+  if (e->sys.qp_f16)
+    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p);
+  else
+    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p);
   return hip_check(hipGetLastError(), "k_reset(where done) launch");
 }
 
@@ -908,7 +1124,8 @@ int pob_default_qp(pob_env *e, int B, const float *qpos, const float *qvel, floa
   switch (e->sys.kind) {
     case POB_HEAVENHELL: hipLaunchKernelGGL((k_default_qp<POB_HEAVENHELL>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
     case POB_GATHER: hipLaunchKernelGGL((k_default_qp<POB_GATHER>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
-    default: hipLaunchKernelGGL((k_default_qp<POB_TAG>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
+    case POB_TAG: hipLaunchKernelGGL((k_default_qp<POB_TAG>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
+    default: hipLaunchKernelGGL((k_default_qp<POB_ANT>), grid_for(B, 64), dim3(64), 0, st, (const void *)e->d_sys, B, qpos, qvel, pos, rot, vel, ang); break;
   }
   return hip_check(hipGetLastError(), "k_default_qp launch");
 }

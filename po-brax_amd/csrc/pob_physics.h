@@ -50,6 +50,9 @@ struct Lds {
   POB_D float get(int e) const { return base[e * stride + t]; }
   POB_D void set(int e, float v) const { base[e * stride + t] = v; }
   POB_D v3 get3(int e) const { return V(get(e), get(e + 1), get(e + 2)); }
+  POB_D v3 get3_lane(int e, int lane) const {  // another lane's slot (same wave)
+    return V(base[e * stride + lane], base[(e + 1) * stride + lane], base[(e + 2) * stride + lane]);
+  }
   POB_D void set3(int e, v3 v) const { set(e, v.x); set(e + 1, v.y); set(e + 2, v.z); }
   POB_D q4 get4(int e) const { q4 q; q.w = get(e); q.x = get(e + 1); q.y = get(e + 2); q.z = get(e + 3); return q; }
   POB_D void set4(int e, q4 q) const { set(e, q.w); set(e + 1, q.x); set(e + 2, q.y); set(e + 3, q.z); }

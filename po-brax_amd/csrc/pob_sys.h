@@ -46,5 +46,7 @@ struct pob_sys {
   float ga_catch_range, ga_sensor_range, ga_half_span, ga_bin_res, ga_dying_cost, ga_waiting[3];
   float tag_tag_radius, tag_visible_radius, tag_target_step, tag_min_spawn_distance;
   float tag_cage_xy[2], tag_dying_cost;
+  float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
+  int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)
   const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env
 };

@@ -106,13 +106,16 @@ void default_params(pob_params &p) {
 // Returns an error message or nullptr.  grid (GA) is filled separately by the caller.
 const char *build_system(int kind, const pob_params &p, pob_sys &s) {
   memset(&s, 0, sizeof(s));
-  if (kind < 0 || kind > 2) return "unknown env kind";
+  if (kind < 0 || kind > 3) return "unknown env kind";
   if (p.action_repeat < 1) return "action_repeat must be >= 1";
+  if (p.qp_storage != POB_QP_F32 && p.qp_storage != POB_QP_F16) return "unknown qp_storage";
   s.kind = kind;
+  s.qp_f16 = p.qp_storage == POB_QP_F16;
   const int ar = p.action_repeat;
   const double dt = f32d(0.05) * ar;
   const int sub = 10 * ar;
   const double hd = dt / sub;
+  s.ctrl_dt = (float)dt;
   s.substeps = sub;
   s.h = (float)hd; s.half_h = 0.5f * s.h; s.inv_h = (float)(1.0 / hd);
   s.lin_damp = (float)exp(0.0 * hd);
@@ -190,6 +193,10 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     s.ga_half_span = (float)((double)p.ga_sensor_span / 2.0);
     s.ga_bin_res = (float)((2.0 * ((double)p.ga_sensor_span / 2.0)) / p.ga_n_bins);
     s.ga_dying_cost = p.ga_dying_cost;
+  } else if (kind == POB_ANT) {
+    // stock brax ant (envs/ant.py, brax <= 0.0.12): the 9 ant bodies + Ground, no arena;
+    // obs = torso z, rot, joint angles (13) | torso vel, ang, joint vels (14) | cfrc (60)
+    s.N = 10; s.D = 27 + 6 * 10;
   } else {
     s.N = 12; s.D = 29 + 6 * 12 + 2;
     const double x = p.tag_cage_xy[0] + 1.0, y = p.tag_cage_xy[1] + 1.0, r = 0.5 / 2;

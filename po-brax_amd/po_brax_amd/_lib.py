@@ -18,7 +18,10 @@ LIB_PATH = os.environ.get("POB_LIB", os.path.join(HERE, "libpob.so"))
 POB_OK, POB_EINVAL, POB_EHIP, POB_ENOMEM = 0, -1, -2, -3
 F_EPISODE, F_AUTORESET, F_ZERO_STEPS_ON_DONE = 1, 2, 4
 RESET_GYM, RESET_OWN = 0, 1
-KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2}
+KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
+QP_F32, QP_F16 = 0, 1
+MIX_MAX = 4
+ABI_VERSION = 2
 
 
 class pob_params(C.Structure):
@@ -33,6 +36,7 @@ class pob_params(C.Structure):
         ("tag_target_step", C.c_float), ("tag_min_spawn_distance", C.c_float),
         ("tag_cage_xy", C.c_float * 2), ("tag_dying_cost", C.c_float),
         ("action_repeat", C.c_int), ("solver_scale_pos", C.c_float), ("solver_scale_ang", C.c_float),
+        ("qp_storage", C.c_int),
     ]
 
 
@@ -50,7 +54,7 @@ class pob_state(C.Structure):
 EXPORTS = (
     "pob_abi_version", "pob_last_error", "pob_default_params", "pob_env_create",
     "pob_env_destroy", "pob_env_dims", "pob_env_default_angle", "pob_reset", "pob_step",
-    "pob_reset_where_done", "pob_default_qp", "pob_random_split", "pob_random_uniform",
+    "pob_step_mixed", "pob_reset_where_done", "pob_default_qp", "pob_random_split", "pob_random_uniform",
     "pob_random_actions", "pob_obs_gather",
 )
 
@@ -76,12 +80,16 @@ def _load():
     lib.pob_reset.argtypes = [_VP, C.c_int, _VP, C.POINTER(pob_state), _VP]
     lib.pob_step.argtypes = [_VP, C.c_int, C.POINTER(pob_state), _VP, C.POINTER(pob_state),
                              C.c_uint32, C.c_int, _VP]
+    lib.pob_step_mixed.argtypes = [C.c_int, C.POINTER(_VP), C.POINTER(C.c_int), C.POINTER(pob_state),
+                                   C.POINTER(_VP), C.POINTER(pob_state), C.c_uint32, C.c_int, _VP]
     lib.pob_reset_where_done.argtypes = [_VP, C.c_int, C.c_int, _VP, _VP, C.POINTER(pob_state), _VP]
     lib.pob_default_qp.argtypes = [_VP, C.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
     lib.pob_random_split.argtypes = [_VP, C.c_int, C.c_int, C.c_int, _VP, _VP]
     lib.pob_random_uniform.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _VP, _VP]
     lib.pob_random_actions.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP]
     lib.pob_obs_gather.argtypes = [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP, _VP]
+    if lib.pob_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {lib.pob_abi_version()} != {ABI_VERSION}; rebuild it")
     for name in EXPORTS:
         if name not in ("pob_abi_version", "pob_last_error", "pob_env_destroy"):
             getattr(lib, name).restype = C.c_int

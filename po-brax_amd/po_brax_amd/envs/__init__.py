@@ -1,8 +1,10 @@
 """Env registry and factories -- the drop-in surface of ``po_brax.envs`` (__init__.py:29-121).
 
-Only the three partially observable Ant tasks run on the MI355X engine; the stock brax
-envs the reference re-exports (``ant``, ``fetch``, ``humanoid`` ...) are out of this path's
-scope and raise ``NotImplementedError`` when created.
+The three partially observable Ant tasks and the stock brax ``ant`` (whose 87-dim
+observation the masks of standard_observability_masks.py index) run on the MI355X engine;
+the other stock brax envs the reference re-exports (``fetch``, ``humanoid`` ...) are out of
+this path's scope and raise ``NotImplementedError`` when created.  ``create_mixed`` (an
+engine extension) steps several env batches with one kernel launch.
 """
 from __future__ import annotations
 
@@ -13,6 +15,8 @@ from .env import Env, State, QP, Wrapper, System
 from .ant_heavenhell import AntHeavenHellEnv
 from .ant_gather import AntGatherEnv
 from .ant_tag import AntTagEnv
+from .ant import AntEnv
+from .mixed import MixedEnv
 from . import wrappers
 from .wrappers import (VmapGymWrapper, AutoresetVmapGymWrapper, AutoresetGymWrapper, EvalGymWrapper,
                        ActionRepeatWrapper, EpisodeWrapper, VmapWrapper, VectorWrapper, AutoResetWrapper,
@@ -31,7 +35,7 @@ def _stock(name):
 
 
 _envs = {
-    'ant': _stock('ant'),
+    'ant': AntEnv,
     'ant_tag': AntTagEnv,
     'ant_heavenhell': AntHeavenHellEnv,
     'ant_gather': AntGatherEnv,
@@ -61,6 +65,14 @@ def create(env_name: str,
     if eval_metrics:
         env = wrappers.EvalWrapper(env)
     return env
+
+
+def create_mixed(env_names, episode_length: int = 1000, action_repeat: int = 1,
+                 auto_reset: bool = True, **kwargs) -> MixedEnv:
+    """MixedEnv of ``create(name, batch_size=1, ...)`` chains (one per name); batch sizes are
+    given to ``MixedEnv.reset``.  ``kwargs`` (e.g. ``qp_dtype``, ``device``) go to every env."""
+    return MixedEnv([create(n, episode_length=episode_length, action_repeat=action_repeat,
+                            auto_reset=auto_reset, batch_size=1, **kwargs) for n in env_names])
 
 
 def create_fn(env_name: str, **kwargs) -> Callable[..., Env]:

@@ -189,11 +189,20 @@ class PoBraxEnv(Env):
     reset_metrics: tuple = ()    # metric keys after reset (reference order)
     step_metrics: tuple = ()     # metric keys after step
     done_dtype = torch.float32
+    info_rng = True              # info['rng'] is part of the State (False: stock brax ant)
 
-    def __init__(self, device=None, **params):
+    def __init__(self, device=None, qp_dtype=torch.float32, **params):
+        """``qp_dtype`` (engine extension): storage type of qp / first_qp, float32 (the
+        reference's) or float16 (binary16 storage, float32 arithmetic in the kernels)."""
         self.device = torch.device(device if device is not None else "cuda")
         self._params = _lib.pob_params()
         check(lib.pob_default_params(C.byref(self._params)))
+        qp_dtype = {"float32": torch.float32, "float16": torch.float16, "f32": torch.float32,
+                    "f16": torch.float16}.get(qp_dtype, qp_dtype)
+        if qp_dtype not in (torch.float32, torch.float16):
+            raise ValueError(f"qp_dtype must be float32 or float16, got {qp_dtype}")
+        self.qp_dtype = qp_dtype
+        self._params.qp_storage = _lib.QP_F16 if qp_dtype == torch.float16 else _lib.QP_F32
         self._set_params(params)
         self._action_repeat = 1
         self._handle = None
@@ -238,9 +247,10 @@ class PoBraxEnv(Env):
     # ------------------------------------------------------------------ buffers
     def _empty(self, B: int, episode: bool, first: bool) -> dict:
         f = dict(dtype=torch.float32, device=self.device)
+        q = dict(dtype=self.qp_dtype, device=self.device)
         N, D = self._N, self._D
-        b = dict(pos=torch.empty((B, N, 3), **f), rot=torch.empty((B, N, 4), **f),
-                 vel=torch.empty((B, N, 3), **f), ang=torch.empty((B, N, 3), **f),
+        b = dict(pos=torch.empty((B, N, 3), **q), rot=torch.empty((B, N, 4), **q),
+                 vel=torch.empty((B, N, 3), **q), ang=torch.empty((B, N, 3), **q),
                  obs=torch.empty((B, D), **f), reward=torch.empty((B,), **f),
                  done=torch.empty((B,), **f), m0=torch.empty((B,), **f), m1=torch.empty((B,), **f),
                  m2=torch.empty((B,), **f),
@@ -249,8 +259,8 @@ class PoBraxEnv(Env):
             b["steps"] = torch.empty((B,), **f)
             b["truncation"] = torch.empty((B,), **f)
         if first:
-            b.update(first_pos=torch.empty((B, N, 3), **f), first_rot=torch.empty((B, N, 4), **f),
-                     first_vel=torch.empty((B, N, 3), **f), first_ang=torch.empty((B, N, 3), **f),
+            b.update(first_pos=torch.empty((B, N, 3), **q), first_rot=torch.empty((B, N, 4), **q),
+                     first_vel=torch.empty((B, N, 3), **q), first_ang=torch.empty((B, N, 3), **q),
                      first_obs=torch.empty((B, D), **f))
         return b
 
@@ -269,7 +279,7 @@ class PoBraxEnv(Env):
         b = dict(pos=state.qp.pos, rot=state.qp.rot, vel=state.qp.vel, ang=state.qp.ang,
                  obs=state.obs, reward=state.reward,
                  done=a.get("done", state.done.to(torch.float32)),
-                 rng=state.info["rng"])
+                 rng=state.info["rng"] if "rng" in state.info else a["rng"])
         for k in range(3):
             name = self.slot_names[k] if k < len(self.slot_names) else None
             t = a.get(f"m{k}")
@@ -288,6 +298,9 @@ class PoBraxEnv(Env):
         for k, t in b.items():
             if t is not None and not t.is_contiguous():
                 raise ValueError(f"state tensor {k} must be contiguous")
+        for k in ("pos", "rot", "vel", "ang", "first_pos", "first_rot", "first_vel", "first_ang"):
+            if b.get(k) is not None and b[k].dtype != self.qp_dtype:
+                raise ValueError(f"state tensor {k} is {b[k].dtype}; this env stores qp as {self.qp_dtype}")
         return b
 
     def _state_of(self, b: dict, after_step: bool, squeeze: bool) -> State:
@@ -297,8 +310,8 @@ class PoBraxEnv(Env):
         done = b["done"]
         if after_step and self.done_dtype is not torch.float32:
             done = done != 0
-        info = {"rng": b["rng"]}
-        aux = {"done": b["done"]}
+        info = {"rng": b["rng"]} if self.info_rng else {}
+        aux = {"done": b["done"], "rng": b["rng"]}
         for k in range(3):
             aux[f"m{k}"] = b[f"m{k}"]
         if "steps" in b:
@@ -369,8 +382,15 @@ class PoBraxEnv(Env):
                 for k in ("first_pos", "first_rot", "first_vel", "first_ang", "first_obs"):
                     bout[k] = bin_[k]
         ci, co = self._cstate(bin_), self._cstate(bout)
-        check(lib.pob_step(self._handle, B, C.byref(ci), act.data_ptr(), C.byref(co), flags,
-                           int(episode_length), _lib.stream_handle(self.device)))
+        if _CAPTURE is not None:
+            # MixedEnv collects the launch (envs/mixed.py) and builds the State after it:
+            # _state_of enqueues dtype conversions that must follow the kernel
+            _CAPTURE.append(dict(env=self, B=B, ci=ci, co=co, act=act, flags=flags,
+                                 episode_length=int(episode_length), bin=bin_, bout=bout, squeeze=squeeze))
+            return None
+        else:
+            check(lib.pob_step(self._handle, B, C.byref(ci), act.data_ptr(), C.byref(co), flags,
+                               int(episode_length), _lib.stream_handle(self.device)))
         return self._state_of(bout, True, squeeze)
 
     # helpers for the gym / randomized-autoreset wrappers
@@ -379,6 +399,10 @@ class PoBraxEnv(Env):
         cs = self._cstate(b)
         check(lib.pob_reset_where_done(self._handle, b["pos"].shape[0], mode, _lib.ptr(gym_in),
                                        _lib.ptr(gym_out), C.byref(cs), _lib.stream_handle(self.device)))
+
+
+# set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here
+_CAPTURE = None
 
 
 def as_key(rng) -> torch.Tensor:

@@ -18,7 +18,7 @@ import pob_np as P
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
-NAMES = ["ant_heavenhell", "ant_gather", "ant_tag"]
+NAMES = ["ant_heavenhell", "ant_gather", "ant_tag", "ant"]
 RTOL, ATOL = 1e-5, 1e-6
 EXACT = True  # measured: every float field of every step matches the oracle bit for bit
 
@@ -53,7 +53,7 @@ def _keys(B, seed=0):
 def _state_np(s):
     """GPU State -> oracle state dict (reference layout)."""
     d = dict(pos=_np(s.qp.pos), rot=_np(s.qp.rot), vel=_np(s.qp.vel), ang=_np(s.qp.ang), obs=_np(s.obs),
-             reward=_np(s.reward), done=_np(s.aux["done"]), rng=_np(s.info["rng"]).astype(np.uint32))
+             reward=_np(s.reward), done=_np(s.aux["done"]), rng=_np(s.aux["rng"]).astype(np.uint32))
     for k in range(3):
         d[f"m{k}"] = _np(s.aux[f"m{k}"])
     if "steps" in s.info:

@@ -30,7 +30,7 @@ def test_lib_exports_every_declared_symbol():
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(re.findall(r" T (pob_\w+)", out))
     assert set(_declared()) <= exported
-    assert lib.pob_abi_version() == 1
+    assert lib.pob_abi_version() == 2
 
 
 def test_python_binding_covers_header():
