@@ -30,7 +30,7 @@ def build(force: bool = False, count_flops: bool = False) -> str:
         os.makedirs(os.path.dirname(path), exist_ok=True)
         extra = ["-DORC_COUNT_FLOPS"] if count_flops else []
         subprocess.check_call([
-            "gcc", "-O2", "-std=c99", "-D_GNU_SOURCE", "-ffp-contract=off", "-fno-fast-math",
+            "gcc", "-O2", "-std=c99", "-D_GNU_SOURCE", "-ffp-contract=off", "-fno-fast-math", "-mfma",
             "-fopenmp", "-fPIC", "-shared", *extra, "-o", path, src, "-lm"])
     return path
 

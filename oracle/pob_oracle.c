@@ -64,46 +64,49 @@ static inline v3 vadd(v3 a, v3 b) { FL(3); return V(a.x + b.x, a.y + b.y, a.z + 
 static inline v3 vsub(v3 a, v3 b) { FL(3); return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline v3 vscl(v3 a, float s) { FL(3); return V(a.x * s, a.y * s, a.z * s); }
 static inline v3 vdivs(v3 a, float s) { FL(4); float inv = 1.0f / s; return V(a.x * inv, a.y * inv, a.z * inv); }
-static inline float vdot(v3 a, v3 b) { FL(5); return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* vector / quaternion helpers as fused multiply-add chains: fmaf() is correctly rounded
+ * (FMA3 with -mfma, libm otherwise) and matches the kernels' v_fma_f32 bit for bit.  FL()
+ * counts algorithmic flops (an FMA = 2). */
+static inline float vdot(v3 a, v3 b) { FL(5); return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline v3 vcross(v3 a, v3 b) {
   FL(9);
-  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return V(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
 /* brax.math.rotate: r = 2*(u.v)u + (s^2 - u.u) v + 2 s (u x v) */
 static inline v3 qrot(v3 v, q4 q) {
   FL(2 + 1 + 12 + 6); /* w*w, c-sub, s2, r (12), + s2*cr (6); vdot x2 and vcross count themselves */
   v3 u = V(q.x, q.y, q.z);
-  float t = vdot(u, v);
-  float c = q.w * q.w - vdot(u, u);
+  float t2 = 2.0f * vdot(u, v);
+  float c = fmaf(q.w, q.w, -vdot(u, u));
   float s2 = 2.0f * q.w;
   v3 cr = vcross(u, v);
-  v3 r = V(2.0f * (t * u.x) + c * v.x, 2.0f * (t * u.y) + c * v.y, 2.0f * (t * u.z) + c * v.z);
-  return V(r.x + s2 * cr.x, r.y + s2 * cr.y, r.z + s2 * cr.z);
+  return V(fmaf(t2, u.x, fmaf(c, v.x, s2 * cr.x)), fmaf(t2, u.y, fmaf(c, v.y, s2 * cr.y)),
+           fmaf(t2, u.z, fmaf(c, v.z, s2 * cr.z)));
 }
 /* brax.math.quat_mul */
 static inline q4 qmul(q4 u, q4 v) {
   FL(28);
   q4 r;
-  r.w = u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z;
-  r.x = u.w * v.x + u.x * v.w + u.y * v.z - u.z * v.y;
-  r.y = u.w * v.y - u.x * v.z + u.y * v.w + u.z * v.x;
-  r.z = u.w * v.z + u.x * v.y - u.y * v.x + u.z * v.w;
+  r.w = fmaf(-u.z, v.z, fmaf(-u.y, v.y, fmaf(-u.x, v.x, u.w * v.w)));
+  r.x = fmaf(-u.z, v.y, fmaf(u.y, v.z, fmaf(u.x, v.w, u.w * v.x)));
+  r.y = fmaf(u.z, v.x, fmaf(u.y, v.w, fmaf(-u.x, v.z, u.w * v.y)));
+  r.z = fmaf(u.z, v.w, fmaf(-u.y, v.x, fmaf(u.x, v.y, u.w * v.z)));
   return r;
 }
 /* quat_mul([0, a], q) with the zero terms dropped */
 static inline q4 qmul_vq(v3 a, q4 q) {
   FL(20);
   q4 r;
-  r.w = -(a.x * q.x) - a.y * q.y - a.z * q.z;
-  r.x = a.x * q.w + a.y * q.z - a.z * q.y;
-  r.y = -(a.x * q.z) + a.y * q.w + a.z * q.x;
-  r.z = a.x * q.y - a.y * q.x + a.z * q.w;
+  r.w = fmaf(-a.z, q.z, fmaf(-a.y, q.y, -(a.x * q.x)));
+  r.x = fmaf(-a.z, q.y, fmaf(a.y, q.z, a.x * q.w));
+  r.y = fmaf(a.z, q.x, fmaf(a.y, q.w, -(a.x * q.z)));
+  r.z = fmaf(a.z, q.w, fmaf(-a.y, q.x, a.x * q.y));
   return r;
 }
 static inline q4 qinv(q4 q) { q4 r = {q.w, -q.x, -q.y, -q.z}; return r; }
 static inline q4 qnormalize(q4 q) {
   FL(13);
-  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  float n = sqrtf(fmaf(q.z, q.z, fmaf(q.y, q.y, fmaf(q.x, q.x, q.w * q.w))));
   float inv = 1.0f / n;
   q4 r = {q.w * inv, q.x * inv, q.y * inv, q.z * inv};
   return r;

@@ -2,7 +2,9 @@
 //
 // Every expression here has a FIXED evaluation order and the library is compiled with
 // -ffp-contract=off, so results are reproducible IEEE-754 binary32 (add/sub/mul/div/sqrt
-// correctly rounded on gfx950).  Transcendentals use explicit polynomial forms instead of
+// and the explicit fused multiply-adds FMA() are correctly rounded on gfx950, and the
+// oracle spells the same fmaf() calls).  The vector / quaternion helpers are written as
+// chains of fused multiply-adds (one v_fma_f32 per product-sum term).  Transcendentals use explicit polynomial forms instead of
 // ocml so that the float results are a deterministic function of the inputs.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -13,48 +15,50 @@
 struct v3 { float x, y, z; };
 struct q4 { float w, x, y, z; };
 
+#define FMA(a, b, c) __builtin_fmaf((a), (b), (c))
+
 POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 POB_D v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 POB_D v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 POB_D v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
 POB_D v3 vdivs(v3 a, float s) { float inv = 1.0f / s; return V(a.x * inv, a.y * inv, a.z * inv); }
-POB_D float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+POB_D float vdot(v3 a, v3 b) { return FMA(a.z, b.z, FMA(a.y, b.y, a.x * b.x)); }
 POB_D v3 vcross(v3 a, v3 b) {
-  return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return V(FMA(a.y, b.z, -(a.z * b.y)), FMA(a.z, b.x, -(a.x * b.z)), FMA(a.x, b.y, -(a.y * b.x)));
 }
 POB_D v3 vload(const float *p) { return V(p[0], p[1], p[2]); }
 
 // brax.math.rotate(v, q) = 2 (u.v) u + (s^2 - u.u) v + 2 s (u x v)
 POB_D v3 qrot(v3 v, q4 q) {
   v3 u = V(q.x, q.y, q.z);
-  float t = vdot(u, v);
-  float c = q.w * q.w - vdot(u, u);
+  float t2 = 2.0f * vdot(u, v);
+  float c = FMA(q.w, q.w, -vdot(u, u));
   float s2 = 2.0f * q.w;
   v3 cr = vcross(u, v);
-  v3 r = V(2.0f * (t * u.x) + c * v.x, 2.0f * (t * u.y) + c * v.y, 2.0f * (t * u.z) + c * v.z);
-  return V(r.x + s2 * cr.x, r.y + s2 * cr.y, r.z + s2 * cr.z);
+  return V(FMA(t2, u.x, FMA(c, v.x, s2 * cr.x)), FMA(t2, u.y, FMA(c, v.y, s2 * cr.y)),
+           FMA(t2, u.z, FMA(c, v.z, s2 * cr.z)));
 }
 // brax.math.quat_mul
 POB_D q4 qmul(q4 u, q4 v) {
   q4 r;
-  r.w = u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z;
-  r.x = u.w * v.x + u.x * v.w + u.y * v.z - u.z * v.y;
-  r.y = u.w * v.y - u.x * v.z + u.y * v.w + u.z * v.x;
-  r.z = u.w * v.z + u.x * v.y - u.y * v.x + u.z * v.w;
+  r.w = FMA(-u.z, v.z, FMA(-u.y, v.y, FMA(-u.x, v.x, u.w * v.w)));
+  r.x = FMA(-u.z, v.y, FMA(u.y, v.z, FMA(u.x, v.w, u.w * v.x)));
+  r.y = FMA(u.z, v.x, FMA(u.y, v.w, FMA(-u.x, v.z, u.w * v.y)));
+  r.z = FMA(u.z, v.w, FMA(-u.y, v.x, FMA(u.x, v.y, u.w * v.z)));
   return r;
 }
 // quat_mul([0, a], q)
 POB_D q4 qmul_vq(v3 a, q4 q) {
   q4 r;
-  r.w = -(a.x * q.x) - a.y * q.y - a.z * q.z;
-  r.x = a.x * q.w + a.y * q.z - a.z * q.y;
-  r.y = -(a.x * q.z) + a.y * q.w + a.z * q.x;
-  r.z = a.x * q.y - a.y * q.x + a.z * q.w;
+  r.w = FMA(-a.z, q.z, FMA(-a.y, q.y, -(a.x * q.x)));
+  r.x = FMA(-a.z, q.y, FMA(a.y, q.z, a.x * q.w));
+  r.y = FMA(a.z, q.x, FMA(a.y, q.w, -(a.x * q.z)));
+  r.z = FMA(a.z, q.w, FMA(-a.y, q.x, a.x * q.y));
   return r;
 }
 POB_D q4 qinv(q4 q) { q4 r; r.w = q.w; r.x = -q.x; r.y = -q.y; r.z = -q.z; return r; }
 POB_D q4 qnormalize(q4 q) {
-  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  float n = sqrtf(FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w))));
   float inv = 1.0f / n;
   q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
   return r;
