@@ -24,6 +24,7 @@
 
 #include "../../include/pob.h"
 #include "pob_pair.h"
+#include "pob_quad.h"
 #include "pob_physics.h"
 
 namespace pob {
@@ -39,7 +40,7 @@ struct pob_env {
   float *d_grid = nullptr;
   uint32_t *d_scratch = nullptr;  // any-done word for pob_reset_where_done without a flag
   int device = 0;
-  int lanes_per_env = 2;  // k_step_pair (default) or k_step (POB_STEP_LANES=1)
+  int lanes_per_env = 4;  // k_step_quad (default), k_step_pair (POB_STEP_LANES=2), k_step (=1)
 };
 
 #define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
@@ -446,7 +447,7 @@ POB_D void step_pair_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 
 #pragma unroll
     for (int l = 0; l < PNB; ++l) { Ls.set3(PL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(PL_CA(l), V(0.0f, 0.0f, 0.0f)); }
-    const int iters = launder(Sp)->substeps / 2;
+    const int iters = Sp->substeps / 2;
 #pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) hpbd_substep(Sp, bd, a, Ls, h, (it & 1) != 0);
 
@@ -576,6 +577,177 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
                            (int)(blockIdx.x * blockDim.x + threadIdx.x), lds);
 }
 
+// ------------------------------------------------------------------ step, lane quads
+// Same fused step with FOUR lanes per env (pob_quad.h): lane k owns the torso (replica)
+// and leg k (bodies 2k+1, 2k+2).  39 LDS floats / lane.  Lane 0 runs the per-env POMDP
+// tail; every lane writes its bodies' rows, its joints' obs and its cfrc rows.
+// gt = the quad-lane index within this env batch (4 b + k).
+#ifndef POB_QUAD_MIN_WAVES
+#define POB_QUAD_MIN_WAVES 4
+#endif
+template <int KIND, typename QT>
+POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
+                          const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds) {
+  csys_t &S = *Sp;
+  const Lds Ls{lds, 256, (int)threadIdx.x};
+  const int b = gt >> 2;
+  const int k = gt & 3;
+  float done = 0.0f;
+  const int kind = KIND != POB_MIXED ? KIND : S.kind;
+  if (b < B) {
+    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+    const int sh = obs_shift(kind);
+    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+    QBody bd;
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      const int g = qbody_global(l, k);
+      bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
+      bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
+      bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
+      bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
+    }
+    const float xb = bd.x[0].x;
+    float a[QNJ];
+#pragma unroll
+    for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + 2 * k + jl];
+
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
+    const int iters = Sp->substeps / 2;
+#pragma nounroll
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, bd, a, Ls, k, (it & 1) != 0);
+
+    float *o = out.obs + (size_t)b * D;
+    // joint angle / velocity obs of this lane's joints (a3)
+#pragma unroll
+    for (int jl = 0; jl < QNJ; ++jl) {
+      const int p = jparent(jl), c = jchild(jl);
+      v3 ap = qrot(QJV(k, S.axis, jl), bd.q[p]);
+      const v3 ref = QJV(k, S.ref, jl);
+      v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
+      const int j = 2 * k + jl;
+      o[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      o[sh + 21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
+    }
+    // cfrc rows: lane k rows 2k+1, 2k+2 (lane 0 also the torso row); lane 3 the zero rows
+    float *oc = o + (29 + sh);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      const v3 cv = Ls.get3(QL_CV(l)), ca = Ls.get3(QL_CA(l));
+      oc[3 * g] = clip1(cv.x); oc[1 + 3 * g] = clip1(cv.y); oc[2 + 3 * g] = clip1(cv.z);
+      oc[3 * N + 3 * g] = clip1(ca.x); oc[1 + 3 * N + 3 * g] = clip1(ca.y); oc[2 + 3 * N + 3 * g] = clip1(ca.z);
+    }
+    if (k == 3) {
+      for (int q = 3 * POB_NDYN; q < 3 * N; ++q) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+    }
+    TaskOut t;
+    if (k == 0) {
+      if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
+      o[sh + 2] = bd.x[0].z;
+      o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
+      o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
+      o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
+      if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
+        for (int i = POB_NDYN; i < N; ++i) {
+          cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+          cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+          cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+          cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
+        }
+      }
+      float steps = in.steps ? in.steps[b] : 0.0f;
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
+      t.steps = steps;
+      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+      t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
+      if (kind == POB_ANT) {
+        // full action row; contact rows 0..8 = own slots 0..2, then lanes +1, +2, +3 slots 1..2
+        t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
+        float sc = 0.0f;
+#pragma unroll
+        for (int l = 0; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3(QL_CV(l)));
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+#pragma unroll
+          for (int l = 1; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(QL_CV(l), (int)threadIdx.x + q));
+        }
+        t.contact = 0.0005f * sc;
+      }
+      task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
+      done = t.done;
+    }
+    done = quad_bcast<0>(done);  // all lanes of the quad active here
+    const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+    // dynamic body rows: computed state, or first_qp when the AutoResetWrapper resets
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      if (reset_rows) {
+        cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
+        cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
+        cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
+        cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
+      } else {
+        st3<QT>(out.pos, r3 + 3 * g, bd.x[l]);
+        st4<QT>(out.rot, r4 + 4 * g, bd.q[l]);
+        st3<QT>(out.vel, r3 + 3 * g, bd.v[l]);
+        st3<QT>(out.ang, r3 + 3 * g, bd.w[l]);
+      }
+    }
+    if (k == 0) {
+      if (reset_rows) {  // frozen rows from first_qp
+        cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+        cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
+      }
+      if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+        cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
+        cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
+        cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
+        cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
+        for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
+      }
+      out.reward[b] = t.reward;
+      out.done[b] = t.done;
+      if (out.steps) out.steps[b] = t.steps;
+      if (out.truncation) out.truncation[b] = t.trunc;
+      if (out.m0) out.m0[b] = t.m0;
+      if (out.m1) out.m1[b] = t.m1;
+      if (out.m2) out.m2[b] = t.m2;
+      out.rng[2 * b] = t.rng0;
+      out.rng[2 * b + 1] = t.rng1;
+    }
+  }
+  // obs row of a reset env: every lane's obs writes are done (same wave, program order);
+  // lane 0 overwrites the whole row with first_obs
+  if (b < B && k == 0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+    const int D = obs_dim<KIND>(S);
+    float *o = out.obs + (size_t)b * D;
+    for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+  }
+  if (out.any_done) {
+    const unsigned long long m = __ballot(k == 0 && done != 0.0f);
+    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
+  }
+}
+
+template <int KIND, typename QT>
+__global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const void *sysp, const int B,
+                                                                       const StatePtrs in,
+                                                                       const float *__restrict__ act,
+                                                                       const StatePtrs out, const uint32_t flags,
+                                                                       const int L) {
+  __shared__ float lds[QL_FLOATS * 256];
+  step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds);
+}
+
 // Mixed launch: segment k owns blocks [blk0_k, blk0_{k+1}); the segment index is
 // block-uniform, so every selected table pointer / state pointer stays scalar.
 struct MixSeg {
@@ -598,9 +770,11 @@ POB_D const void *uniform_ptr(const void *p) {
   return (const void *)(size_t)(((uint64_t)hi << 32) | lo);
 }
 
-template <typename QT>
-__global__ __launch_bounds__(256, 2) void k_step_mixed(const MixArgs A, const uint32_t flags, const int L) {
-  __shared__ float lds[PL_FLOATS * 256];
+template <typename QT, int LANES>
+__global__ __launch_bounds__(256, LANES == 4 ? POB_QUAD_MIN_WAVES : 2) void k_step_mixed(const MixArgs A,
+                                                                                         const uint32_t flags,
+                                                                                         const int L) {
+  __shared__ float lds[(LANES == 4 ? QL_FLOATS : PL_FLOATS) * 256];
   const int bx = (int)blockIdx.x;
   int seg = 0;
 #pragma unroll
@@ -624,8 +798,12 @@ __global__ __launch_bounds__(256, 2) void k_step_mixed(const MixArgs A, const ui
   const float *act = POB_PICK(act);
   const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
 #undef POB_PICK
-  step_pair_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                                (bx - blk0) * 256 + (int)threadIdx.x, lds);
+  if (LANES == 4)
+    step_quad_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                  (bx - blk0) * 256 + (int)threadIdx.x, lds);
+  else
+    step_pair_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                  (bx - blk0) * 256 + (int)threadIdx.x, lds);
 }
 
 // ----------------------------------------------------------------------------- reset
@@ -926,6 +1104,16 @@ static void launch_reset(int kind, dim3 g, hipStream_t st, const void *sp, int B
   }
 }
 template <typename QT>
+static void launch_step_quad(int kind, dim3 g, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
+  switch (kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_quad<POB_TAG, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_quad<POB_ANT, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+  }
+}
+template <typename QT>
 static void launch_step_pair(int kind, dim3 g, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                              const float *act, const StatePtrs &po, uint32_t flags, int L) {
   switch (kind) {
@@ -955,11 +1143,14 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   pob_env *e = new (std::nothrow) pob_env();
   if (!e) return fail(POB_ENOMEM, "out of host memory");
   e->params = prm;
-  if (const char *v = getenv("POB_STEP_LANES")) e->lanes_per_env = atoi(v) == 1 ? 1 : 2;
+  if (const char *v = getenv("POB_STEP_LANES")) {
+    const int n = atoi(v);
+    e->lanes_per_env = n == 1 ? 1 : (n == 2 ? 2 : 4);
+  }
   if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
-  if (e->sys.qp_f16 && e->lanes_per_env != 2) {
+  if (e->sys.qp_f16 && e->lanes_per_env == 1) {
     delete e;
-    return fail(POB_EINVAL, "binary16 qp storage needs the two-lane step kernel (unset POB_STEP_LANES)");
+    return fail(POB_EINVAL, "binary16 qp storage needs a multi-lane step kernel (POB_STEP_LANES 2 or 4)");
   }
   int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
   if (rc) { delete e; return rc; }
@@ -1048,7 +1239,11 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  if (e->lanes_per_env == 2) {
+  if (e->lanes_per_env == 4) {
+    const dim3 g = grid_for(4 * B, 256);
+    if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
+    else launch_step_quad<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
+  } else if (e->lanes_per_env == 2) {
     const dim3 g = grid_for(2 * B, 256);
     if (e->sys.qp_f16) launch_step_pair<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
     else launch_step_pair<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
@@ -1075,19 +1270,26 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   for (int k = 0; k < n; ++k) {
     const pob_env *e = envs[k];
     if (int rc = check_step(e, B[k], &in[k], act[k], &out[k], flags, episode_length)) return rc;
-    if (e->lanes_per_env != 2) return fail(POB_EINVAL, "mixed step needs the two-lane step kernel");
+    if (e->lanes_per_env == 1) return fail(POB_EINVAL, "mixed step needs a multi-lane step kernel");
+    if (e->lanes_per_env != envs[0]->lanes_per_env) return fail(POB_EINVAL, "mixed step: envs must share lanes per env");
     if (e->sys.qp_f16 != envs[0]->sys.qp_f16) return fail(POB_EINVAL, "mixed step: envs must share qp_storage");
     if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
     MixSeg &s = A.s[k];
     s.sysp = e->d_sys; s.act = act[k]; s.in = to_ptrs(in[k]); s.out = to_ptrs(out[k]);
     s.B = B[k]; s.blk0 = (int)blk;
-    blk += (2LL * B[k] + 255) / 256;
+    blk += ((long long)envs[0]->lanes_per_env * B[k] + 255) / 256;
     if (blk > INT_MAX) return fail(POB_EINVAL, "mixed step: batch too large");
   }
   for (int k = n; k < POB_MIX_MAX; ++k) { A.s[k] = A.s[n - 1]; A.s[k].blk0 = INT_MAX; }
   hipStream_t st = (hipStream_t)stream;
-  if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half>), dim3((unsigned)blk), dim3(256), 0, st, A, flags, episode_length);
-  else hipLaunchKernelGGL((k_step_mixed<float>), dim3((unsigned)blk), dim3(256), 0, st, A, flags, episode_length);
+  const dim3 g((unsigned)blk);
+  if (envs[0]->lanes_per_env == 4) {
+    if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half, 4>), g, dim3(256), 0, st, A, flags, episode_length);
+    else hipLaunchKernelGGL((k_step_mixed<float, 4>), g, dim3(256), 0, st, A, flags, episode_length);
+  } else {
+    if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half, 2>), g, dim3(256), 0, st, A, flags, episode_length);
+    else hipLaunchKernelGGL((k_step_mixed<float, 2>), g, dim3(256), 0, st, A, flags, episode_length);
+  }
   return hip_check(hipGetLastError(), "k_step_mixed launch");
 }
 

@@ -18,6 +18,11 @@
 #pragma once
 #include "pob_physics.h"
 
+// The pair kernel's live set leaves room for the compiler to keep table values in
+// registers (measured +5 % over per-use scalar reloads), so its table accesses are NOT
+// laundered (cf. launder() in pob_physics.h, which the one-lane kernel needs).
+POB_D csys_t *plain_tbl(csys_t *p) { return p; }
+
 #define PNB 5  // local bodies per lane
 #define PNJ 4  // local joints per lane
 
@@ -72,7 +77,7 @@ POB_D int hground_index(int k, bool h) { return k == 0 ? 0 : (k + (h ? 2 : 0)); 
 POB_D void hdetect(csys_t *Sp, const HBody &b, HContacts &ct, const bool h) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    csys_t &S = *launder(Sp);
+    csys_t &S = *plain_tbl(Sp);
     const int l = hcontact_body(k);
     const int g0 = k == 0 ? 0 : k, g1 = k == 0 ? 0 : k + 2;
     v3 pe = vadd(b.x[l], qrot(HSV(h, S.ground_end[g0], S.ground_end[g1]), b.q[l]));
@@ -86,7 +91,7 @@ POB_D void hdetect(csys_t *Sp, const HBody &b, HContacts &ct, const bool h) {
       mn = V(fminf(mn.x, b.x[l].x), fminf(mn.y, b.x[l].y), fminf(mn.z, b.x[l].z));
       mx = V(fmaxf(mx.x, b.x[l].x), fmaxf(mx.y, b.x[l].y), fmaxf(mx.z, b.x[l].z));
     }
-    csys_t &S = *launder(Sp);
+    csys_t &S = *plain_tbl(Sp);
     const int nw = S.n_walls;
     for (int w = 0; w < nw; ++w) {
       const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
@@ -97,7 +102,7 @@ POB_D void hdetect(csys_t *Sp, const HBody &b, HContacts &ct, const bool h) {
 #pragma unroll
   for (int l = 0; l < PNB; ++l) {
     POB_FENCE();
-    csys_t &S = *launder(Sp);
+    csys_t &S = *plain_tbl(Sp);
     const int nend = (l == 0) ? 1 : 2;
     v3 pe[2];
 #pragma unroll
@@ -113,7 +118,7 @@ POB_D void hdetect(csys_t *Sp, const HBody &b, HContacts &ct, const bool h) {
 #pragma unroll
       for (int q = 0; q < nend; ++q) {
         v3 n;
-        float pen = sphere_box(*launder(Sp), w, pe[q], r, n);
+        float pen = sphere_box(*plain_tbl(Sp), w, pe[q], r, n);
         if (pen > best) { best = pen; bn = n; bsel = q == 1; }
       }
     }
@@ -154,7 +159,7 @@ POB_D void hcontact_position(csys_t *Sp, const HBody &b, const Lds &L, const HCo
     const int l = hcontact_body(k);
     const float pen = ct.pen[k];
     if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
+      csys_t &S = *plain_tbl(Sp);
       v3 e, n;
       float rad;
       hcontact_geom(S, ct, k, h, e, n, rad);
@@ -197,7 +202,7 @@ POB_D void hcontact_velocity(csys_t *Sp, const HBody &b, const HContacts &ct, co
     const int l = hcontact_body(k);
     const float pen = ct.pen[k];
     if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
+      csys_t &S = *plain_tbl(Sp);
       v3 e, n;
       float rad;
       hcontact_geom(S, ct, k, h, e, n, rad);
@@ -244,7 +249,7 @@ POB_D void qacc(q4 &a, q4 t) { a.w += t.w; a.x += t.x; a.y += t.y; a.z += t.z; }
 // for even jl the parent (torso) terms go to *tt instead
 POB_D void hjoint_position(csys_t *Sp, const HBody &b, const int jl, const bool h, v3 (&DX)[PNB], q4 (&DQ)[PNB],
                            TorsoTerms *tt) {
-  csys_t &S = *launder(Sp);
+  csys_t &S = *plain_tbl(Sp);
   const int p = jparent(jl), c = jchild(jl);
   const float imp = p == 0 ? S.inv_mass[0] : hsel(h, S.inv_mass[p], S.inv_mass[p + 4]);
   const float imc = hsel(h, S.inv_mass[c], S.inv_mass[c + 4]);
@@ -313,7 +318,7 @@ POB_D void hpbd_substep(csys_t *Sp, HBody &b, const float (&act)[PNJ], const Lds
     v3 tt[PNJ];
 #pragma unroll
     for (int jl = 0; jl < PNJ; ++jl) {
-      csys_t &S = *launder(Sp);
+      csys_t &S = *plain_tbl(Sp);
       const int p = jparent(jl), c = jchild(jl);
       v3 a = qrot(HSV(h, S.axis[jl], S.axis[jl + 4]), b.q[p]);
       v3 t = vscl(a, act[jl] * hsel(h, S.strength[jl], S.strength[jl + 4]));
@@ -333,7 +338,7 @@ POB_D void hpbd_substep(csys_t *Sp, HBody &b, const float (&act)[PNJ], const Lds
     dw[2] = vadd(V(0.0f, 0.0f, 0.0f), tt[1]);
     dw[3] = vsub(vadd(V(0.0f, 0.0f, 0.0f), tt[2]), tt[3]);
     dw[4] = vadd(V(0.0f, 0.0f, 0.0f), tt[3]);
-    csys_t &S = *launder(Sp);
+    csys_t &S = *plain_tbl(Sp);
 #pragma unroll
     for (int l = 0; l < PNB; ++l) {
       const v3 v = b.v[l], w = b.w[l];
@@ -395,7 +400,7 @@ POB_D void hpbd_substep(csys_t *Sp, HBody &b, const float (&act)[PNJ], const Lds
   }
   // 4. velocity projection
   {
-    csys_t &S = *launder(Sp);
+    csys_t &S = *plain_tbl(Sp);
 #pragma unroll
     for (int l = 0; l < PNB; ++l) {
       b.q[l] = qnormalize(b.q[l]);

@@ -33,12 +33,18 @@ struct Contacts {
 // (scalar-cache hits).
 typedef __attribute__((address_space(4))) const pob_sys csys_t;  // constant address space
 POB_D csys_t *launder(csys_t *p) {
+#ifndef POB_NO_LAUNDER
   asm volatile("" : "+s"(p));
+#endif
   return p;
 }
 // Scheduling fence between the independent joint / contact blocks: without it the machine
 // scheduler interleaves all of them for ILP and the live set blows past 512 registers.
+#ifdef POB_NO_FENCE
+#define POB_FENCE() ((void)0)
+#else
 #define POB_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 
 // Per-lane LDS scratch, lane-minor (element e of lane t at base[e * BS + t]): conflict-free
 // ds_read/ds_write_b32.  Holds what the substep keeps live but rarely touches: the

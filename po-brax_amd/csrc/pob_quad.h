@@ -1,0 +1,416 @@
+// pob_quad.h -- the PBD Ant step with FOUR lanes per environment (gfx950).
+//
+// Why: the two-lane kernel (pob_pair.h) runs 2 waves per SIMD and its VALU pipe is busy
+// about a third of the time -- the rest is dependency and memory latency that two waves
+// cannot cover (profiles/r1g_summary.md).  One leg per lane cuts the per-lane state to
+// three bodies (VGPRs and 39 LDS floats per lane), so four waves share each SIMD, and it
+// shortens every wave's instruction stream, which is what bounds small batches.
+//
+// Split: lane k (0..3) of an env's lane quad owns the torso (replicated in all four
+// lanes) and leg k: local body 0 = torso, 1 = Aux k+1 (global 2k+1), 2 = lower leg
+// (global 2k+2); local joint 0 = global 2k (torso -> aux), 1 = global 2k+1 (aux -> leg).
+// Leg tables are selected per lane from the scalar system table (4-way v_cndmask).
+// Every body's accumulations run in its owner lane in the oracle's order.  The torso's
+// cross-leg sums (actuator + damping torques of joints 0,2,4,6; the position corrections
+// those joints apply to the torso) are gathered with DPP quad broadcasts, and every lane
+// adds the four legs' terms in global joint order -- the exact left-to-right float order of
+// oracle/pob_oracle.c, so the four torso replicas stay bit-identical to the oracle's.
+#pragma once
+#include "pob_physics.h"
+
+#define QNB 3  // local bodies per lane
+#define QNJ 2  // local joints per lane
+
+struct QBody {
+  v3 x[QNB];
+  q4 q[QNB];
+  v3 v[QNB];
+  v3 w[QNB];
+};
+
+// value of quad lane J broadcast to the lane's quad (DPP quad_perm [J,J,J,J]).  Inline asm
+// so that it is never sunk into lane-masked control flow (a DPP read of a disabled lane
+// returns 0); the s_nop covers the VALU-write -> DPP-read hazard.
+template <int J>
+POB_D float quad_bcast(float x) {
+  float r;
+  if (J == 0)
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf" : "=&v"(r) : "v"(x));
+  else if (J == 1)
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf" : "=&v"(r) : "v"(x));
+  else if (J == 2)
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf" : "=&v"(r) : "v"(x));
+  else
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf" : "=&v"(r) : "v"(x));
+  return r;
+}
+// The same broadcast through the DPP builtin, for values consumed unconditionally in
+// straight-line code (the torso sums): the compiler then places the hazard wait states
+// and schedules the moves, instead of one s_nop per asm statement.
+template <int J>
+POB_D float quad_bcast_b(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), J * 0x55, 0xf, 0xf, false));
+}
+template <int J> POB_D v3 quad_bcast3(v3 a) { return V(quad_bcast_b<J>(a.x), quad_bcast_b<J>(a.y), quad_bcast_b<J>(a.z)); }
+template <int J> POB_D q4 quad_bcast4(q4 a) {
+  q4 r; r.w = quad_bcast_b<J>(a.w); r.x = quad_bcast_b<J>(a.x); r.y = quad_bcast_b<J>(a.y); r.z = quad_bcast_b<J>(a.z);
+  return r;
+}
+
+// leg-k select of four (scalar) table values
+POB_D float qsel(int k, float a0, float a1, float a2, float a3) {
+  return k < 2 ? (k == 0 ? a0 : a1) : (k == 2 ? a2 : a3);
+}
+// joint table row of local joint jl (global 2k + jl), body table row of local body l
+#define QJV(k, arr, jl) V(qsel(k, (arr)[jl][0], (arr)[(jl) + 2][0], (arr)[(jl) + 4][0], (arr)[(jl) + 6][0]), \
+                          qsel(k, (arr)[jl][1], (arr)[(jl) + 2][1], (arr)[(jl) + 4][1], (arr)[(jl) + 6][1]), \
+                          qsel(k, (arr)[jl][2], (arr)[(jl) + 2][2], (arr)[(jl) + 4][2], (arr)[(jl) + 6][2]))
+#define QJS(k, arr, jl) qsel(k, (arr)[jl], (arr)[(jl) + 2], (arr)[(jl) + 4], (arr)[(jl) + 6])
+#define QBS(k, arr, l) ((l) == 0 ? (arr)[0] : qsel(k, (arr)[l], (arr)[(l) + 2], (arr)[(l) + 4], (arr)[(l) + 6]))
+
+POB_D constexpr int qbody_global(int l, int k) { return l == 0 ? 0 : l + 2 * k; }
+
+// Per-lane LDS scratch (lane-minor): substep-start pose of the 3 local bodies (21 floats)
+// and their Info.contact accumulators (18 floats).
+#define QL_PX(l) (7 * (l))
+#define QL_PQ(l) (7 * (l) + 3)
+#define QL_CV(l) (21 + 6 * (l))
+#define QL_CA(l) (21 + 6 * (l) + 3)
+#define QL_FLOATS 39
+
+struct QContacts {
+  // [0] torso ground, [1] lower-leg ground, [2 + l] deepest wall contact of local capsule l
+  float pen[2 + QNB];
+  v3 n[QNB];
+  bool sel[QNB];
+};
+POB_D constexpr int qcontact_body(int c) { return c == 0 ? 0 : (c == 1 ? 2 : c - 2); }
+
+// capsule end point q of local body l (torso: the sphere centre)
+POB_D v3 qcap_end(csys_t &S, int k, int l, int q) {
+  if (l == 0) return SV(S.cap_end[0][q]);
+  return V(qsel(k, S.cap_end[l][q][0], S.cap_end[l + 2][q][0], S.cap_end[l + 4][q][0], S.cap_end[l + 6][q][0]),
+           qsel(k, S.cap_end[l][q][1], S.cap_end[l + 2][q][1], S.cap_end[l + 4][q][1], S.cap_end[l + 6][q][1]),
+           qsel(k, S.cap_end[l][q][2], S.cap_end[l + 2][q][2], S.cap_end[l + 4][q][2], S.cap_end[l + 6][q][2]));
+}
+// ground contact c (0 torso, 1 lower leg k = ground collider k + 1)
+POB_D v3 qground_end(csys_t &S, int k, int c) {
+  if (c == 0) return SV(S.ground_end[0]);
+  return V(qsel(k, S.ground_end[1][0], S.ground_end[2][0], S.ground_end[3][0], S.ground_end[4][0]),
+           qsel(k, S.ground_end[1][1], S.ground_end[2][1], S.ground_end[3][1], S.ground_end[4][1]),
+           qsel(k, S.ground_end[1][2], S.ground_end[2][2], S.ground_end[3][2], S.ground_end[4][2]));
+}
+POB_D float qground_r(csys_t &S, int k, int c) {
+  return c == 0 ? S.ground_r[0] : qsel(k, S.ground_r[1], S.ground_r[2], S.ground_r[3], S.ground_r[4]);
+}
+
+POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int l = qcontact_body(c);
+    v3 pe = vadd(b.x[l], qrot(qground_end(S, k, c), b.q[l]));
+    ct.pen[c] = qground_r(S, k, c) - pe.z;
+  }
+  uint32_t near_mask = 0u;
+  {
+    v3 mn = b.x[0], mx = b.x[0];
+#pragma unroll
+    for (int l = 1; l < QNB; ++l) {
+      mn = V(fminf(mn.x, b.x[l].x), fminf(mn.y, b.x[l].y), fminf(mn.z, b.x[l].z));
+      mx = V(fmaxf(mx.x, b.x[l].x), fmaxf(mx.y, b.x[l].y), fmaxf(mx.z, b.x[l].z));
+    }
+    const int nw = S.n_walls;
+    for (int w = 0; w < nw; ++w) {
+      const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
+                        mx.y >= S.wall_lo[w][1] && mn.z <= S.wall_hi[w][2] && mx.z >= S.wall_lo[w][2];
+      if (__any(near)) near_mask |= 1u << w;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) {
+    POB_FENCE();
+    const int nend = (l == 0) ? 1 : 2;
+    float best = 0.0f;
+    v3 bn = V(0.0f, 0.0f, 0.0f);
+    bool bsel = false;
+    if (near_mask != 0u) {
+      v3 pe[2];
+#pragma unroll
+      for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[l], qrot(qcap_end(S, k, l, q), b.q[l]));
+      const float r = QBS(k, S.cap_r, l);
+      const int nw = S.n_walls;
+      for (int w = 0; w < nw; ++w) {
+        if (!(near_mask & (1u << w))) continue;
+#pragma unroll
+        for (int q = 0; q < nend; ++q) {
+          v3 n;
+          float pen = sphere_box(S, w, pe[q], r, n);
+          if (pen > best) { best = pen; bn = n; bsel = q == 1; }
+        }
+      }
+    }
+    ct.pen[2 + l] = best;
+    ct.n[l] = bn;
+    ct.sel[l] = bsel;
+  }
+}
+
+POB_D void qcontact_geom(csys_t &S, const QContacts &ct, int c, const int k, v3 &e, v3 &n, float &r) {
+  if (c < 2) {
+    e = qground_end(S, k, c);
+    n = V(0.0f, 0.0f, 1.0f);
+    r = qground_r(S, k, c);
+  } else {
+    const int l = c - 2;
+    e = ct.sel[l] ? qcap_end(S, k, l, 1) : qcap_end(S, k, l, 0);
+    r = QBS(k, S.cap_r, l);
+    n = ct.n[l];
+  }
+}
+
+// contact processing order of one body = oracle order (ground contact first, then wall)
+POB_D void qcontact_position(csys_t &S, const QBody &b, const Lds &L, const QContacts &ct, const int k,
+                             v3 (&DX)[QNB], q4 (&DQ)[QNB]) {
+#pragma unroll
+  for (int c = 0; c < 2 + QNB; ++c) {
+    POB_FENCE();
+    const int l = qcontact_body(c);
+    const float pen = ct.pen[c];
+    if (pen > 0.0f) {
+      v3 e, n;
+      float rad;
+      qcontact_geom(S, ct, c, k, e, n, rad);
+      const float im = QBS(k, S.inv_mass, l);
+      v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
+      v3 cp = vsub(pe, vscl(n, rad));
+      v3 rr = vsub(cp, b.x[l]);
+      v3 cn = vcross(rr, n);
+      float w = im + vdot(cn, cn);
+      float lam = pen / w;
+      v3 P = vscl(n, lam);
+      q4 dq = qmul_vq(vcross(rr, P), b.q[l]);
+      DX[l] = vadd(DX[l], vscl(P, im));
+      DQ[l].w += 0.5f * dq.w; DQ[l].x += 0.5f * dq.x; DQ[l].y += 0.5f * dq.y; DQ[l].z += 0.5f * dq.z;
+      v3 cprev = vadd(L.get3(QL_PX(l)), qrot(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l))));
+      v3 dp = vsub(cp, cprev);
+      v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
+      float lt = sqrtf(vdot(dpt, dpt));
+      if (lt > 0.0f) {
+        v3 t = vdivs(dpt, lt);
+        v3 ctn = vcross(rr, t);
+        float wt = im + vdot(ctn, ctn);
+        float lamt = lt / wt;
+        if (lamt < S.friction * lam) {
+          v3 Pt = vscl(t, -lamt);
+          q4 dqt = qmul_vq(vcross(rr, Pt), b.q[l]);
+          DX[l] = vadd(DX[l], vscl(Pt, im));
+          DQ[l].w += 0.5f * dqt.w; DQ[l].x += 0.5f * dqt.x; DQ[l].y += 0.5f * dqt.y; DQ[l].z += 0.5f * dqt.z;
+        }
+      }
+    }
+  }
+}
+
+POB_D void qcontact_velocity(csys_t &S, const QBody &b, const QContacts &ct, const int k, v3 (&dV)[QNB],
+                             v3 (&dW)[QNB]) {
+#pragma unroll
+  for (int c = 0; c < 2 + QNB; ++c) {
+    POB_FENCE();
+    const int l = qcontact_body(c);
+    const float pen = ct.pen[c];
+    if (pen > 0.0f) {
+      v3 e, n;
+      float rad;
+      qcontact_geom(S, ct, c, k, e, n, rad);
+      const float im = QBS(k, S.inv_mass, l);
+      v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
+      v3 cp = vsub(pe, vscl(n, rad));
+      v3 rr = vsub(cp, b.x[l]);
+      v3 vr = vadd(b.v[l], vcross(b.w[l], rr));
+      float vn = vdot(vr, n);
+      v3 vt = vsub(vr, vscl(n, vn));
+      float lt = sqrtf(vdot(vt, vt));
+      v3 dv = V(0.0f, 0.0f, 0.0f);
+      if (lt > 0.0f) {
+        float fr = fminf(S.friction * pen * S.inv_h, lt);
+        dv = vscl(vt, -(fr / lt));
+      }
+      if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+      float D = sqrtf(vdot(dv, dv));
+      if (D > 0.0f) {
+        v3 dh = vdivs(dv, D);
+        v3 cd = vcross(rr, dh);
+        float w = im + vdot(cd, cd);
+        v3 P = vdivs(dv, w);
+        dV[l] = vadd(dV[l], vscl(P, im));
+        dW[l] = vadd(dW[l], vcross(rr, P));
+      }
+    }
+  }
+}
+
+// torso terms of the lane's hip joint (global 2k): what the oracle adds to DX[0] / DQ[0]
+struct QTorso {
+  v3 dx;             // point constraint: P * imp (zero if the anchors coincide)
+  q4 dqp, dqh, dql;  // point, hinge and limit rotation terms (+0.5 * dq)
+};
+POB_D q4 qhalf(q4 d, float sign) {
+  q4 r; r.w = sign * (0.5f * d.w); r.x = sign * (0.5f * d.x); r.y = sign * (0.5f * d.y); r.z = sign * (0.5f * d.z);
+  return r;
+}
+POB_D void q4acc(q4 &a, q4 t) { a.w += t.w; a.x += t.x; a.y += t.y; a.z += t.z; }
+
+// local joint jl's point / hinge / limit corrections into DX/DQ (local bodies); for the
+// hip (jl = 0) the torso terms go to *tt
+POB_D void qjoint_position(csys_t &S, const QBody &b, const int jl, const int k, v3 (&DX)[QNB], q4 (&DQ)[QNB],
+                           QTorso *tt) {
+  const int p = jparent(jl), c = jchild(jl);
+  const float imp = QBS(k, S.inv_mass, p);
+  const float imc = QBS(k, S.inv_mass, c);
+  const bool torso_parent = p == 0;
+  v3 rp = qrot(QJV(k, S.off_p, jl), b.q[p]);
+  v3 rc = qrot(QJV(k, S.off_c, jl), b.q[c]);
+  v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
+  float L = sqrtf(vdot(d, d));
+  if (torso_parent) {
+    tt->dx = V(0.0f, 0.0f, 0.0f);
+    tt->dqp.w = tt->dqp.x = tt->dqp.y = tt->dqp.z = 0.0f;
+  }
+  if (L > 0.0f) {
+    v3 n = vdivs(d, L);
+    v3 cp = vcross(rp, n), cc = vcross(rc, n);
+    float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
+    float lam = (L / wsum) * S.s_pos;
+    v3 P = vscl(n, lam);
+    if (torso_parent) {
+      tt->dx = vscl(P, imp);
+      tt->dqp = qhalf(qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
+    } else {
+      DX[p] = vadd(DX[p], vscl(P, imp));
+      qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
+    }
+    DX[c] = vsub(DX[c], vscl(P, imc));
+    qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
+  }
+  const v3 axis = QJV(k, S.axis, jl);
+  v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
+  v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+  if (torso_parent) tt->dqh = qhalf(qmul_vq(Pa, b.q[p]), 1.0f);
+  else qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
+  qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
+  const v3 ref = QJV(k, S.ref, jl);
+  v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
+  float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+  const float lo = QJS(k, S.lim_lo, jl), hi = QJS(k, S.lim_hi, jl);
+  float dl = 0.0f;
+  if (psi < lo) dl = psi - lo;
+  else if (psi > hi) dl = psi - hi;
+  v3 Pl = vscl(ap, dl * S.half_s_ang);
+  if (torso_parent) tt->dql = qhalf(qmul_vq(Pl, b.q[p]), 1.0f);
+  else qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
+  qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
+}
+
+// add quad lane J's hip terms onto the torso accumulators (global joint 2J)
+template <int J>
+POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t) {
+  dx = vadd(dx, quad_bcast3<J>(t.dx));
+  q4acc(dq, quad_bcast4<J>(t.dqp));
+  q4acc(dq, quad_bcast4<J>(t.dqh));
+  q4acc(dq, quad_bcast4<J>(t.dql));
+}
+
+// One XPBD substep on a lane quad (see the header comment for the split).
+POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds &L, const int k,
+                        const bool COLLIDE) {
+  csys_t &S = *Sp;
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
+  // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
+  {
+    v3 tt[QNJ];
+#pragma unroll
+    for (int jl = 0; jl < QNJ; ++jl) {
+      const int p = jparent(jl), c = jchild(jl);
+      v3 a = qrot(QJV(k, S.axis, jl), b.q[p]);
+      v3 t = vscl(a, act[jl] * QJS(k, S.strength, jl));
+      v3 d = vscl(vsub(b.w[p], b.w[c]), QJS(k, S.jdamp, jl));
+      tt[jl] = vadd(t, d);
+    }
+    v3 dw[QNB];
+    {
+      const v3 t0 = quad_bcast3<0>(tt[0]), t2 = quad_bcast3<1>(tt[0]);
+      const v3 t4 = quad_bcast3<2>(tt[0]), t6 = quad_bcast3<3>(tt[0]);
+      dw[0] = vsub(vsub(vsub(vsub(V(0.0f, 0.0f, 0.0f), t0), t2), t4), t6);
+    }
+    dw[1] = vsub(vadd(V(0.0f, 0.0f, 0.0f), tt[0]), tt[1]);
+    dw[2] = vadd(V(0.0f, 0.0f, 0.0f), tt[1]);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      const v3 v = b.v[l], w = b.w[l];
+      b.v[l] = V(S.lin_damp * v.x + 0.0f * S.h, S.lin_damp * v.y + 0.0f * S.h, S.lin_damp * v.z + S.gz * S.h);
+      b.w[l] = V(S.ang_damp * w.x + dw[l].x * S.h, S.ang_damp * w.y + dw[l].y * S.h,
+                 S.ang_damp * w.z + dw[l].z * S.h);
+    }
+    // 2. kinetic
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      b.x[l] = vadd(b.x[l], vscl(b.v[l], S.h));
+      q4 dq = qmul_vq(b.w[l], b.q[l]);
+      q4 q = b.q[l];
+      q.w = q.w + S.half_h * dq.w; q.x = q.x + S.half_h * dq.x;
+      q.y = q.y + S.half_h * dq.y; q.z = q.z + S.half_h * dq.z;
+      b.q[l] = qnormalize(q);
+    }
+  }
+  // 3. position projection
+  QContacts ct;
+  {
+    v3 DX[QNB];
+    q4 DQ[QNB];
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { DX[l] = V(0.0f, 0.0f, 0.0f); DQ[l].w = DQ[l].x = DQ[l].y = DQ[l].z = 0.0f; }
+    QTorso tq;
+    POB_FENCE();
+    qjoint_position(S, b, 0, k, DX, DQ, &tq);
+    POB_FENCE();
+    qjoint_position(S, b, 1, k, DX, DQ, nullptr);
+    POB_FENCE();
+    // torso: global joints 0, 2, 4, 6 (quad lanes 0..3) in order
+    qtorso_add<0>(DX[0], DQ[0], tq);
+    qtorso_add<1>(DX[0], DQ[0], tq);
+    qtorso_add<2>(DX[0], DQ[0], tq);
+    qtorso_add<3>(DX[0], DQ[0], tq);
+    if (COLLIDE) {
+      qdetect(S, b, ct, k);
+      qcontact_position(S, b, L, ct, k, DX, DQ);
+    }
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      b.x[l] = vadd(b.x[l], DX[l]);
+      b.q[l].w += DQ[l].w; b.q[l].x += DQ[l].x; b.q[l].y += DQ[l].y; b.q[l].z += DQ[l].z;
+    }
+  }
+  // 4. velocity projection
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) {
+    b.q[l] = qnormalize(b.q[l]);
+    b.v[l] = vscl(vsub(b.x[l], L.get3(QL_PX(l))), S.inv_h);
+    q4 dq = qmul(b.q[l], qinv(L.get4(QL_PQ(l))));
+    float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
+    b.w[l] = V(sg * ((2.0f * dq.x) * S.inv_h), sg * ((2.0f * dq.y) * S.inv_h), sg * ((2.0f * dq.z) * S.inv_h));
+  }
+  // 5. velocity-level contacts
+  if (COLLIDE) {
+    v3 dV[QNB], dW[QNB];
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
+    qcontact_velocity(S, b, ct, k, dV, dW);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
+      L.set3(QL_CV(l), vadd(L.get3(QL_CV(l)), dV[l]));
+      L.set3(QL_CA(l), vadd(L.get3(QL_CA(l)), dW[l]));
+    }
+  }
+}

@@ -22,4 +22,5 @@ run trace --kernel-trace --stats &&
 run pmc_fetch --pmc FETCH_SIZE &&
 run pmc_write --pmc WRITE_SIZE &&
 run pmc_valu --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS &&
-run pmc_busy --pmc SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+run pmc_busy --pmc SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE &&
+run pmc_stall --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_TRANS_F SQ_INSTS_SMEM SQ_INSTS_VMEM
