@@ -585,13 +585,20 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
 #ifndef POB_QUAD_MIN_WAVES
 #define POB_QUAD_MIN_WAVES 4
 #endif
+// stage the per-leg table in LDS (all threads of the block; before any divergence)
+POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
+  for (int i = (int)threadIdx.x; i < 4 * POB_LEG_FLOATS; i += (int)blockDim.x) legtab[i] = Sp->leg[i / POB_LEG_FLOATS][i % POB_LEG_FLOATS];
+  __syncthreads();
+}
 template <int KIND, typename QT>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
-                          const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds) {
+                          const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
+                          const float *legtab) {
   csys_t &S = *Sp;
   const Lds Ls{lds, 256, (int)threadIdx.x};
   const int b = gt >> 2;
   const int k = gt & 3;
+  const float *LT = legtab + k * POB_LEG_FLOATS;
   float done = 0.0f;
   const int kind = KIND != POB_MIXED ? KIND : S.kind;
   if (b < B) {
@@ -616,15 +623,15 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
 #pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, bd, a, Ls, k, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, (it & 1) != 0);
 
     float *o = out.obs + (size_t)b * D;
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
       const int p = jparent(jl), c = jchild(jl);
-      v3 ap = qrot(QJV(k, S.axis, jl), bd.q[p]);
-      const v3 ref = QJV(k, S.ref, jl);
+      v3 ap = qrot(QJV(LT, jl, QJ_AXIS), bd.q[p]);
+      const v3 ref = QJV(LT, jl, QJ_REF);
       v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
       const int j = 2 * k + jl;
       o[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
@@ -744,8 +751,10 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
                                                                        const StatePtrs out, const uint32_t flags,
                                                                        const int L) {
   __shared__ float lds[QL_FLOATS * 256];
+  __shared__ float legtab[4 * POB_LEG_FLOATS];
+  stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds);
+                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
 }
 
 // Mixed launch: segment k owns blocks [blk0_k, blk0_{k+1}); the segment index is
@@ -775,6 +784,7 @@ __global__ __launch_bounds__(256, LANES == 4 ? POB_QUAD_MIN_WAVES : 2) void k_st
                                                                                          const uint32_t flags,
                                                                                          const int L) {
   __shared__ float lds[(LANES == 4 ? QL_FLOATS : PL_FLOATS) * 256];
+  __shared__ float legtab[LANES == 4 ? 4 * POB_LEG_FLOATS : 1];
   const int bx = (int)blockIdx.x;
   int seg = 0;
 #pragma unroll
@@ -798,12 +808,14 @@ __global__ __launch_bounds__(256, LANES == 4 ? POB_QUAD_MIN_WAVES : 2) void k_st
   const float *act = POB_PICK(act);
   const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
 #undef POB_PICK
-  if (LANES == 4)
+  if (LANES == 4) {
+    stage_leg_table((csys_t *)(size_t)sysp, legtab);
     step_quad_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                                  (bx - blk0) * 256 + (int)threadIdx.x, lds);
-  else
+                                  (bx - blk0) * 256 + (int)threadIdx.x, lds, legtab);
+  } else {
     step_pair_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
                                   (bx - blk0) * 256 + (int)threadIdx.x, lds);
+  }
 }
 
 // ----------------------------------------------------------------------------- reset

@@ -9,7 +9,8 @@
 // Split: lane k (0..3) of an env's lane quad owns the torso (replicated in all four
 // lanes) and leg k: local body 0 = torso, 1 = Aux k+1 (global 2k+1), 2 = lower leg
 // (global 2k+2); local joint 0 = global 2k (torso -> aux), 1 = global 2k+1 (aux -> leg).
-// Leg tables are selected per lane from the scalar system table (4-way v_cndmask).
+// Leg tables come from an LDS copy of pob_sys::leg (one row per leg); the scalar table
+// (torso and global constants) is laundered per stage (pob_physics.h).
 // Every body's accumulations run in its owner lane in the oracle's order.  The torso's
 // cross-leg sums (actuator + damping torques of joints 0,2,4,6; the position corrections
 // those joints apply to the torso) are gathered with DPP quad broadcasts, and every lane
@@ -57,16 +58,22 @@ template <int J> POB_D q4 quad_bcast4(q4 a) {
   return r;
 }
 
-// leg-k select of four (scalar) table values
-POB_D float qsel(int k, float a0, float a1, float a2, float a3) {
-  return k < 2 ? (k == 0 ? a0 : a1) : (k == 2 ? a2 : a3);
-}
-// joint table row of local joint jl (global 2k + jl), body table row of local body l
-#define QJV(k, arr, jl) V(qsel(k, (arr)[jl][0], (arr)[(jl) + 2][0], (arr)[(jl) + 4][0], (arr)[(jl) + 6][0]), \
-                          qsel(k, (arr)[jl][1], (arr)[(jl) + 2][1], (arr)[(jl) + 4][1], (arr)[(jl) + 6][1]), \
-                          qsel(k, (arr)[jl][2], (arr)[(jl) + 2][2], (arr)[(jl) + 4][2], (arr)[(jl) + 6][2]))
-#define QJS(k, arr, jl) qsel(k, (arr)[jl], (arr)[(jl) + 2], (arr)[(jl) + 4], (arr)[(jl) + 6])
-#define QBS(k, arr, l) ((l) == 0 ? (arr)[0] : qsel(k, (arr)[l], (arr)[(l) + 2], (arr)[(l) + 4], (arr)[(l) + 6]))
+// Leg tables: each block stages pob_sys::leg (4 legs x POB_LEG_FLOATS) in LDS, and a lane
+// reads its own leg's row through LT = leg table + k * POB_LEG_FLOATS (ds_read_b32; the
+// four rows sit in distinct banks).  Selecting among four scalar table values per lane
+// instead costs either four vector loads or a divergent branch per value (measured).
+#define QJV(LT, jl, f) V((LT)[POB_LEG_JOINT(jl) + (f)], (LT)[POB_LEG_JOINT(jl) + (f) + 1], (LT)[POB_LEG_JOINT(jl) + (f) + 2])
+#define QJ_OFFP 0
+#define QJ_OFFC 3
+#define QJ_AXIS 6
+#define QJ_REF 9
+#define QJ_LO 12
+#define QJ_HI 13
+#define QJ_DAMP 14
+#define QJ_STRENGTH 15
+#define QJS(LT, jl, f) ((LT)[POB_LEG_JOINT(jl) + (f)])
+POB_D float q_inv_mass(csys_t &S, const float *LT, int l) { return l == 0 ? S.inv_mass[0] : LT[POB_LEG_BODY(l)]; }
+POB_D float q_cap_r(csys_t &S, const float *LT, int l) { return l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1]; }
 
 POB_D constexpr int qbody_global(int l, int k) { return l == 0 ? 0 : l + 2 * k; }
 
@@ -87,29 +94,27 @@ struct QContacts {
 POB_D constexpr int qcontact_body(int c) { return c == 0 ? 0 : (c == 1 ? 2 : c - 2); }
 
 // capsule end point q of local body l (torso: the sphere centre)
-POB_D v3 qcap_end(csys_t &S, int k, int l, int q) {
+POB_D v3 qcap_end(csys_t &S, const float *LT, int l, int q) {
   if (l == 0) return SV(S.cap_end[0][q]);
-  return V(qsel(k, S.cap_end[l][q][0], S.cap_end[l + 2][q][0], S.cap_end[l + 4][q][0], S.cap_end[l + 6][q][0]),
-           qsel(k, S.cap_end[l][q][1], S.cap_end[l + 2][q][1], S.cap_end[l + 4][q][1], S.cap_end[l + 6][q][1]),
-           qsel(k, S.cap_end[l][q][2], S.cap_end[l + 2][q][2], S.cap_end[l + 4][q][2], S.cap_end[l + 6][q][2]));
+  const float *e = LT + POB_LEG_BODY(l) + 2 + 3 * q;
+  return V(e[0], e[1], e[2]);
 }
 // ground contact c (0 torso, 1 lower leg k = ground collider k + 1)
-POB_D v3 qground_end(csys_t &S, int k, int c) {
+POB_D v3 qground_end(csys_t &S, const float *LT, int c) {
   if (c == 0) return SV(S.ground_end[0]);
-  return V(qsel(k, S.ground_end[1][0], S.ground_end[2][0], S.ground_end[3][0], S.ground_end[4][0]),
-           qsel(k, S.ground_end[1][1], S.ground_end[2][1], S.ground_end[3][1], S.ground_end[4][1]),
-           qsel(k, S.ground_end[1][2], S.ground_end[2][2], S.ground_end[3][2], S.ground_end[4][2]));
+  return V(LT[POB_LEG_GROUND], LT[POB_LEG_GROUND + 1], LT[POB_LEG_GROUND + 2]);
 }
-POB_D float qground_r(csys_t &S, int k, int c) {
-  return c == 0 ? S.ground_r[0] : qsel(k, S.ground_r[1], S.ground_r[2], S.ground_r[3], S.ground_r[4]);
+POB_D float qground_r(csys_t &S, const float *LT, int c) {
+  return c == 0 ? S.ground_r[0] : LT[POB_LEG_GROUND + 3];
 }
 
-POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
+POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
+    csys_t &S = *launder(Sp);
     const int l = qcontact_body(c);
-    v3 pe = vadd(b.x[l], qrot(qground_end(S, k, c), b.q[l]));
-    ct.pen[c] = qground_r(S, k, c) - pe.z;
+    v3 pe = vadd(b.x[l], qrot(qground_end(S, LT, c), b.q[l]));
+    ct.pen[c] = qground_r(S, LT, c) - pe.z;
   }
   uint32_t near_mask = 0u;
   {
@@ -119,6 +124,7 @@ POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
       mn = V(fminf(mn.x, b.x[l].x), fminf(mn.y, b.x[l].y), fminf(mn.z, b.x[l].z));
       mx = V(fmaxf(mx.x, b.x[l].x), fmaxf(mx.y, b.x[l].y), fmaxf(mx.z, b.x[l].z));
     }
+    csys_t &S = *launder(Sp);
     const int nw = S.n_walls;
     for (int w = 0; w < nw; ++w) {
       const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
@@ -129,6 +135,7 @@ POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) {
     POB_FENCE();
+    csys_t &S = *launder(Sp);
     const int nend = (l == 0) ? 1 : 2;
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
@@ -136,8 +143,8 @@ POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
     if (near_mask != 0u) {
       v3 pe[2];
 #pragma unroll
-      for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[l], qrot(qcap_end(S, k, l, q), b.q[l]));
-      const float r = QBS(k, S.cap_r, l);
+      for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[l], qrot(qcap_end(S, LT, l, q), b.q[l]));
+      const float r = q_cap_r(S, LT, l);
       const int nw = S.n_walls;
       for (int w = 0; w < nw; ++w) {
         if (!(near_mask & (1u << w))) continue;
@@ -155,21 +162,21 @@ POB_D void qdetect(csys_t &S, const QBody &b, QContacts &ct, const int k) {
   }
 }
 
-POB_D void qcontact_geom(csys_t &S, const QContacts &ct, int c, const int k, v3 &e, v3 &n, float &r) {
+POB_D void qcontact_geom(csys_t &S, const float *LT, const QContacts &ct, int c, v3 &e, v3 &n, float &r) {
   if (c < 2) {
-    e = qground_end(S, k, c);
+    e = qground_end(S, LT, c);
     n = V(0.0f, 0.0f, 1.0f);
-    r = qground_r(S, k, c);
+    r = qground_r(S, LT, c);
   } else {
     const int l = c - 2;
-    e = ct.sel[l] ? qcap_end(S, k, l, 1) : qcap_end(S, k, l, 0);
-    r = QBS(k, S.cap_r, l);
+    e = ct.sel[l] ? qcap_end(S, LT, l, 1) : qcap_end(S, LT, l, 0);
+    r = q_cap_r(S, LT, l);
     n = ct.n[l];
   }
 }
 
 // contact processing order of one body = oracle order (ground contact first, then wall)
-POB_D void qcontact_position(csys_t &S, const QBody &b, const Lds &L, const QContacts &ct, const int k,
+POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const Lds &L, const QContacts &ct,
                              v3 (&DX)[QNB], q4 (&DQ)[QNB]) {
 #pragma unroll
   for (int c = 0; c < 2 + QNB; ++c) {
@@ -177,10 +184,11 @@ POB_D void qcontact_position(csys_t &S, const QBody &b, const Lds &L, const QCon
     const int l = qcontact_body(c);
     const float pen = ct.pen[c];
     if (pen > 0.0f) {
+      csys_t &S = *launder(Sp);
       v3 e, n;
       float rad;
-      qcontact_geom(S, ct, c, k, e, n, rad);
-      const float im = QBS(k, S.inv_mass, l);
+      qcontact_geom(S, LT, ct, c, e, n, rad);
+      const float im = q_inv_mass(S, LT, l);
       v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
       v3 cp = vsub(pe, vscl(n, rad));
       v3 rr = vsub(cp, b.x[l]);
@@ -211,7 +219,7 @@ POB_D void qcontact_position(csys_t &S, const QBody &b, const Lds &L, const QCon
   }
 }
 
-POB_D void qcontact_velocity(csys_t &S, const QBody &b, const QContacts &ct, const int k, v3 (&dV)[QNB],
+POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const QContacts &ct, v3 (&dV)[QNB],
                              v3 (&dW)[QNB]) {
 #pragma unroll
   for (int c = 0; c < 2 + QNB; ++c) {
@@ -219,10 +227,11 @@ POB_D void qcontact_velocity(csys_t &S, const QBody &b, const QContacts &ct, con
     const int l = qcontact_body(c);
     const float pen = ct.pen[c];
     if (pen > 0.0f) {
+      csys_t &S = *launder(Sp);
       v3 e, n;
       float rad;
-      qcontact_geom(S, ct, c, k, e, n, rad);
-      const float im = QBS(k, S.inv_mass, l);
+      qcontact_geom(S, LT, ct, c, e, n, rad);
+      const float im = q_inv_mass(S, LT, l);
       v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
       v3 cp = vsub(pe, vscl(n, rad));
       v3 rr = vsub(cp, b.x[l]);
@@ -262,14 +271,15 @@ POB_D void q4acc(q4 &a, q4 t) { a.w += t.w; a.x += t.x; a.y += t.y; a.z += t.z; 
 
 // local joint jl's point / hinge / limit corrections into DX/DQ (local bodies); for the
 // hip (jl = 0) the torso terms go to *tt
-POB_D void qjoint_position(csys_t &S, const QBody &b, const int jl, const int k, v3 (&DX)[QNB], q4 (&DQ)[QNB],
+POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const int jl, v3 (&DX)[QNB], q4 (&DQ)[QNB],
                            QTorso *tt) {
+  csys_t &S = *launder(Sp);
   const int p = jparent(jl), c = jchild(jl);
-  const float imp = QBS(k, S.inv_mass, p);
-  const float imc = QBS(k, S.inv_mass, c);
+  const float imp = q_inv_mass(S, LT, p);
+  const float imc = q_inv_mass(S, LT, c);
   const bool torso_parent = p == 0;
-  v3 rp = qrot(QJV(k, S.off_p, jl), b.q[p]);
-  v3 rc = qrot(QJV(k, S.off_c, jl), b.q[c]);
+  v3 rp = qrot(QJV(LT, jl, QJ_OFFP), b.q[p]);
+  v3 rc = qrot(QJV(LT, jl, QJ_OFFC), b.q[c]);
   v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
   float L = sqrtf(vdot(d, d));
   if (torso_parent) {
@@ -292,20 +302,24 @@ POB_D void qjoint_position(csys_t &S, const QBody &b, const int jl, const int k,
     DX[c] = vsub(DX[c], vscl(P, imc));
     qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
   }
-  const v3 axis = QJV(k, S.axis, jl);
+  POB_FENCE();
+  csys_t &S2 = *launder(Sp);
+  const v3 axis = QJV(LT, jl, QJ_AXIS);
   v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
-  v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+  v3 Pa = vscl(vcross(ap, ac), S2.half_s_ang);
   if (torso_parent) tt->dqh = qhalf(qmul_vq(Pa, b.q[p]), 1.0f);
   else qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
   qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
-  const v3 ref = QJV(k, S.ref, jl);
+  POB_FENCE();
+  csys_t &S3 = *launder(Sp);
+  const v3 ref = QJV(LT, jl, QJ_REF);
   v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
   float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-  const float lo = QJS(k, S.lim_lo, jl), hi = QJS(k, S.lim_hi, jl);
+  const float lo = QJS(LT, jl, QJ_LO), hi = QJS(LT, jl, QJ_HI);
   float dl = 0.0f;
   if (psi < lo) dl = psi - lo;
   else if (psi > hi) dl = psi - hi;
-  v3 Pl = vscl(ap, dl * S.half_s_ang);
+  v3 Pl = vscl(ap, dl * S3.half_s_ang);
   if (torso_parent) tt->dql = qhalf(qmul_vq(Pl, b.q[p]), 1.0f);
   else qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
   qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
@@ -321,9 +335,8 @@ POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t) {
 }
 
 // One XPBD substep on a lane quad (see the header comment for the split).
-POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds &L, const int k,
+POB_D void qpbd_substep(csys_t *Sp, const float *LT, QBody &b, const float (&act)[QNJ], const Lds &L,
                         const bool COLLIDE) {
-  csys_t &S = *Sp;
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
   // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
@@ -332,9 +345,9 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
       const int p = jparent(jl), c = jchild(jl);
-      v3 a = qrot(QJV(k, S.axis, jl), b.q[p]);
-      v3 t = vscl(a, act[jl] * QJS(k, S.strength, jl));
-      v3 d = vscl(vsub(b.w[p], b.w[c]), QJS(k, S.jdamp, jl));
+      v3 a = qrot(QJV(LT, jl, QJ_AXIS), b.q[p]);
+      v3 t = vscl(a, act[jl] * QJS(LT, jl, QJ_STRENGTH));
+      v3 d = vscl(vsub(b.w[p], b.w[c]), QJS(LT, jl, QJ_DAMP));
       tt[jl] = vadd(t, d);
     }
     v3 dw[QNB];
@@ -345,6 +358,7 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
     }
     dw[1] = vsub(vadd(V(0.0f, 0.0f, 0.0f), tt[0]), tt[1]);
     dw[2] = vadd(V(0.0f, 0.0f, 0.0f), tt[1]);
+    csys_t &S = *launder(Sp);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       const v3 v = b.v[l], w = b.w[l];
@@ -372,9 +386,9 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
     for (int l = 0; l < QNB; ++l) { DX[l] = V(0.0f, 0.0f, 0.0f); DQ[l].w = DQ[l].x = DQ[l].y = DQ[l].z = 0.0f; }
     QTorso tq;
     POB_FENCE();
-    qjoint_position(S, b, 0, k, DX, DQ, &tq);
+    qjoint_position(Sp, LT, b, 0, DX, DQ, &tq);
     POB_FENCE();
-    qjoint_position(S, b, 1, k, DX, DQ, nullptr);
+    qjoint_position(Sp, LT, b, 1, DX, DQ, nullptr);
     POB_FENCE();
     // torso: global joints 0, 2, 4, 6 (quad lanes 0..3) in order
     qtorso_add<0>(DX[0], DQ[0], tq);
@@ -382,8 +396,8 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
     qtorso_add<2>(DX[0], DQ[0], tq);
     qtorso_add<3>(DX[0], DQ[0], tq);
     if (COLLIDE) {
-      qdetect(S, b, ct, k);
-      qcontact_position(S, b, L, ct, k, DX, DQ);
+      qdetect(Sp, LT, b, ct);
+      qcontact_position(Sp, LT, b, L, ct, DX, DQ);
     }
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
@@ -394,6 +408,7 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
   // 4. velocity projection
 #pragma unroll
   for (int l = 0; l < QNB; ++l) {
+    csys_t &S = *launder(Sp);
     b.q[l] = qnormalize(b.q[l]);
     b.v[l] = vscl(vsub(b.x[l], L.get3(QL_PX(l))), S.inv_h);
     q4 dq = qmul(b.q[l], qinv(L.get4(QL_PQ(l))));
@@ -405,7 +420,7 @@ POB_D void qpbd_substep(csys_t *Sp, QBody &b, const float (&act)[QNJ], const Lds
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontact_velocity(S, b, ct, k, dV, dW);
+    qcontact_velocity(Sp, LT, b, ct, dV, dW);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);

@@ -17,6 +17,13 @@
 #define POB_MAXOBJ 32   // GA apples + bombs
 #define POB_MAXBINS 32  // GA 2 * n_bins
 
+// per-leg table of the four-lanes-per-env kernel (pob_quad.h), leg k = joints 2k, 2k+1,
+// bodies 2k+1, 2k+2, ground collider k+1; staged in LDS once per block
+#define POB_LEG_JOINT(jl) (16 * (jl))   // off_p(3) off_c(3) axis(3) ref(3) lim_lo lim_hi jdamp strength
+#define POB_LEG_BODY(l) (32 + 8 * ((l) - 1))  // inv_mass cap_r cap_end[2][3]   (l = 1, 2)
+#define POB_LEG_GROUND 48               // ground_end(3) ground_r
+#define POB_LEG_FLOATS 52
+
 struct pob_sys {
   int kind, N, D, n_obj;
   int substeps, n_walls, n_grid;
@@ -46,6 +53,7 @@ struct pob_sys {
   float ga_catch_range, ga_sensor_range, ga_half_span, ga_bin_res, ga_dying_cost, ga_waiting[3];
   float tag_tag_radius, tag_visible_radius, tag_target_step, tag_min_spawn_distance;
   float tag_cage_xy[2], tag_dying_cost;
+  float leg[4][POB_LEG_FLOATS];  // gathered copies of the per-leg rows above
   float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
   int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)
   const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env

@@ -208,6 +208,27 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     s.tag_cage_xy[0] = p.tag_cage_xy[0]; s.tag_cage_xy[1] = p.tag_cage_xy[1];
     s.tag_dying_cost = p.tag_dying_cost;
   }
+  // per-leg gathered table (pob_quad.h): the same numbers, laid out per leg
+  for (int k = 0; k < 4; ++k) {
+    float *L = s.leg[k];
+    for (int jl = 0; jl < 2; ++jl) {
+      const int j = 2 * k + jl;
+      float *J = L + POB_LEG_JOINT(jl);
+      for (int c = 0; c < 3; ++c) {
+        J[c] = s.off_p[j][c]; J[3 + c] = s.off_c[j][c]; J[6 + c] = s.axis[j][c]; J[9 + c] = s.ref[j][c];
+      }
+      J[12] = s.lim_lo[j]; J[13] = s.lim_hi[j]; J[14] = s.jdamp[j]; J[15] = s.strength[j];
+    }
+    for (int l = 1; l <= 2; ++l) {
+      const int i = 2 * k + l;
+      float *Bd = L + POB_LEG_BODY(l);
+      Bd[0] = s.inv_mass[i]; Bd[1] = s.cap_r[i];
+      for (int q = 0; q < 2; ++q)
+        for (int c = 0; c < 3; ++c) Bd[2 + 3 * q + c] = s.cap_end[i][q][c];
+    }
+    for (int c = 0; c < 3; ++c) L[POB_LEG_GROUND + c] = s.ground_end[k + 1][c];
+    L[POB_LEG_GROUND + 3] = s.ground_r[k + 1];
+  }
   // broadphase boxes: wall AABB + the largest distance from a body centre to any point of
   // its capsule (|end| + r) + 1e-3 margin (>> float rounding of the sphere-box distance)
   double reach = 0.0;
