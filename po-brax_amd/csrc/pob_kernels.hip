@@ -1,11 +1,10 @@
 // pob_kernels.hip -- fused rollout kernels + the C ABI of libpob.so (include/pob.h).
 //
 // Kernels (batch-major HBM layout; qp stored as float32 or binary16, computed in float32):
-//   k_step_pair<KIND,QT> physics (PBD) + per-env POMDP logic + obs + Episode/AutoReset
-//                    wrappers, TWO lanes per environment (pob_pair.h) -- the default
+//   k_step_quad<KIND,QT> physics (PBD) + per-env POMDP logic + obs + Episode/AutoReset
+//                    wrappers, FOUR lanes per environment (pob_quad.h)
 //   k_step_mixed<QT> the same body for up to POB_MIX_MAX envs of different kinds in ONE
 //                    launch (block ranges select the env; the task tail dispatches on kind)
-//   k_step<KIND>     one lane per environment (POB_STEP_LANES=1; float32 qp only)
 //   k_reset<KIND,BS,QT> threefry keys -> joint noise -> forward kinematics -> env placement
 //                    (HH goal swap / GA top-16-of-156 choice / TAG rejection loop) ->
 //                    sys.info contact -> obs; also the masked "reset where done" variants
@@ -23,7 +22,6 @@
 #include <new>
 
 #include "../../include/pob.h"
-#include "pob_pair.h"
 #include "pob_quad.h"
 #include "pob_physics.h"
 
@@ -40,7 +38,6 @@ struct pob_env {
   float *d_grid = nullptr;
   uint32_t *d_scratch = nullptr;  // any-done word for pob_reset_where_done without a flag
   int device = 0;
-  int lanes_per_env = 4;  // k_step_quad (default), k_step_pair (POB_STEP_LANES=2), k_step (=1)
 };
 
 #define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
@@ -315,268 +312,6 @@ POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const i
   else task_step<POB_ANT, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
 }
 
-// ------------------------------------------------------------------------------ step
-// Fused step: brax AutoResetWrapper(VmapWrapper(EpisodeWrapper(ActionRepeat(env)))).step
-// (envs/__init__.py:59-70) with env.step = ant_heavenhell.py:106-123 /
-// ant_gather.py:125-150 / ant_tag.py:107-127 and System.step = physics_step().
-// One lane per env; float32 qp.
-template <int KIND>
-__global__ __launch_bounds__(256) void k_step(const void *sysp, const int B, const StatePtrs in,
-                                              const float *__restrict__ act, const StatePtrs out,
-                                              const uint32_t flags, const int L) {
-  __shared__ float lds[POB_LDS_FLOATS * 256];
-  csys_t *Sp = (csys_t *)(size_t)sysp;
-  csys_t &S = *Sp;
-  const Lds Ls{lds, 256, (int)threadIdx.x};
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  float done = 0.0f;
-  if (b < B) {
-    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
-    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
-    Body bd;
-    load_body(in.pos + r3, in.rot + r4, in.vel + r3, in.ang + r3, bd);
-    float a[POB_NJ];
-#pragma unroll
-    for (int j = 0; j < POB_NJ; ++j) a[j] = act[(size_t)b * POB_NJ + j];
-    const float prev_done = in.done[b];
-    float steps = in.steps ? in.steps[b] : 0.0f;
-    if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && prev_done != 0.0f) steps = 0.0f;
-    float m0 = in.m0 ? in.m0[b] : 0.0f, m1 = in.m1 ? in.m1[b] : 0.0f, m2 = in.m2 ? in.m2[b] : 0.0f;
-    uint32_t rng0 = in.rng[2 * b], rng1 = in.rng[2 * b + 1];
-    const float xb = bd.x[0].x;
-
-    physics_step(Sp, bd, a, Ls);
-    v3 cv[POB_NDYN], ca[POB_NDYN];
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) { cv[i] = Ls.get3(POB_LDS_CV(i)); ca[i] = Ls.get3(POB_LDS_CA(i)); }
-
-    float *opos = out.pos + r3, *orot = out.rot + r4, *ovel = out.vel + r3, *oang = out.ang + r3;
-    float *o = out.obs + (size_t)b * D;
-    if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
-      for (int i = POB_NDYN; i < N; ++i) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          opos[3 * i + c] = in.pos[r3 + 3 * i + c];
-          ovel[3 * i + c] = in.vel[r3 + 3 * i + c];
-          oang[3 * i + c] = in.ang[r3 + 3 * i + c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) orot[4 * i + c] = in.rot[r4 + 4 * i + c];
-      }
-    }
-    store_body<float>(bd, out.pos, out.rot, out.vel, out.ang, r3, r4);
-
-    write_obs_common(S, N, bd, cv, ca, o, obs_shift(KIND));
-    TaskOut t;
-    t.steps = steps; t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
-    t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
-    if (KIND == POB_ANT) {
-      t.ctrl = ant_ctrl_cost(a);
-      float sc = 0.0f;
-#pragma unroll
-      for (int i = 0; i < POB_NDYN; ++i) sc = ant_contact_add(sc, cv[i]);
-      t.contact = 0.0005f * sc;
-    }
-    task_step<KIND, float>(S, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
-    done = t.done;
-    const float reward = t.reward, trunc = t.trunc;
-    steps = t.steps; m0 = t.m0; m1 = t.m1; m2 = t.m2; rng0 = t.rng0; rng1 = t.rng1;
-    if ((flags & POB_F_AUTORESET) && done != 0.0f) {  // brax AutoResetWrapper.step [ext]
-      for (int k = 0; k < 3 * N; ++k) {
-        opos[k] = in.first_pos[r3 + k]; ovel[k] = in.first_vel[r3 + k]; oang[k] = in.first_ang[r3 + k];
-      }
-      for (int k = 0; k < 4 * N; ++k) orot[k] = in.first_rot[r4 + k];
-      for (int k = 0; k < D; ++k) o[k] = in.first_obs[(size_t)b * D + k];
-    }
-    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-      for (int k = 0; k < 3 * N; ++k) {
-        out.first_pos[r3 + k] = in.first_pos[r3 + k]; out.first_vel[r3 + k] = in.first_vel[r3 + k];
-        out.first_ang[r3 + k] = in.first_ang[r3 + k];
-      }
-      for (int k = 0; k < 4 * N; ++k) out.first_rot[r4 + k] = in.first_rot[r4 + k];
-      for (int k = 0; k < D; ++k) out.first_obs[(size_t)b * D + k] = in.first_obs[(size_t)b * D + k];
-    }
-    out.reward[b] = reward;
-    out.done[b] = done;
-    if (out.steps) out.steps[b] = steps;
-    if (out.truncation) out.truncation[b] = trunc;
-    if (out.m0) out.m0[b] = m0;
-    if (out.m1) out.m1[b] = m1;
-    if (out.m2) out.m2[b] = m2;
-    out.rng[2 * b] = rng0;
-    out.rng[2 * b + 1] = rng1;
-  }
-  if (out.any_done) {
-    const unsigned long long m = __ballot(done != 0.0f);
-    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
-  }
-}
-
-
-// ------------------------------------------------------------------ step, lane pairs
-// Same fused step with TWO lanes per env (pob_pair.h): lane h owns the torso (replica) and
-// bodies 4h+1..4h+4.  2 waves / SIMD (VGPR+AGPR <= 256, 65 LDS floats / lane).  Lane 0
-// runs the per-env POMDP tail; lane 1 writes its bodies' rows, joints and cfrc rows.
-// gt = the pair-lane index within this env batch (2 b + h).
-template <int KIND, typename QT>
-POB_D void step_pair_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
-                          const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds) {
-  csys_t &S = *Sp;
-  const Lds Ls{lds, 256, (int)threadIdx.x};
-  const int b = gt >> 1;
-  const bool h = (gt & 1) != 0;
-  float done = 0.0f;
-  const int kind = KIND != POB_MIXED ? KIND : S.kind;
-  if (b < B) {
-    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
-    const int sh = obs_shift(kind);
-    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
-    HBody bd;
-#pragma unroll
-    for (int l = 0; l < PNB; ++l) {
-      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
-      bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
-      bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
-      bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
-      bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
-    }
-    const float xb = bd.x[0].x;
-    float a[PNJ];
-#pragma unroll
-    for (int jl = 0; jl < PNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + jl + (h ? 4 : 0)];
-
-#pragma unroll
-    for (int l = 0; l < PNB; ++l) { Ls.set3(PL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(PL_CA(l), V(0.0f, 0.0f, 0.0f)); }
-    const int iters = Sp->substeps / 2;
-#pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep(Sp, bd, a, Ls, h, (it & 1) != 0);
-
-    float *o = out.obs + (size_t)b * D;
-    // joint angle / velocity obs of this lane's joints (a3)
-#pragma unroll
-    for (int jl = 0; jl < PNJ; ++jl) {
-      const int p = jparent(jl), c = jchild(jl);
-      v3 ap = qrot(HSV(h, S.axis[jl], S.axis[jl + 4]), bd.q[p]);
-      const v3 ref = HSV(h, S.ref[jl], S.ref[jl + 4]);
-      v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
-      const int j = jl + (h ? 4 : 0);
-      o[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-      o[sh + 21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
-    }
-    // cfrc rows: lane 0 rows 0..4, lane 1 rows 5..8 and the zero rows of frozen bodies
-    float *oc = o + (29 + sh);
-#pragma unroll
-    for (int l = 0; l < PNB; ++l) {
-      if (l == 0 && h) continue;
-      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
-      const v3 cv = Ls.get3(PL_CV(l)), ca = Ls.get3(PL_CA(l));
-      oc[3 * g] = clip1(cv.x); oc[1 + 3 * g] = clip1(cv.y); oc[2 + 3 * g] = clip1(cv.z);
-      oc[3 * N + 3 * g] = clip1(ca.x); oc[1 + 3 * N + 3 * g] = clip1(ca.y); oc[2 + 3 * N + 3 * g] = clip1(ca.z);
-    }
-    if (h) {
-      for (int k = 3 * POB_NDYN; k < 3 * N; ++k) { oc[k] = 0.0f; oc[3 * N + k] = 0.0f; }
-    }
-    TaskOut t;
-    if (!h) {
-      if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
-      o[sh + 2] = bd.x[0].z;
-      o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
-      o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
-      o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
-      if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
-        for (int i = POB_NDYN; i < N; ++i) {
-          cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
-          cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
-          cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
-          cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
-        }
-      }
-      float steps = in.steps ? in.steps[b] : 0.0f;
-      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
-      t.steps = steps;
-      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
-      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
-      t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
-      if (kind == POB_ANT) {
-        // full action row and contact rows 0..4 (own slots) then 5..8 (partner's slots)
-        t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
-        float sc = 0.0f;
-#pragma unroll
-        for (int l = 0; l < PNB; ++l) sc = ant_contact_add(sc, Ls.get3(PL_CV(l)));
-#pragma unroll
-        for (int l = 1; l < PNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(PL_CV(l), (int)threadIdx.x + 1));
-        t.contact = 0.0005f * sc;
-      }
-      task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
-      done = t.done;
-    }
-    const float done_partner = pair_swap(done);  // all lanes of the pair active here
-    done = h ? done_partner : done;
-    const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
-    // dynamic body rows: computed state, or first_qp when the AutoResetWrapper resets
-#pragma unroll
-    for (int l = 0; l < PNB; ++l) {
-      if (l == 0 && h) continue;
-      const int g = l == 0 ? 0 : l + (h ? 4 : 0);
-      if (reset_rows) {
-        cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
-        cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
-        cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
-        cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
-      } else {
-        st3<QT>(out.pos, r3 + 3 * g, bd.x[l]);
-        st4<QT>(out.rot, r4 + 4 * g, bd.q[l]);
-        st3<QT>(out.vel, r3 + 3 * g, bd.v[l]);
-        st3<QT>(out.ang, r3 + 3 * g, bd.w[l]);
-      }
-    }
-    if (!h) {
-      if (reset_rows) {  // frozen rows from first_qp
-        cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
-      }
-      if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-        cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
-        cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
-        cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
-        cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
-        for (int k = 0; k < D; ++k) out.first_obs[(size_t)b * D + k] = in.first_obs[(size_t)b * D + k];
-      }
-      out.reward[b] = t.reward;
-      out.done[b] = t.done;
-      if (out.steps) out.steps[b] = t.steps;
-      if (out.truncation) out.truncation[b] = t.trunc;
-      if (out.m0) out.m0[b] = t.m0;
-      if (out.m1) out.m1[b] = t.m1;
-      if (out.m2) out.m2[b] = t.m2;
-      out.rng[2 * b] = t.rng0;
-      out.rng[2 * b + 1] = t.rng1;
-    }
-  }
-  // obs row of a reset env: both lanes' obs writes are done (same wave, program order);
-  // lane 0 overwrites the whole row with first_obs
-  if (b < B && !h && (flags & POB_F_AUTORESET) && done != 0.0f) {
-    const int D = obs_dim<KIND>(S);
-    float *o = out.obs + (size_t)b * D;
-    for (int k = 0; k < D; ++k) o[k] = in.first_obs[(size_t)b * D + k];
-  }
-  if (out.any_done) {
-    const unsigned long long m = __ballot(!h && done != 0.0f);
-    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
-  }
-}
-
-template <int KIND, typename QT>
-__global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const int B, const StatePtrs in,
-                                                      const float *__restrict__ act, const StatePtrs out,
-                                                      const uint32_t flags, const int L) {
-  __shared__ float lds[PL_FLOATS * 256];
-  step_pair_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds);
-}
-
 // ------------------------------------------------------------------ step, lane quads
 // Same fused step with FOUR lanes per env (pob_quad.h): lane k owns the torso (replica)
 // and leg k (bodies 2k+1, 2k+2).  39 LDS floats / lane.  Lane 0 runs the per-env POMDP
@@ -587,7 +322,8 @@ __global__ __launch_bounds__(256, 2) void k_step_pair(const void *sysp, const in
 #endif
 // stage the per-leg table in LDS (all threads of the block; before any divergence)
 POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
-  for (int i = (int)threadIdx.x; i < 4 * POB_LEG_FLOATS; i += (int)blockDim.x) legtab[i] = Sp->leg[i / POB_LEG_FLOATS][i % POB_LEG_FLOATS];
+  const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];  // [4][POB_LEG_FLOATS], contiguous
+  for (int i = (int)threadIdx.x; i < 4 * POB_LEG_FLOATS; i += (int)blockDim.x) legtab[i] = src[i];
   __syncthreads();
 }
 template <int KIND, typename QT>
@@ -623,7 +359,13 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
 #pragma nounroll
+#if defined(POB_EXP_NO_COLLIDE)
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, false);  // timing experiment only
+#elif defined(POB_EXP_NO_PHYSICS)
+    for (int it = 0; it < 0 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, false);  // timing experiment only
+#else
     for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, (it & 1) != 0);
+#endif
 
     float *o = out.obs + (size_t)b * D;
     // joint angle / velocity obs of this lane's joints (a3)
@@ -779,12 +521,11 @@ POB_D const void *uniform_ptr(const void *p) {
   return (const void *)(size_t)(((uint64_t)hi << 32) | lo);
 }
 
-template <typename QT, int LANES>
-__global__ __launch_bounds__(256, LANES == 4 ? POB_QUAD_MIN_WAVES : 2) void k_step_mixed(const MixArgs A,
-                                                                                         const uint32_t flags,
-                                                                                         const int L) {
-  __shared__ float lds[(LANES == 4 ? QL_FLOATS : PL_FLOATS) * 256];
-  __shared__ float legtab[LANES == 4 ? 4 * POB_LEG_FLOATS : 1];
+template <typename QT>
+__global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_mixed(const MixArgs A, const uint32_t flags,
+                                                                        const int L) {
+  __shared__ float lds[QL_FLOATS * 256];
+  __shared__ float legtab[4 * POB_LEG_FLOATS];
   const int bx = (int)blockIdx.x;
   int seg = 0;
 #pragma unroll
@@ -808,14 +549,9 @@ __global__ __launch_bounds__(256, LANES == 4 ? POB_QUAD_MIN_WAVES : 2) void k_st
   const float *act = POB_PICK(act);
   const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
 #undef POB_PICK
-  if (LANES == 4) {
-    stage_leg_table((csys_t *)(size_t)sysp, legtab);
-    step_quad_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                                  (bx - blk0) * 256 + (int)threadIdx.x, lds, legtab);
-  } else {
-    step_pair_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                                  (bx - blk0) * 256 + (int)threadIdx.x, lds);
-  }
+  stage_leg_table((csys_t *)(size_t)sysp, legtab);
+  step_quad_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                (bx - blk0) * 256 + (int)threadIdx.x, lds, legtab);
 }
 
 // ----------------------------------------------------------------------------- reset
@@ -1125,17 +861,6 @@ static void launch_step_quad(int kind, dim3 g, hipStream_t st, const void *sp, i
     default: hipLaunchKernelGGL((k_step_quad<POB_ANT, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
   }
 }
-template <typename QT>
-static void launch_step_pair(int kind, dim3 g, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
-                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
-  switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_pair<POB_HEAVENHELL, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step_pair<POB_GATHER, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_TAG: hipLaunchKernelGGL((k_step_pair<POB_TAG, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    default: hipLaunchKernelGGL((k_step_pair<POB_ANT, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-  }
-}
-
 extern "C" {
 
 int pob_abi_version(void) { return POB_ABI_VERSION; }
@@ -1155,15 +880,7 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   pob_env *e = new (std::nothrow) pob_env();
   if (!e) return fail(POB_ENOMEM, "out of host memory");
   e->params = prm;
-  if (const char *v = getenv("POB_STEP_LANES")) {
-    const int n = atoi(v);
-    e->lanes_per_env = n == 1 ? 1 : (n == 2 ? 2 : 4);
-  }
   if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
-  if (e->sys.qp_f16 && e->lanes_per_env == 1) {
-    delete e;
-    return fail(POB_EINVAL, "binary16 qp storage needs a multi-lane step kernel (POB_STEP_LANES 2 or 4)");
-  }
   int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
   if (rc) { delete e; return rc; }
   rc = hip_check(hipMalloc(&e->d_scratch, 64), "hipMalloc(scratch)");
@@ -1251,23 +968,9 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  if (e->lanes_per_env == 4) {
-    const dim3 g = grid_for(4 * B, 256);
-    if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
-    else launch_step_quad<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
-  } else if (e->lanes_per_env == 2) {
-    const dim3 g = grid_for(2 * B, 256);
-    if (e->sys.qp_f16) launch_step_pair<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
-    else launch_step_pair<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
-  } else {
-    const dim3 g = grid_for(B, 256);
-    switch (e->sys.kind) {
-      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step<POB_HEAVENHELL>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      case POB_GATHER: hipLaunchKernelGGL((k_step<POB_GATHER>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      case POB_TAG: hipLaunchKernelGGL((k_step<POB_TAG>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-      default: hipLaunchKernelGGL((k_step<POB_ANT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, episode_length); break;
-    }
-  }
+  const dim3 g = grid_for(4 * B, 256);
+  if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
+  else launch_step_quad<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");
 }
 
@@ -1282,26 +985,19 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   for (int k = 0; k < n; ++k) {
     const pob_env *e = envs[k];
     if (int rc = check_step(e, B[k], &in[k], act[k], &out[k], flags, episode_length)) return rc;
-    if (e->lanes_per_env == 1) return fail(POB_EINVAL, "mixed step needs a multi-lane step kernel");
-    if (e->lanes_per_env != envs[0]->lanes_per_env) return fail(POB_EINVAL, "mixed step: envs must share lanes per env");
     if (e->sys.qp_f16 != envs[0]->sys.qp_f16) return fail(POB_EINVAL, "mixed step: envs must share qp_storage");
     if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
     MixSeg &s = A.s[k];
     s.sysp = e->d_sys; s.act = act[k]; s.in = to_ptrs(in[k]); s.out = to_ptrs(out[k]);
     s.B = B[k]; s.blk0 = (int)blk;
-    blk += ((long long)envs[0]->lanes_per_env * B[k] + 255) / 256;
+    blk += (4LL * B[k] + 255) / 256;
     if (blk > INT_MAX) return fail(POB_EINVAL, "mixed step: batch too large");
   }
   for (int k = n; k < POB_MIX_MAX; ++k) { A.s[k] = A.s[n - 1]; A.s[k].blk0 = INT_MAX; }
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blk);
-  if (envs[0]->lanes_per_env == 4) {
-    if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half, 4>), g, dim3(256), 0, st, A, flags, episode_length);
-    else hipLaunchKernelGGL((k_step_mixed<float, 4>), g, dim3(256), 0, st, A, flags, episode_length);
-  } else {
-    if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half, 2>), g, dim3(256), 0, st, A, flags, episode_length);
-    else hipLaunchKernelGGL((k_step_mixed<float, 2>), g, dim3(256), 0, st, A, flags, episode_length);
-  }
+  if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half>), g, dim3(256), 0, st, A, flags, episode_length);
+  else hipLaunchKernelGGL((k_step_mixed<float>), g, dim3(256), 0, st, A, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step_mixed launch");
 }
 

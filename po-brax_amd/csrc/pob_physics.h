@@ -1,9 +1,7 @@
-// pob_physics.h -- the PBD Ant step on one lane (= one environment), gfx950.
-//
-// One lane owns one env: the 9 dynamic bodies (pos, rot, vel, ang = 117 floats), the
-// substep-start copy (63), the Jacobi accumulators and the per-contact scratch all live in
-// VGPRs (fully unrolled over bodies / joints / contacts, compile-time indices only), so a
-// control step touches HBM only to load and store the state once.
+// pob_physics.h -- shared physics pieces of the rollout kernels (gfx950): the system-table
+// access helpers, the per-lane LDS view, sphere-box and the whole-ant (one lane) contact
+// detection + velocity-level contact solve used by the reset kernel's sys.info(qp)
+// (a2).  The step itself runs four lanes per env (pob_quad.h).
 //
 // Algorithm = brax v1 System.step with dynamics_mode "pbd" as restated in DESIGN.md §3
 // (brax is not vendored: reference call sites ant_heavenhell.py:108, ant_gather.py:127,
@@ -28,8 +26,8 @@ struct Contacts {
 };
 
 // Hide the table pointer from loop-invariant code motion: without this the compiler
-// hoists every table value of the unrolled substep into SGPRs and spills hundreds of
-// them.  Re-laundering per joint / contact keeps each value's scalar load next to its use
+// hoists every table value of an unrolled block into SGPRs and spills them.
+// Re-laundering per joint / contact keeps each value's scalar load next to its use
 // (scalar-cache hits).
 typedef __attribute__((address_space(4))) const pob_sys csys_t;  // constant address space
 POB_D csys_t *launder(csys_t *p) {
@@ -47,9 +45,8 @@ POB_D csys_t *launder(csys_t *p) {
 #endif
 
 // Per-lane LDS scratch, lane-minor (element e of lane t at base[e * BS + t]): conflict-free
-// ds_read/ds_write_b32.  Holds what the substep keeps live but rarely touches: the
-// substep-start pose (63 floats, read by static friction and the velocity projection) and
-// the Info.contact accumulators (54 floats, touched once per collide substep).
+// ds_read/ds_write_b32.  Holds what the substep keeps live but rarely touches (the
+// substep-start pose and the Info.contact accumulators, pob_quad.h).
 struct Lds {
   float *base;
   int stride, t;
@@ -63,11 +60,6 @@ struct Lds {
   POB_D q4 get4(int e) const { q4 q; q.w = get(e); q.x = get(e + 1); q.y = get(e + 2); q.z = get(e + 3); return q; }
   POB_D void set4(int e, q4 q) const { set(e, q.w); set(e + 1, q.x); set(e + 2, q.y); set(e + 3, q.z); }
 };
-#define POB_LDS_PX(i) (7 * (i))          // prev pos (3) + prev rot (4) of body i
-#define POB_LDS_PQ(i) (7 * (i) + 3)
-#define POB_LDS_CV(i) (63 + 6 * (i))     // Info.contact vel / ang of body i
-#define POB_LDS_CA(i) (63 + 6 * (i) + 3)
-#define POB_LDS_FLOATS 117
 
 POB_D constexpr int jparent(int j) { return (j & 1) ? j : 0; }
 POB_D constexpr int jchild(int j) { return j + 1; }
@@ -170,49 +162,6 @@ POB_D void contact_geom(csys_t &S, const Contacts &ct, int k, v3 &e, v3 &n, floa
   }
 }
 
-POB_D void contact_position(csys_t *Sp, const Body &b, const Lds &L, const Contacts &ct,
-                            v3 (&DX)[POB_NDYN], q4 (&DQ)[POB_NDYN]) {
-#pragma unroll
-  for (int k = 0; k < POB_NGROUND + POB_NDYN; ++k) {
-    POB_FENCE();
-    const int i = contact_body(k);
-    const float pen = ct.pen[k];
-    if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
-      v3 e, n;
-      float rad;
-      contact_geom(S, ct, k, e, n, rad);
-      const float im = S.inv_mass[i];
-      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
-      v3 cp = vsub(pe, vscl(n, rad));
-      v3 rr = vsub(cp, b.x[i]);
-      v3 cn = vcross(rr, n);
-      float w = im + vdot(cn, cn);
-      float lam = pen / w;
-      v3 P = vscl(n, lam);
-      q4 dq = qmul_vq(vcross(rr, P), b.q[i]);
-      DX[i] = vadd(DX[i], vscl(P, im));
-      DQ[i].w += 0.5f * dq.w; DQ[i].x += 0.5f * dq.x; DQ[i].y += 0.5f * dq.y; DQ[i].z += 0.5f * dq.z;
-      v3 cprev = vadd(L.get3(POB_LDS_PX(i)), qrot(qrot(rr, qinv(b.q[i])), L.get4(POB_LDS_PQ(i))));
-      v3 dp = vsub(cp, cprev);
-      v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
-      float lt = sqrtf(vdot(dpt, dpt));
-      if (lt > 0.0f) {
-        v3 t = vdivs(dpt, lt);
-        v3 ctn = vcross(rr, t);
-        float wt = im + vdot(ctn, ctn);
-        float lamt = lt / wt;
-        if (lamt < S.friction * lam) {
-          v3 Pt = vscl(t, -lamt);
-          q4 dqt = qmul_vq(vcross(rr, Pt), b.q[i]);
-          DX[i] = vadd(DX[i], vscl(Pt, im));
-          DQ[i].w += 0.5f * dqt.w; DQ[i].x += 0.5f * dqt.x; DQ[i].y += 0.5f * dqt.y; DQ[i].z += 0.5f * dqt.z;
-        }
-      }
-    }
-  }
-}
-
 POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&dV)[POB_NDYN],
                             v3 (&dW)[POB_NDYN]) {
 #pragma unroll
@@ -250,141 +199,6 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       }
     }
   }
-}
-
-POB_D void joints_position(csys_t *Sp, const Body &b, v3 (&DX)[POB_NDYN], q4 (&DQ)[POB_NDYN]) {
-#pragma unroll
-  for (int j = 0; j < POB_NJ; ++j) {
-    POB_FENCE();
-    csys_t &S = *launder(Sp);
-    const int p = jparent(j), c = jchild(j);
-    const float imp = S.inv_mass[p], imc = S.inv_mass[c];
-    // point-to-point constraint between the joint anchors
-    v3 rp = qrot(SV(S.off_p[j]), b.q[p]), rc = qrot(SV(S.off_c[j]), b.q[c]);
-    v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
-    float L = sqrtf(vdot(d, d));
-    if (L > 0.0f) {
-      v3 n = vdivs(d, L);
-      v3 cp = vcross(rp, n), cc = vcross(rc, n);
-      float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
-      float lam = (L / wsum) * S.s_pos;
-      v3 P = vscl(n, lam);
-      DX[p] = vadd(DX[p], vscl(P, imp));
-      qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
-      DX[c] = vsub(DX[c], vscl(P, imc));
-      qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
-    }
-    // hinge axis alignment (unit inverse inertia: w_p = w_c = 1)
-    const v3 axis = SV(S.axis[j]);
-    v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
-    v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
-    qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
-    qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
-    // angle limits about the parent's hinge axis (brax math.signed_angle)
-    const v3 ref = SV(S.ref[j]);
-    v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
-    float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-    float dl = 0.0f;
-    if (psi < S.lim_lo[j]) dl = psi - S.lim_lo[j];
-    else if (psi > S.lim_hi[j]) dl = psi - S.lim_hi[j];
-    v3 Pl = vscl(ap, dl * S.half_s_ang);
-    qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
-    qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
-  }
-}
-
-// One XPBD substep; COLLIDE selects the second substep of each brax PBD iteration.
-POB_D void pbd_substep(csys_t *Sp, Body &b, const float (&act)[POB_NJ], const Lds &L, const bool COLLIDE) {
-#pragma unroll
-  for (int i = 0; i < POB_NDYN; ++i) { L.set3(POB_LDS_PX(i), b.x[i]); L.set4(POB_LDS_PQ(i), b.q[i]); }
-  // 1. acceleration level: torque actuators + joint angular damping; gravity
-  {
-    v3 dw[POB_NDYN];
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) dw[i] = V(0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int j = 0; j < POB_NJ; ++j) {
-      csys_t &S = *launder(Sp);
-      const int p = jparent(j), c = jchild(j);
-      v3 a = qrot(SV(S.axis[j]), b.q[p]);
-      v3 t = vscl(a, act[j] * S.strength[j]);
-      v3 d = vscl(vsub(b.w[p], b.w[c]), S.jdamp[j]);
-      v3 tt = vadd(t, d);
-      dw[p] = vsub(dw[p], tt);
-      dw[c] = vadd(dw[c], tt);
-    }
-    csys_t &S = *launder(Sp);
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) {
-      const v3 v = b.v[i], w = b.w[i];
-      b.v[i] = V(S.lin_damp * v.x + 0.0f * S.h, S.lin_damp * v.y + 0.0f * S.h, S.lin_damp * v.z + S.gz * S.h);
-      b.w[i] = V(S.ang_damp * w.x + dw[i].x * S.h, S.ang_damp * w.y + dw[i].y * S.h,
-                 S.ang_damp * w.z + dw[i].z * S.h);
-    }
-    // 2. kinetic
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) {
-      b.x[i] = vadd(b.x[i], vscl(b.v[i], S.h));
-      q4 dq = qmul_vq(b.w[i], b.q[i]);
-      q4 q = b.q[i];
-      q.w = q.w + S.half_h * dq.w; q.x = q.x + S.half_h * dq.x;
-      q.y = q.y + S.half_h * dq.y; q.z = q.z + S.half_h * dq.z;
-      b.q[i] = qnormalize(q);
-    }
-  }
-  // 3. position projection (Jacobi: joints + contacts from the same state)
-  Contacts ct;
-  {
-    v3 DX[POB_NDYN];
-    q4 DQ[POB_NDYN];
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) { DX[i] = V(0.0f, 0.0f, 0.0f); DQ[i].w = DQ[i].x = DQ[i].y = DQ[i].z = 0.0f; }
-    joints_position(Sp, b, DX, DQ);
-    if (COLLIDE) {
-      detect(Sp, b, ct);
-      contact_position(Sp, b, L, ct, DX, DQ);
-    }
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) {
-      b.x[i] = vadd(b.x[i], DX[i]);
-      b.q[i].w += DQ[i].w; b.q[i].x += DQ[i].x; b.q[i].y += DQ[i].y; b.q[i].z += DQ[i].z;
-    }
-  }
-  // 4. velocity projection
-  {
-    csys_t &S = *launder(Sp);
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) {
-      b.q[i] = qnormalize(b.q[i]);
-      b.v[i] = vscl(vsub(b.x[i], L.get3(POB_LDS_PX(i))), S.inv_h);
-      q4 dq = qmul(b.q[i], qinv(L.get4(POB_LDS_PQ(i))));
-      float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
-      b.w[i] = V(sg * ((2.0f * dq.x) * S.inv_h), sg * ((2.0f * dq.y) * S.inv_h), sg * ((2.0f * dq.z) * S.inv_h));
-    }
-  }
-  // 5. velocity-level contact solve, accumulated into Info.contact (LDS)
-  if (COLLIDE) {
-    v3 dV[POB_NDYN], dW[POB_NDYN];
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) { dV[i] = V(0.0f, 0.0f, 0.0f); dW[i] = V(0.0f, 0.0f, 0.0f); }
-    contact_velocity(Sp, b, ct, dV, dW);
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) {
-      b.v[i] = vadd(b.v[i], dV[i]); b.w[i] = vadd(b.w[i], dW[i]);
-      L.set3(POB_LDS_CV(i), vadd(L.get3(POB_LDS_CV(i)), dV[i]));
-      L.set3(POB_LDS_CA(i), vadd(L.get3(POB_LDS_CA(i)), dW[i]));
-    }
-  }
-}
-
-// brax System.step: substeps/2 iterations of (plain substep, collide substep); the summed
-// contact impulses (Info.contact) are left in L at POB_LDS_CV / POB_LDS_CA.
-POB_D void physics_step(csys_t *Sp, Body &b, const float (&act)[POB_NJ], const Lds &L) {
-#pragma unroll
-  for (int i = 0; i < POB_NDYN; ++i) { L.set3(POB_LDS_CV(i), V(0.0f, 0.0f, 0.0f)); L.set3(POB_LDS_CA(i), V(0.0f, 0.0f, 0.0f)); }
-  const int iters = launder(Sp)->substeps / 2;
-#pragma nounroll
-  for (int it = 0; it < 2 * iters; ++it) pbd_substep(Sp, b, act, L, (it & 1) != 0);
 }
 
 // sys.info(qp).contact at a static state
