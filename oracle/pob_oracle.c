@@ -104,6 +104,22 @@ static inline q4 qmul_vq(v3 a, q4 q) {
   return r;
 }
 static inline q4 qinv(q4 q) { q4 r = {q.w, -q.x, -q.y, -q.z}; return r; }
+/* a * s + b, fused per component */
+static inline v3 vfma(v3 a, float s, v3 b) {
+  FL(6);
+  return V(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z));
+}
+/* x + rotate(v, q) with the translation folded into the rotation's fused chain */
+static inline v3 qrot_add(v3 v, q4 q, v3 x) {
+  FL(2 + 1 + 12 + 6 + 3);
+  v3 u = V(q.x, q.y, q.z);
+  float t2 = 2.0f * vdot(u, v);
+  float c = fmaf(q.w, q.w, -vdot(u, u));
+  float s2 = 2.0f * q.w;
+  v3 cr = vcross(u, v);
+  return V(fmaf(t2, u.x, fmaf(c, v.x, fmaf(s2, cr.x, x.x))), fmaf(t2, u.y, fmaf(c, v.y, fmaf(s2, cr.y, x.y))),
+           fmaf(t2, u.z, fmaf(c, v.z, fmaf(s2, cr.z, x.z))));
+}
 static inline q4 qnormalize(q4 q) {
   FL(13);
   float n = sqrtf(fmaf(q.z, q.z, fmaf(q.y, q.y, fmaf(q.x, q.x, q.w * q.w))));
@@ -496,15 +512,16 @@ static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
   v3 h = e->wall_h[w];
   v3 d = vsub(p, e->wall_c[w]);
   FL(6 + 6 + 3 + 5); /* local x/y, clamp, e, d2 */
-  float lx = d.x * c + d.y * s, ly = -(d.x * s) + d.y * c, lz = d.z;
+  float lx = fmaf(d.y, s, d.x * c), ly = fmaf(d.y, c, -(d.x * s)), lz = d.z;
   float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
-  float d2 = ex * ex + ey * ey + ez * ez;
+  float d2 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
   float pen, nx, ny, nz;
   if (d2 > 0.0f) {
     FL(5);
     float dist = sqrtf(d2);
-    pen = r - dist; nx = ex / dist; ny = ey / dist; nz = ez / dist;
+    float inv = 1.0f / dist;
+    pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
   } else {
     FL(4);
     float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
@@ -514,7 +531,7 @@ static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
     else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
   }
   FL(6);
-  *n = V(nx * c - ny * s, nx * s + ny * c, nz);
+  *n = V(fmaf(-ny, s, nx * c), fmaf(ny, c, nx * s), nz);
   return pen;
 }
 
@@ -524,7 +541,7 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   int k = 0;
   for (int g = 0; g < e->n_ground; ++g, ++k) {
     int i = e->ground_body[g];
-    v3 pe = vadd(b->x[i], qrot(e->ground_end[g], b->q[i]));
+    v3 pe = qrot_add(e->ground_end[g], b->q[i], b->x[i]);
     FL(1);
     ct->pen[k] = e->ground_r[g] - pe.z;
     ct->n[k] = V(0.0f, 0.0f, 1.0f);
@@ -534,7 +551,7 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
     float best = 0.0f; v3 bn = V(0, 0, 0), be = e->cap_end[i][0];
     for (int w = 0; w < e->n_walls; ++w)
       for (int q = 0; q < e->cap_nend[i]; ++q) {
-        v3 pe = vadd(b->x[i], qrot(e->cap_end[i][q], b->q[i]));
+        v3 pe = qrot_add(e->cap_end[i][q], b->q[i], b->x[i]);
         v3 n; float pen = sphere_box(e, w, pe, e->cap_r[i], &n);
         if (pen > best) { best = pen; bn = n; be = e->cap_end[i][q]; }
       }
@@ -543,6 +560,8 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   ct->count = k;
 }
 
+static void qadd_half(q4 *acc, q4 d, float sign);
+
 /* position-level contact projection (normal + static friction) into DX/DQ */
 static void contact_position(const orc_env *e, const body_t *b, const body_t *prev,
                              const contacts_t *ct, v3 *DX, q4 *DQ) {
@@ -550,8 +569,8 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = vadd(b->x[i], qrot(ct->e[k], b->q[i]));
-    v3 cp = vsub(pe, vscl(n, ct->r[k]));
+    v3 pe = qrot_add(ct->e[k], b->q[i], b->x[i]);
+    v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 cn = vcross(rr, n);
     FL(2 + 8);
@@ -559,12 +578,12 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     float lam = pen / w;
     v3 P = vscl(n, lam);
     q4 dq = qmul_vq(vcross(rr, P), b->q[i]);
-    DX[i] = vadd(DX[i], vscl(P, im));
-    DQ[i].w += 0.5f * dq.w; DQ[i].x += 0.5f * dq.x; DQ[i].y += 0.5f * dq.y; DQ[i].z += 0.5f * dq.z;
+    DX[i] = vfma(P, im, DX[i]);
+    qadd_half(&DQ[i], dq, 1.0f);
     /* static friction against the motion of the contact point over the substep */
-    v3 cprev = vadd(prev->x[i], qrot(qrot(rr, qinv(b->q[i])), prev->q[i]));
+    v3 cprev = qrot_add(qrot(rr, qinv(b->q[i])), prev->q[i], prev->x[i]);
     v3 dp = vsub(cp, cprev);
-    v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
+    v3 dpt = vfma(n, -vdot(dp, n), dp);
     float lt = sqrtf(vdot(dpt, dpt));
     FL(1);
     if (lt > 0.0f) {
@@ -577,8 +596,8 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
         FL(8);
         v3 Pt = vscl(t, -lamt);
         q4 dqt = qmul_vq(vcross(rr, Pt), b->q[i]);
-        DX[i] = vadd(DX[i], vscl(Pt, im));
-        DQ[i].w += 0.5f * dqt.w; DQ[i].x += 0.5f * dqt.x; DQ[i].y += 0.5f * dqt.y; DQ[i].z += 0.5f * dqt.z;
+        DX[i] = vfma(Pt, im, DX[i]);
+        qadd_half(&DQ[i], dqt, 1.0f);
       }
     }
   }
@@ -590,12 +609,12 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = vadd(b->x[i], qrot(ct->e[k], b->q[i]));
-    v3 cp = vsub(pe, vscl(n, ct->r[k]));
+    v3 pe = qrot_add(ct->e[k], b->q[i], b->x[i]);
+    v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 vr = vadd(b->v[i], vcross(b->w[i], rr));
     float vn = vdot(vr, n);
-    v3 vt = vsub(vr, vscl(n, vn));
+    v3 vt = vfma(n, -vn, vr);
     float lt = sqrtf(vdot(vt, vt));
     FL(1);
     v3 dv = V(0.0f, 0.0f, 0.0f);
@@ -604,7 +623,7 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
       float fr = fminf(e->friction * pen * e->inv_h, lt);
       dv = vscl(vt, -(fr / lt));
     }
-    if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+    if (vn < 0.0f) dv = vfma(n, -vn, dv);
     float D = sqrtf(vdot(dv, dv));
     FL(1);
     if (D > 0.0f) {
@@ -613,17 +632,19 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
       v3 cd = vcross(rr, dh);
       float w = im + vdot(cd, cd);
       v3 P = vdivs(dv, w);
-      dV[i] = vadd(dV[i], vscl(P, im));
+      dV[i] = vfma(P, im, dV[i]);
       dW[i] = vadd(dW[i], vcross(rr, P));
     }
   }
 }
 
 /* ------------------------------------------------------------------ the PBD step */
+/* acc += sign * 0.5 * d as one fused multiply-add per component (sign * 0.5 exact) */
 static void qadd_half(q4 *acc, q4 d, float sign) {
   FL(12);
-  acc->w += sign * (0.5f * d.w); acc->x += sign * (0.5f * d.x);
-  acc->y += sign * (0.5f * d.y); acc->z += sign * (0.5f * d.z);
+  const float h = 0.5f * sign;
+  acc->w = fmaf(h, d.w, acc->w); acc->x = fmaf(h, d.x, acc->x);
+  acc->y = fmaf(h, d.y, acc->y); acc->z = fmaf(h, d.z, acc->z);
 }
 
 static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
@@ -635,18 +656,20 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
     v3 d = vsub(vadd(b->x[c], rc), vadd(b->x[p], rp));
     float L = sqrtf(vdot(d, d));
     FL(1);
+    /* P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway */
+    v3 P = V(0.0f, 0.0f, 0.0f);
     if (L > 0.0f) {
       FL(5);
       v3 n = vdivs(d, L);
       v3 cp = vcross(rp, n), cc = vcross(rc, n);
       float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
       float lam = (L / wsum) * e->s_pos;
-      v3 P = vscl(n, lam);
-      DX[p] = vadd(DX[p], vscl(P, imp));
-      qadd_half(&DQ[p], qmul_vq(vcross(rp, P), b->q[p]), 1.0f);
-      DX[c] = vsub(DX[c], vscl(P, imc));
-      qadd_half(&DQ[c], qmul_vq(vcross(rc, P), b->q[c]), -1.0f);
+      P = vscl(n, lam);
     }
+    DX[p] = vfma(P, imp, DX[p]);
+    qadd_half(&DQ[p], qmul_vq(vcross(rp, P), b->q[p]), 1.0f);
+    DX[c] = vfma(P, -imc, DX[c]);
+    qadd_half(&DQ[c], qmul_vq(vcross(rc, P), b->q[c]), -1.0f);
     /* hinge axis alignment (unit inverse inertia: w_p = w_c = 1) */
     v3 ap = qrot(e->axis[j], b->q[p]), ac = qrot(e->axis[j], b->q[c]);
     v3 Pa = vscl(vcross(ap, ac), e->half_s_ang);
@@ -683,19 +706,19 @@ static void pbd_substep(const orc_env *e, body_t *b, const float *act, int colli
   for (int i = 0; i < NDYN; ++i) {
     FL(18);
     v3 v = b->v[i], w = b->w[i];
-    b->v[i] = V(e->lin_damp * v.x + e->g[0] * e->h, e->lin_damp * v.y + e->g[1] * e->h,
-                e->lin_damp * v.z + e->g[2] * e->h);
-    b->w[i] = V(e->ang_damp * w.x + dw[i].x * e->h, e->ang_damp * w.y + dw[i].y * e->h,
-                e->ang_damp * w.z + dw[i].z * e->h);
+    b->v[i] = V(fmaf(e->lin_damp, v.x, e->g[0] * e->h), fmaf(e->lin_damp, v.y, e->g[1] * e->h),
+                fmaf(e->lin_damp, v.z, e->g[2] * e->h));
+    b->w[i] = V(fmaf(e->ang_damp, w.x, dw[i].x * e->h), fmaf(e->ang_damp, w.y, dw[i].y * e->h),
+                fmaf(e->ang_damp, w.z, dw[i].z * e->h));
   }
   /* 2. kinetic */
   for (int i = 0; i < NDYN; ++i) {
-    b->x[i] = vadd(b->x[i], vscl(b->v[i], e->h));
+    b->x[i] = vfma(b->v[i], e->h, b->x[i]);
     q4 dq = qmul_vq(b->w[i], b->q[i]);
     FL(8);
     q4 q = b->q[i];
-    q.w = q.w + e->half_h * dq.w; q.x = q.x + e->half_h * dq.x;
-    q.y = q.y + e->half_h * dq.y; q.z = q.z + e->half_h * dq.z;
+    q.w = fmaf(e->half_h, dq.w, q.w); q.x = fmaf(e->half_h, dq.x, q.x);
+    q.y = fmaf(e->half_h, dq.y, q.y); q.z = fmaf(e->half_h, dq.z, q.z);
     b->q[i] = qnormalize(q);
   }
   /* 3. position projection (Jacobi over joints + contacts) */

@@ -57,16 +57,29 @@ POB_D q4 qmul_vq(v3 a, q4 q) {
   return r;
 }
 POB_D q4 qinv(q4 q) { q4 r; r.w = q.w; r.x = -q.x; r.y = -q.y; r.z = -q.z; return r; }
+// a * s + b, fused per component
+POB_D v3 vfma(v3 a, float s, v3 b) { return V(FMA(a.x, s, b.x), FMA(a.y, s, b.y), FMA(a.z, s, b.z)); }
+// x + rotate(v, q) with the translation folded into the rotation's fused chain
+POB_D v3 qrot_add(v3 v, q4 q, v3 x) {
+  v3 u = V(q.x, q.y, q.z);
+  float t2 = 2.0f * vdot(u, v);
+  float c = FMA(q.w, q.w, -vdot(u, u));
+  float s2 = 2.0f * q.w;
+  v3 cr = vcross(u, v);
+  return V(FMA(t2, u.x, FMA(c, v.x, FMA(s2, cr.x, x.x))), FMA(t2, u.y, FMA(c, v.y, FMA(s2, cr.y, x.y))),
+           FMA(t2, u.z, FMA(c, v.z, FMA(s2, cr.z, x.z))));
+}
 POB_D q4 qnormalize(q4 q) {
   float n = sqrtf(FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w))));
   float inv = 1.0f / n;
   q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
   return r;
 }
-// acc += sign * 0.5 * d
+// acc += sign * 0.5 * d, one fused multiply-add per component (sign * 0.5 is exact)
 POB_D void qadd_half(q4 &acc, q4 d, float sign) {
-  acc.w += sign * (0.5f * d.w); acc.x += sign * (0.5f * d.x);
-  acc.y += sign * (0.5f * d.y); acc.z += sign * (0.5f * d.z);
+  const float h = 0.5f * sign;
+  acc.w = FMA(h, d.w, acc.w); acc.x = FMA(h, d.x, acc.x);
+  acc.y = FMA(h, d.y, acc.y); acc.z = FMA(h, d.z, acc.z);
 }
 
 // Cephes-form atanf / atan2f

@@ -73,14 +73,15 @@ POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
   const float c = S.wall_cos[w], s = S.wall_sin[w];
   const v3 h = SV(S.wall_h[w]);
   v3 d = vsub(p, SV(S.wall_c[w]));
-  float lx = d.x * c + d.y * s, ly = -(d.x * s) + d.y * c, lz = d.z;
+  float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
   float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
-  float d2 = ex * ex + ey * ey + ez * ez;
+  float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
   float pen, nx, ny, nz;
   if (d2 > 0.0f) {
     float dist = sqrtf(d2);
-    pen = r - dist; nx = ex / dist; ny = ey / dist; nz = ez / dist;
+    const float inv = 1.0f / dist;
+    pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
   } else {
     float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
     nx = 0.0f; ny = 0.0f; nz = 0.0f;
@@ -88,7 +89,7 @@ POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
     else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
     else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
   }
-  n = V(nx * c - ny * s, nx * s + ny * c, nz);
+  n = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
   return pen;
 }
 
@@ -99,7 +100,7 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
   for (int g = 0; g < POB_NGROUND; ++g) {
     csys_t &S = *launder(Sp);
     const int i = ground_body(g);
-    v3 pe = vadd(b.x[i], qrot(SV(S.ground_end[g]), b.q[i]));
+    v3 pe = qrot_add(SV(S.ground_end[g]), b.q[i], b.x[i]);
     ct.pen[g] = S.ground_r[g] - pe.z;
   }
   // wave-uniform broadphase: bit w set iff some lane's body-centre AABB meets wall w's grown box
@@ -126,7 +127,7 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
     const int nend = (i == 0) ? 1 : 2;
     v3 pe[2];
 #pragma unroll
-    for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[i], qrot(SV(S.cap_end[i][q]), b.q[i]));
+    for (int q = 0; q < nend; ++q) pe[q] = qrot_add(SV(S.cap_end[i][q]), b.q[i], b.x[i]);
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
@@ -175,26 +176,26 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       float rad;
       contact_geom(S, ct, k, e, n, rad);
       const float im = S.inv_mass[i];
-      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
-      v3 cp = vsub(pe, vscl(n, rad));
+      v3 pe = qrot_add(e, b.q[i], b.x[i]);
+      v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[i]);
       v3 vr = vadd(b.v[i], vcross(b.w[i], rr));
       float vn = vdot(vr, n);
-      v3 vt = vsub(vr, vscl(n, vn));
+      v3 vt = vfma(n, -vn, vr);
       float lt = sqrtf(vdot(vt, vt));
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
         dv = vscl(vt, -(fr / lt));
       }
-      if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+      if (vn < 0.0f) dv = vfma(n, -vn, dv);
       float D = sqrtf(vdot(dv, dv));
       if (D > 0.0f) {
         v3 dh = vdivs(dv, D);
         v3 cd = vcross(rr, dh);
         float w = im + vdot(cd, cd);
         v3 P = vdivs(dv, w);
-        dV[i] = vadd(dV[i], vscl(P, im));
+        dV[i] = vfma(P, im, dV[i]);
         dW[i] = vadd(dW[i], vcross(rr, P));
       }
     }

@@ -113,7 +113,7 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
   for (int c = 0; c < 2; ++c) {
     csys_t &S = *launder(Sp);
     const int l = qcontact_body(c);
-    v3 pe = vadd(b.x[l], qrot(qground_end(S, LT, c), b.q[l]));
+    v3 pe = qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
     ct.pen[c] = qground_r(S, LT, c) - pe.z;
   }
   uint32_t near_mask = 0u;
@@ -143,7 +143,7 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
     if (near_mask != 0u) {
       v3 pe[2];
 #pragma unroll
-      for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[l], qrot(qcap_end(S, LT, l, q), b.q[l]));
+      for (int q = 0; q < nend; ++q) pe[q] = qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
       const float r = q_cap_r(S, LT, l);
       const int nw = S.n_walls;
       for (int w = 0; w < nw; ++w) {
@@ -189,19 +189,19 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       float rad;
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
-      v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
-      v3 cp = vsub(pe, vscl(n, rad));
+      v3 pe = qrot_add(e, b.q[l], b.x[l]);
+      v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 cn = vcross(rr, n);
       float w = im + vdot(cn, cn);
       float lam = pen / w;
       v3 P = vscl(n, lam);
       q4 dq = qmul_vq(vcross(rr, P), b.q[l]);
-      DX[l] = vadd(DX[l], vscl(P, im));
-      DQ[l].w += 0.5f * dq.w; DQ[l].x += 0.5f * dq.x; DQ[l].y += 0.5f * dq.y; DQ[l].z += 0.5f * dq.z;
-      v3 cprev = vadd(L.get3(QL_PX(l)), qrot(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l))));
+      DX[l] = vfma(P, im, DX[l]);
+      qadd_half(DQ[l], dq, 1.0f);
+      v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
       v3 dp = vsub(cp, cprev);
-      v3 dpt = vsub(dp, vscl(n, vdot(dp, n)));
+      v3 dpt = vfma(n, -vdot(dp, n), dp);
       float lt = sqrtf(vdot(dpt, dpt));
       if (lt > 0.0f) {
         v3 t = vdivs(dpt, lt);
@@ -211,8 +211,8 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
         if (lamt < S.friction * lam) {
           v3 Pt = vscl(t, -lamt);
           q4 dqt = qmul_vq(vcross(rr, Pt), b.q[l]);
-          DX[l] = vadd(DX[l], vscl(Pt, im));
-          DQ[l].w += 0.5f * dqt.w; DQ[l].x += 0.5f * dqt.x; DQ[l].y += 0.5f * dqt.y; DQ[l].z += 0.5f * dqt.z;
+          DX[l] = vfma(Pt, im, DX[l]);
+          qadd_half(DQ[l], dqt, 1.0f);
         }
       }
     }
@@ -232,42 +232,38 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       float rad;
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
-      v3 pe = vadd(b.x[l], qrot(e, b.q[l]));
-      v3 cp = vsub(pe, vscl(n, rad));
+      v3 pe = qrot_add(e, b.q[l], b.x[l]);
+      v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 vr = vadd(b.v[l], vcross(b.w[l], rr));
       float vn = vdot(vr, n);
-      v3 vt = vsub(vr, vscl(n, vn));
+      v3 vt = vfma(n, -vn, vr);
       float lt = sqrtf(vdot(vt, vt));
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
         dv = vscl(vt, -(fr / lt));
       }
-      if (vn < 0.0f) dv = vadd(dv, vscl(n, -vn));
+      if (vn < 0.0f) dv = vfma(n, -vn, dv);
       float D = sqrtf(vdot(dv, dv));
       if (D > 0.0f) {
         v3 dh = vdivs(dv, D);
         v3 cd = vcross(rr, dh);
         float w = im + vdot(cd, cd);
         v3 P = vdivs(dv, w);
-        dV[l] = vadd(dV[l], vscl(P, im));
+        dV[l] = vfma(P, im, dV[l]);
         dW[l] = vadd(dW[l], vcross(rr, P));
       }
     }
   }
 }
 
-// torso terms of the lane's hip joint (global 2k): what the oracle adds to DX[0] / DQ[0]
+// torso terms of the lane's hip joint (global 2k): the oracle adds P * imp to DX[0] and
+// +0.5 * (dqp, dqh, dql) to DQ[0], each as fused multiply-adds in joint order
 struct QTorso {
-  v3 dx;             // point constraint: P * imp (zero if the anchors coincide)
-  q4 dqp, dqh, dql;  // point, hinge and limit rotation terms (+0.5 * dq)
+  v3 P;              // point-constraint impulse (zero if the anchors coincide)
+  q4 dqp, dqh, dql;  // point, hinge and limit rotation terms (raw quat_mul results)
 };
-POB_D q4 qhalf(q4 d, float sign) {
-  q4 r; r.w = sign * (0.5f * d.w); r.x = sign * (0.5f * d.x); r.y = sign * (0.5f * d.y); r.z = sign * (0.5f * d.z);
-  return r;
-}
-POB_D void q4acc(q4 &a, q4 t) { a.w += t.w; a.x += t.x; a.y += t.y; a.z += t.z; }
 
 // local joint jl's point / hinge / limit corrections into DX/DQ (local bodies); for the
 // hip (jl = 0) the torso terms go to *tt
@@ -282,32 +278,30 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   v3 rc = qrot(QJV(LT, jl, QJ_OFFC), b.q[c]);
   v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
   float L = sqrtf(vdot(d, d));
-  if (torso_parent) {
-    tt->dx = V(0.0f, 0.0f, 0.0f);
-    tt->dqp.w = tt->dqp.x = tt->dqp.y = tt->dqp.z = 0.0f;
-  }
+  // P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway
+  v3 P = V(0.0f, 0.0f, 0.0f);
   if (L > 0.0f) {
     v3 n = vdivs(d, L);
     v3 cp = vcross(rp, n), cc = vcross(rc, n);
     float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
     float lam = (L / wsum) * S.s_pos;
-    v3 P = vscl(n, lam);
-    if (torso_parent) {
-      tt->dx = vscl(P, imp);
-      tt->dqp = qhalf(qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
-    } else {
-      DX[p] = vadd(DX[p], vscl(P, imp));
-      qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
-    }
-    DX[c] = vsub(DX[c], vscl(P, imc));
-    qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
+    P = vscl(n, lam);
   }
+  if (torso_parent) {
+    tt->P = P;
+    tt->dqp = qmul_vq(vcross(rp, P), b.q[p]);
+  } else {
+    DX[p] = vfma(P, imp, DX[p]);
+    qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
+  }
+  DX[c] = vfma(P, -imc, DX[c]);
+  qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
   POB_FENCE();
   csys_t &S2 = *launder(Sp);
   const v3 axis = QJV(LT, jl, QJ_AXIS);
   v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
   v3 Pa = vscl(vcross(ap, ac), S2.half_s_ang);
-  if (torso_parent) tt->dqh = qhalf(qmul_vq(Pa, b.q[p]), 1.0f);
+  if (torso_parent) tt->dqh = qmul_vq(Pa, b.q[p]);
   else qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
   qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
   POB_FENCE();
@@ -320,18 +314,18 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   if (psi < lo) dl = psi - lo;
   else if (psi > hi) dl = psi - hi;
   v3 Pl = vscl(ap, dl * S3.half_s_ang);
-  if (torso_parent) tt->dql = qhalf(qmul_vq(Pl, b.q[p]), 1.0f);
+  if (torso_parent) tt->dql = qmul_vq(Pl, b.q[p]);
   else qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
   qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
 }
 
 // add quad lane J's hip terms onto the torso accumulators (global joint 2J)
 template <int J>
-POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t) {
-  dx = vadd(dx, quad_bcast3<J>(t.dx));
-  q4acc(dq, quad_bcast4<J>(t.dqp));
-  q4acc(dq, quad_bcast4<J>(t.dqh));
-  q4acc(dq, quad_bcast4<J>(t.dql));
+POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t, const float imp0) {
+  dx = vfma(quad_bcast3<J>(t.P), imp0, dx);
+  qadd_half(dq, quad_bcast4<J>(t.dqp), 1.0f);
+  qadd_half(dq, quad_bcast4<J>(t.dqh), 1.0f);
+  qadd_half(dq, quad_bcast4<J>(t.dql), 1.0f);
 }
 
 // One XPBD substep on a lane quad (see the header comment for the split).
@@ -362,18 +356,18 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, QBody &b, const float (&act
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       const v3 v = b.v[l], w = b.w[l];
-      b.v[l] = V(S.lin_damp * v.x + 0.0f * S.h, S.lin_damp * v.y + 0.0f * S.h, S.lin_damp * v.z + S.gz * S.h);
-      b.w[l] = V(S.ang_damp * w.x + dw[l].x * S.h, S.ang_damp * w.y + dw[l].y * S.h,
-                 S.ang_damp * w.z + dw[l].z * S.h);
+      b.v[l] = V(FMA(S.lin_damp, v.x, 0.0f * S.h), FMA(S.lin_damp, v.y, 0.0f * S.h), FMA(S.lin_damp, v.z, S.gz * S.h));
+      b.w[l] = V(FMA(S.ang_damp, w.x, dw[l].x * S.h), FMA(S.ang_damp, w.y, dw[l].y * S.h),
+                 FMA(S.ang_damp, w.z, dw[l].z * S.h));
     }
     // 2. kinetic
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
-      b.x[l] = vadd(b.x[l], vscl(b.v[l], S.h));
+      b.x[l] = vfma(b.v[l], S.h, b.x[l]);
       q4 dq = qmul_vq(b.w[l], b.q[l]);
       q4 q = b.q[l];
-      q.w = q.w + S.half_h * dq.w; q.x = q.x + S.half_h * dq.x;
-      q.y = q.y + S.half_h * dq.y; q.z = q.z + S.half_h * dq.z;
+      q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
+      q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
       b.q[l] = qnormalize(q);
     }
   }
@@ -391,10 +385,13 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, QBody &b, const float (&act
     qjoint_position(Sp, LT, b, 1, DX, DQ, nullptr);
     POB_FENCE();
     // torso: global joints 0, 2, 4, 6 (quad lanes 0..3) in order
-    qtorso_add<0>(DX[0], DQ[0], tq);
-    qtorso_add<1>(DX[0], DQ[0], tq);
-    qtorso_add<2>(DX[0], DQ[0], tq);
-    qtorso_add<3>(DX[0], DQ[0], tq);
+    {
+      const float imp0 = launder(Sp)->inv_mass[0];
+      qtorso_add<0>(DX[0], DQ[0], tq, imp0);
+      qtorso_add<1>(DX[0], DQ[0], tq, imp0);
+      qtorso_add<2>(DX[0], DQ[0], tq, imp0);
+      qtorso_add<3>(DX[0], DQ[0], tq, imp0);
+    }
     if (COLLIDE) {
       qdetect(Sp, LT, b, ct);
       qcontact_position(Sp, LT, b, L, ct, DX, DQ);
