@@ -180,12 +180,18 @@ def main() -> int:
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": 157.3, "unit": "TFLOP/s",
         "frac": round(tflops / 157.3, 5), "traffic": None,
-        "kernel": "k_step_mixed" if args.env == "mixed" else f"k_step_pair<{args.env}>",
+        "kernel": "k_step_mixed" if args.env == "mixed" else f"k_step_quad<{args.env}>",
         "kernel_ms": round(kern_ms, 4),
         "flops_per_env_step": round(fpe, 1), "bytes_per_env_step": round(bpe, 1),
         "hbm": {"achieved": round(hbm_gbs, 2), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(hbm_gbs / 8000.0, 6)},
     }
+
+    tr = committed_traffic(args.env, B, args.qp_dtype)
+    if tr is not None:
+        roofline["traffic"] = tr["traffic_bytes"]
+        roofline["traffic_source"] = (f"profiles/{tr['source']}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
+                                      f"WRITE_SIZE per launch of the same kernel and config")
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -212,6 +218,22 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def committed_traffic(env: str, B: int, qp: str):
+    """HBM bytes per launch from the newest committed PMC profile of this exact config
+    (profiles/*_traffic.json, written by profiles/summarize.py); None if there is none."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            t = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if t.get("env") == env and t.get("batch") == B and t.get("qp_storage", "f32") == qp and \
+                "k_step" in (t.get("kernel") or ""):
+            best = t
+    return best
 
 
 def cpu_baseline(name: str, seconds: float) -> dict:
