@@ -41,6 +41,7 @@ struct pob_env {
 };
 
 #define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
+#define POB_F_STAGED (1u << 16)  // internal step flag: coalesced LDS-staged state loads
 
 // ---------------------------------------------------------------------------- state
 #define POB_STATE_FIELDS(X)                                                                    \
@@ -320,6 +321,54 @@ POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const i
 #ifndef POB_QUAD_MIN_WAVES
 #define POB_QUAD_MIN_WAVES 4
 #endif
+// Per-wave LDS region: the block's per-lane scratch is laid out wave-major (wave w owns
+// floats [w * POB_STAGE_FLOATS, (w + 1) * POB_STAGE_FLOATS), element e of its lane t at
+// e * 64 + t: conflict-free), so a wave can reuse its whole region as a contiguous staging
+// buffer for coalesced state I/O while the other waves of the block still run physics.
+#define POB_STAGE_FLOATS (QL_FLOATS * 64)
+POB_D void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Coalesced copy of n_el consecutive qp elements (from element el0) into stg: 16 B (f32)
+// / 8 B (f16) vector loads by all 64 lanes.
+template <typename QT>
+POB_D void stage_load(const float *X, size_t el0, int n_el, float *stg, int lane);
+template <>
+POB_D void stage_load<float>(const float *X, size_t el0, int n_el, float *stg, int lane) {
+  for (int i = 4 * lane; i < n_el; i += 256) {
+    const float *p = X + el0 + i;
+    if (i + 4 <= n_el) {
+      const float4 v = *reinterpret_cast<const float4 *>(p);
+      stg[i] = v.x; stg[i + 1] = v.y; stg[i + 2] = v.z; stg[i + 3] = v.w;
+    } else {
+      for (int q = 0; q < n_el - i; ++q) stg[i + q] = p[q];
+    }
+  }
+}
+template <>
+POB_D void stage_load<__half>(const float *X, size_t el0, int n_el, float *stg, int lane) {
+  const __half *H = reinterpret_cast<const __half *>(X);
+  for (int i = 4 * lane; i < n_el; i += 256) {
+    const __half *p = H + el0 + i;
+    if (i + 4 <= n_el) {
+      const uint2 v = *reinterpret_cast<const uint2 *>(p);
+      const __half2 a = *reinterpret_cast<const __half2 *>(&v.x), c = *reinterpret_cast<const __half2 *>(&v.y);
+      stg[i] = __low2float(a); stg[i + 1] = __high2float(a); stg[i + 2] = __low2float(c); stg[i + 3] = __high2float(c);
+    } else {
+      for (int q = 0; q < n_el - i; ++q) stg[i + q] = __half2float(p[q]);
+    }
+  }
+}
+// Coalesced store of the dynamic-body part (first C9 = 9 c elements) of nenv consecutive
+// rows of N * c elements, from stg (row-major nenv x C9).
+template <typename QT, int C>
+POB_D void stage_store_dyn(float *X, size_t el0, int N, int nenv, const float *stg, int lane) {
+  constexpr int C9 = POB_NDYN * C;
+  for (int i = lane; i < nenv * C9; i += 64) {
+    const int e = i / C9, j = i - e * C9;
+    Q<QT>::st(X, el0 + (size_t)e * N * C + j, stg[i]);
+  }
+}
+
 // stage the per-leg table in LDS (all threads of the block; before any divergence)
 POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
   const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];  // [4][POB_LEG_FLOATS], contiguous
@@ -331,17 +380,46 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
                           const float *legtab) {
   csys_t &S = *Sp;
-  const Lds Ls{lds, 256, (int)threadIdx.x};
+  const int lane = (int)threadIdx.x & 63;
+  float *stg = lds + ((int)threadIdx.x >> 6) * POB_STAGE_FLOATS;  // this wave's region
+  const Lds Ls{stg, 64, lane};
   const int b = gt >> 2;
   const int k = gt & 3;
   const float *LT = legtab + k * POB_LEG_FLOATS;
-  float done = 0.0f;
   const int kind = KIND != POB_MIXED ? KIND : S.kind;
-  if (b < B) {
-    const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
-    const int sh = obs_shift(kind);
-    const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
-    QBody bd;
+  const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+  const int sh = obs_shift(kind);
+  const bool act_lane = b < B;
+  // the wave's 16 envs are consecutive rows of every state array
+  const int b_first = (gt - lane) >> 2;
+  const int nenv = B - b_first < 16 ? (B - b_first > 0 ? B - b_first : 0) : 16;
+  const int le = b - b_first;
+  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+
+  // ---- state load: coalesced vector loads into the wave's region, then every lane
+  // picks its bodies (the host sets POB_F_STAGED when the qp pointers are 16-B aligned
+  // and 16 envs x N x 4 fit the region); otherwise per-lane loads
+  QBody bd;
+  if (flags & POB_F_STAGED) {
+#pragma unroll
+    for (int arr = 0; arr < 4; ++arr) {
+      const int c = arr == 1 ? 4 : 3;
+      const float *X = arr == 0 ? in.pos : (arr == 1 ? in.rot : (arr == 2 ? in.vel : in.ang));
+      stage_load<QT>(X, (size_t)b_first * N * c, nenv * N * c, stg, lane);
+      wave_lds_sync();
+      if (act_lane) {
+#pragma unroll
+        for (int l = 0; l < QNB; ++l) {
+          const int o = (le * N + qbody_global(l, k)) * c;
+          if (arr == 0) bd.x[l] = V(stg[o], stg[o + 1], stg[o + 2]);
+          else if (arr == 1) { bd.q[l].w = stg[o]; bd.q[l].x = stg[o + 1]; bd.q[l].y = stg[o + 2]; bd.q[l].z = stg[o + 3]; }
+          else if (arr == 2) bd.v[l] = V(stg[o], stg[o + 1], stg[o + 2]);
+          else bd.w[l] = V(stg[o], stg[o + 1], stg[o + 2]);
+        }
+      }
+      wave_lds_sync();
+    }
+  } else if (act_lane) {
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       const int g = qbody_global(l, k);
@@ -350,11 +428,17 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
       bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
     }
+  }
+
+  // ---- physics (10 substeps in registers + the lane's LDS slots)
+  float jang[QNJ], jvel[QNJ];
+  v3 cvl[QNB], cal[QNB];
+  TaskOut t;
+  if (act_lane) {
     const float xb = bd.x[0].x;
     float a[QNJ];
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + 2 * k + jl];
-
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
@@ -366,8 +450,6 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #else
     for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, (it & 1) != 0);
 #endif
-
-    float *o = out.obs + (size_t)b * D;
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
@@ -375,38 +457,12 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       v3 ap = qrot(QJV(LT, jl, QJ_AXIS), bd.q[p]);
       const v3 ref = QJV(LT, jl, QJ_REF);
       v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
-      const int j = 2 * k + jl;
-      o[sh + 7 + j] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-      o[sh + 21 + j] = vdot(vsub(bd.w[c], bd.w[p]), ap);
+      jang[jl] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      jvel[jl] = vdot(vsub(bd.w[c], bd.w[p]), ap);
     }
-    // cfrc rows: lane k rows 2k+1, 2k+2 (lane 0 also the torso row); lane 3 the zero rows
-    float *oc = o + (29 + sh);
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) {
-      if (l == 0 && k != 0) continue;
-      const int g = qbody_global(l, k);
-      const v3 cv = Ls.get3(QL_CV(l)), ca = Ls.get3(QL_CA(l));
-      oc[3 * g] = clip1(cv.x); oc[1 + 3 * g] = clip1(cv.y); oc[2 + 3 * g] = clip1(cv.z);
-      oc[3 * N + 3 * g] = clip1(ca.x); oc[1 + 3 * N + 3 * g] = clip1(ca.y); oc[2 + 3 * N + 3 * g] = clip1(ca.z);
-    }
-    if (k == 3) {
-      for (int q = 3 * POB_NDYN; q < 3 * N; ++q) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
-    }
-    TaskOut t;
+    for (int l = 0; l < QNB; ++l) { cvl[l] = Ls.get3(QL_CV(l)); cal[l] = Ls.get3(QL_CA(l)); }
     if (k == 0) {
-      if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
-      o[sh + 2] = bd.x[0].z;
-      o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
-      o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
-      o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
-      if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
-        for (int i = POB_NDYN; i < N; ++i) {
-          cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
-          cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
-          cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
-          cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
-        }
-      }
       float steps = in.steps ? in.steps[b] : 0.0f;
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
       t.steps = steps;
@@ -418,71 +474,128 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
         float sc = 0.0f;
 #pragma unroll
-        for (int l = 0; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3(QL_CV(l)));
+        for (int l = 0; l < QNB; ++l) sc = ant_contact_add(sc, cvl[l]);
 #pragma unroll
         for (int q = 1; q < 4; ++q) {
 #pragma unroll
-          for (int l = 1; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(QL_CV(l), (int)threadIdx.x + q));
+          for (int l = 1; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(QL_CV(l), lane + q));
         }
         t.contact = 0.0005f * sc;
       }
-      task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
-      done = t.done;
-    }
-    done = quad_bcast<0>(done);  // all lanes of the quad active here
-    const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
-    // dynamic body rows: computed state, or first_qp when the AutoResetWrapper resets
-#pragma unroll
-    for (int l = 0; l < QNB; ++l) {
-      if (l == 0 && k != 0) continue;
-      const int g = qbody_global(l, k);
-      if (reset_rows) {
-        cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
-        cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
-        cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
-        cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
-      } else {
-        st3<QT>(out.pos, r3 + 3 * g, bd.x[l]);
-        st4<QT>(out.rot, r4 + 4 * g, bd.q[l]);
-        st3<QT>(out.vel, r3 + 3 * g, bd.v[l]);
-        st3<QT>(out.ang, r3 + 3 * g, bd.w[l]);
-      }
-    }
-    if (k == 0) {
-      if (reset_rows) {  // frozen rows from first_qp
-        cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-        cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
-      }
-      if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-        cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
-        cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
-        cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
-        cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
-        for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
-      }
-      out.reward[b] = t.reward;
-      out.done[b] = t.done;
-      if (out.steps) out.steps[b] = t.steps;
-      if (out.truncation) out.truncation[b] = t.trunc;
-      if (out.m0) out.m0[b] = t.m0;
-      if (out.m1) out.m1[b] = t.m1;
-      if (out.m2) out.m2[b] = t.m2;
-      out.rng[2 * b] = t.rng0;
-      out.rng[2 * b + 1] = t.rng1;
     }
   }
-  // obs row of a reset env: every lane's obs writes are done (same wave, program order);
-  // lane 0 overwrites the whole row with first_obs
-  if (b < B && k == 0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
-    const int D = obs_dim<KIND>(S);
-    float *o = out.obs + (size_t)b * D;
-    for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+  wave_lds_sync();  // every LDS read of the physics slots is done: the region is staging now
+
+  // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
+  float done = 0.0f;
+  const int P = POB_STAGE_FLOATS / D < 16 ? POB_STAGE_FLOATS / D : 16;
+  for (int p0 = 0; p0 < nenv; p0 += P) {
+    const int pn = nenv - p0 < P ? nenv - p0 : P;
+    if (act_lane && le >= p0 && le < p0 + pn) {
+      float *o = stg + (le - p0) * D;
+#pragma unroll
+      for (int jl = 0; jl < QNJ; ++jl) {
+        o[sh + 7 + 2 * k + jl] = jang[jl];
+        o[sh + 21 + 2 * k + jl] = jvel[jl];
+      }
+      // cfrc rows: lane k rows 2k+1, 2k+2 (lane 0 also the torso row); lane 3 the zero rows
+      float *oc = o + (29 + sh);
+#pragma unroll
+      for (int l = 0; l < QNB; ++l) {
+        if (l == 0 && k != 0) continue;
+        const int g = qbody_global(l, k);
+        oc[3 * g] = clip1(cvl[l].x); oc[1 + 3 * g] = clip1(cvl[l].y); oc[2 + 3 * g] = clip1(cvl[l].z);
+        oc[3 * N + 3 * g] = clip1(cal[l].x); oc[1 + 3 * N + 3 * g] = clip1(cal[l].y); oc[2 + 3 * N + 3 * g] = clip1(cal[l].z);
+      }
+      if (k == 3) {
+        for (int q = 3 * POB_NDYN; q < 3 * N; ++q) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+      }
+      if (k == 0) {
+        if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
+        o[sh + 2] = bd.x[0].z;
+        o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
+        o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
+        o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
+        if (out.pos != in.pos) {  // functional mode: carry the frozen rows over (the task
+          for (int i = POB_NDYN; i < N; ++i) {  // tail then moves GA objects / the TAG target)
+            cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+            cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+            cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+            cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
+          }
+        }
+        task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
+        done = t.done;
+      }
+      done = quad_bcast<0>(done);  // the quad's four lanes are active together here
+      // AutoResetWrapper: the row of a reset env is first_obs (written last, same lane order)
+      if (k == 0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+        wave_lds_sync();
+        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+      }
+    }
+    wave_lds_sync();
+    float *dst = out.obs + (size_t)(b_first + p0) * D;
+    for (int i = lane; i < pn * D; i += 64) dst[i] = stg[i];
+    wave_lds_sync();
+  }
+
+  // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
+  const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#pragma unroll
+  for (int arr = 0; arr < 4; ++arr) {
+    const int c = arr == 1 ? 4 : 3;
+    if (act_lane) {
+#pragma unroll
+      for (int l = 0; l < QNB; ++l) {
+        if (l == 0 && k != 0) continue;
+        const int g = qbody_global(l, k);
+        float *o = stg + (le * POB_NDYN + g) * c;
+        if (reset_rows) {
+          const float *F = arr == 0 ? in.first_pos : (arr == 1 ? in.first_rot : (arr == 2 ? in.first_vel : in.first_ang));
+          const size_t src = (arr == 1 ? r4 : r3) + (size_t)g * c;
+          for (int q = 0; q < c; ++q) o[q] = Q<QT>::ld(F, src + q);
+        } else if (arr == 0) { o[0] = bd.x[l].x; o[1] = bd.x[l].y; o[2] = bd.x[l].z; }
+        else if (arr == 1) { o[0] = bd.q[l].w; o[1] = bd.q[l].x; o[2] = bd.q[l].y; o[3] = bd.q[l].z; }
+        else if (arr == 2) { o[0] = bd.v[l].x; o[1] = bd.v[l].y; o[2] = bd.v[l].z; }
+        else { o[0] = bd.w[l].x; o[1] = bd.w[l].y; o[2] = bd.w[l].z; }
+      }
+    }
+    wave_lds_sync();
+    if (arr == 1) stage_store_dyn<QT, 4>(out.rot, (size_t)b_first * N * 4, N, nenv, stg, lane);
+    else stage_store_dyn<QT, 3>(arr == 0 ? out.pos : (arr == 2 ? out.vel : out.ang), (size_t)b_first * N * 3, N,
+                                nenv, stg, lane);
+    wave_lds_sync();
+  }
+
+  // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
+  if (act_lane && k == 0) {
+    if (reset_rows) {  // frozen rows from first_qp
+      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
+    }
+    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
+      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
+      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
+      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
+      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
+    }
+    out.reward[b] = t.reward;
+    out.done[b] = t.done;
+    if (out.steps) out.steps[b] = t.steps;
+    if (out.truncation) out.truncation[b] = t.trunc;
+    if (out.m0) out.m0[b] = t.m0;
+    if (out.m1) out.m1[b] = t.m1;
+    if (out.m2) out.m2[b] = t.m2;
+    out.rng[2 * b] = t.rng0;
+    out.rng[2 * b + 1] = t.rng1;
   }
   if (out.any_done) {
-    const unsigned long long m = __ballot(k == 0 && done != 0.0f);
-    if (m != 0ull && (threadIdx.x & 63) == 0) atomicOr(out.any_done, 1u);
+    const unsigned long long m = __ballot(act_lane && k == 0 && done != 0.0f);
+    if (m != 0ull && lane == 0) atomicOr(out.any_done, 1u);
   }
 }
 
@@ -946,6 +1059,13 @@ int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, voi
   return hip_check(hipGetLastError(), "k_reset launch");
 }
 
+// the coalesced staged state load needs 16-B aligned qp rows and 16 envs' rows of the
+// widest array (rot) to fit the wave's staging area
+static bool can_stage(const pob_env *e, const pob_state *in) {
+  const uintptr_t m = (uintptr_t)in->pos | (uintptr_t)in->rot | (uintptr_t)in->vel | (uintptr_t)in->ang;
+  return (m & 15u) == 0 && 16 * e->sys.N * 4 <= POB_STAGE_FLOATS;
+}
+
 static int check_step(const pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out,
                       uint32_t flags, int episode_length) {
   if (!e) return fail(POB_EINVAL, "env is NULL");
@@ -965,6 +1085,8 @@ static int check_step(const pob_env *e, int B, const pob_state *in, const float 
 int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out, uint32_t flags,
              int episode_length, void *stream) {
   if (int rc = check_step(e, B, in, act, out, flags, episode_length)) return rc;
+  flags &= ~POB_F_STAGED;
+  if (can_stage(e, in)) flags |= POB_F_STAGED;
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
@@ -981,12 +1103,15 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   MixArgs A;
   memset(&A, 0, sizeof(A));
   A.n = n;
+  flags &= ~POB_F_STAGED;
+  bool stage = true;
   long long blk = 0;
   for (int k = 0; k < n; ++k) {
     const pob_env *e = envs[k];
     if (int rc = check_step(e, B[k], &in[k], act[k], &out[k], flags, episode_length)) return rc;
     if (e->sys.qp_f16 != envs[0]->sys.qp_f16) return fail(POB_EINVAL, "mixed step: envs must share qp_storage");
     if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
+    stage = stage && can_stage(e, &in[k]);
     MixSeg &s = A.s[k];
     s.sysp = e->d_sys; s.act = act[k]; s.in = to_ptrs(in[k]); s.out = to_ptrs(out[k]);
     s.B = B[k]; s.blk0 = (int)blk;
@@ -994,6 +1119,7 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
     if (blk > INT_MAX) return fail(POB_EINVAL, "mixed step: batch too large");
   }
   for (int k = n; k < POB_MIX_MAX; ++k) { A.s[k] = A.s[n - 1]; A.s[k].blk0 = INT_MAX; }
+  if (stage) flags |= POB_F_STAGED;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blk);
   if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half>), g, dim3(256), 0, st, A, flags, episode_length);
