@@ -358,6 +358,46 @@ POB_D void stage_load<__half>(const float *X, size_t el0, int n_el, float *stg, 
     }
   }
 }
+// All loads of one array issued before any is consumed: MAXI 16-B (8-B for f16) chunks per
+// lane in registers (predicated), then written to stg.  Two of these back to back keep two
+// arrays' loads in flight at once.
+template <typename QT, int MAXI>
+struct ChunkLoad {
+  float v[MAXI][4];
+  POB_D void issue(const float *X, size_t el0, int n_el, int lane) {
+#pragma unroll
+    for (int m = 0; m < MAXI; ++m) {
+      const int i = 4 * lane + 256 * m;
+      if (i + 4 <= n_el) {
+        if constexpr (sizeof(QT) == 4) {
+          const float4 q = *reinterpret_cast<const float4 *>(X + el0 + i);
+          v[m][0] = q.x; v[m][1] = q.y; v[m][2] = q.z; v[m][3] = q.w;
+        } else {
+          const uint2 q = *reinterpret_cast<const uint2 *>(reinterpret_cast<const __half *>(X) + el0 + i);
+          const __half2 a = *reinterpret_cast<const __half2 *>(&q.x), c = *reinterpret_cast<const __half2 *>(&q.y);
+          v[m][0] = __low2float(a); v[m][1] = __high2float(a); v[m][2] = __low2float(c); v[m][3] = __high2float(c);
+        }
+      } else if (i < n_el) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (q < n_el - i) v[m][q] = Q<QT>::ld(X, el0 + i + q);
+      }
+    }
+  }
+  POB_D void put(float *stg, int n_el, int lane) const {
+#pragma unroll
+    for (int m = 0; m < MAXI; ++m) {
+      const int i = 4 * lane + 256 * m;
+      if (i + 4 <= n_el) { stg[i] = v[m][0]; stg[i + 1] = v[m][1]; stg[i + 2] = v[m][2]; stg[i + 3] = v[m][3]; }
+      else if (i < n_el) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (q < n_el - i) stg[i + q] = v[m][q];
+      }
+    }
+  }
+};
+
 // Coalesced store of the dynamic-body part (first C9 = 9 c elements) of nenv consecutive
 // rows of N * c elements, from stg (row-major nenv x C9).
 template <typename QT, int C>
@@ -400,7 +440,37 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   // picks its bodies (the host sets POB_F_STAGED when the qp pointers are 16-B aligned
   // and 16 envs x N x 4 fit the region); otherwise per-lane loads
   QBody bd;
-  if (flags & POB_F_STAGED) {
+  constexpr int NMAX = KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : (KIND == POB_ANT ? 10 : POB_MAXB));
+  constexpr int MAXI = (16 * NMAX * 4 + 255) / 256;  // 16-B chunks per lane of one array
+  if ((flags & POB_F_STAGED) && NMAX <= 16 && 16 * N * 7 <= POB_STAGE_FLOATS) {
+    // pairs (pos, rot), (vel, ang): both arrays' loads in flight before either is consumed
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int c0 = 3, c1 = pr == 0 ? 4 : 3;
+      const int n0 = nenv * N * c0, n1 = nenv * N * c1;
+      ChunkLoad<QT, MAXI> A0, A1;
+      A0.issue(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, lane);
+      A1.issue(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, lane);
+      A0.put(stg, n0, lane);
+      A1.put(stg + n0, n1, lane);
+      wave_lds_sync();
+      if (act_lane) {
+#pragma unroll
+        for (int l = 0; l < QNB; ++l) {
+          const int g = qbody_global(l, k);
+          const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
+          if (pr == 0) {
+            bd.x[l] = V(s0[0], s0[1], s0[2]);
+            bd.q[l].w = s1[0]; bd.q[l].x = s1[1]; bd.q[l].y = s1[2]; bd.q[l].z = s1[3];
+          } else {
+            bd.v[l] = V(s0[0], s0[1], s0[2]);
+            bd.w[l] = V(s1[0], s1[1], s1[2]);
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  } else if (flags & POB_F_STAGED) {
 #pragma unroll
     for (int arr = 0; arr < 4; ++arr) {
       const int c = arr == 1 ? 4 : 3;

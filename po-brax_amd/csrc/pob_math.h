@@ -21,7 +21,42 @@ POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return 
 POB_D v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 POB_D v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 POB_D v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
-POB_D v3 vdivs(v3 a, float s) { float inv = 1.0f / s; return V(a.x * inv, a.y * inv, a.z * inv); }
+// Correctly rounded 1/x and sqrt(x) for |x| in [2^-96, 2^96] without the full IEEE
+// expansions: hardware estimate + FMA correction (checked against IEEE 1/x and sqrtf on
+// every float32 in that range by scripts/check_fast_ieee.hip); other inputs take the IEEE
+// operation.  Same results as the oracle's 1.0f / x and sqrtf(x).
+POB_D bool pob_fast_range(float x) {
+  const float a = fabsf(x);
+  return a >= 0x1p-96f && a <= 0x1p+96f;
+}
+POB_D float pob_rcp_fast(float x) {
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float e = FMA(-x, y, 1.0f);
+  return FMA(e, y, y);
+}
+POB_D float pob_sqrt_fast(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rdn = FMA(-sdn, s, x), rup = FMA(-sup, s, x);
+  float r = rdn <= 0.0f ? sdn : s;
+  r = rup > 0.0f ? sup : r;
+  return r;
+}
+// the IEEE slow paths are out-of-line so that the compiler does not speculate them
+__device__ __attribute__((noinline)) float pob_rcp_ieee(float x) { return 1.0f / x; }
+__device__ __attribute__((noinline)) float pob_sqrt_ieee(float x) { return sqrtf(x); }
+POB_D float pob_rcp(float x) {
+  float r = pob_rcp_fast(x);
+  if (!pob_fast_range(x)) r = pob_rcp_ieee(x);
+  return r;
+}
+POB_D float pob_sqrt(float x) {
+  float r = pob_sqrt_fast(x);
+  if (!pob_fast_range(x)) r = pob_sqrt_ieee(x);
+  return r;
+}
+
+POB_D v3 vdivs(v3 a, float s) { float inv = pob_rcp(s); return V(a.x * inv, a.y * inv, a.z * inv); }
 POB_D float vdot(v3 a, v3 b) { return FMA(a.z, b.z, FMA(a.y, b.y, a.x * b.x)); }
 POB_D v3 vcross(v3 a, v3 b) {
   return V(FMA(a.y, b.z, -(a.z * b.y)), FMA(a.z, b.x, -(a.x * b.z)), FMA(a.x, b.y, -(a.y * b.x)));
@@ -70,8 +105,8 @@ POB_D v3 qrot_add(v3 v, q4 q, v3 x) {
            FMA(t2, u.z, FMA(c, v.z, FMA(s2, cr.z, x.z))));
 }
 POB_D q4 qnormalize(q4 q) {
-  float n = sqrtf(FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w))));
-  float inv = 1.0f / n;
+  float n = pob_sqrt(FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w))));
+  float inv = pob_rcp(n);
   q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
   return r;
 }
@@ -86,7 +121,7 @@ POB_D void qadd_half(q4 &acc, q4 d, float sign) {
 POB_D float pob_atanf(float x) {
   float sign = 1.0f, y = 0.0f;
   if (x < 0.0f) { sign = -1.0f; x = -x; }
-  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -(1.0f / x); }
+  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -pob_rcp(x); }
   else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = (x - 1.0f) / (x + 1.0f); }
   float z = x * x;
   y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -

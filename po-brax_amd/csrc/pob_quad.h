@@ -202,7 +202,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
       v3 dp = vsub(cp, cprev);
       v3 dpt = vfma(n, -vdot(dp, n), dp);
-      float lt = sqrtf(vdot(dpt, dpt));
+      float lt = pob_sqrt(vdot(dpt, dpt));
       if (lt > 0.0f) {
         v3 t = vdivs(dpt, lt);
         v3 ctn = vcross(rr, t);
@@ -238,14 +238,14 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 vr = vadd(b.v[l], vcross(b.w[l], rr));
       float vn = vdot(vr, n);
       v3 vt = vfma(n, -vn, vr);
-      float lt = sqrtf(vdot(vt, vt));
+      float lt = pob_sqrt(vdot(vt, vt));
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
         dv = vscl(vt, -(fr / lt));
       }
       if (vn < 0.0f) dv = vfma(n, -vn, dv);
-      float D = sqrtf(vdot(dv, dv));
+      float D = pob_sqrt(vdot(dv, dv));
       if (D > 0.0f) {
         v3 dh = vdivs(dv, D);
         v3 cd = vcross(rr, dh);
@@ -277,7 +277,7 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   v3 rp = qrot(QJV(LT, jl, QJ_OFFP), b.q[p]);
   v3 rc = qrot(QJV(LT, jl, QJ_OFFC), b.q[c]);
   v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
-  float L = sqrtf(vdot(d, d));
+  float L = pob_sqrt(vdot(d, d));
   // P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway
   v3 P = V(0.0f, 0.0f, 0.0f);
   if (L > 0.0f) {

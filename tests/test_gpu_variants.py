@@ -170,3 +170,29 @@ def test_stock_ant_env_surface():
     assert pos.shape == (8, 13) and vel.shape == (8, 14) and cfrc.shape == (8, 60)
     assert torch.equal(pos[:, 0], s.qp.pos[:, 0, 2])       # torso z
     assert torch.equal(vel[:, :3], s.qp.vel[:, 0])          # torso velocity
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather"])
+def test_unaligned_state_uses_fallback_loads(name):
+    """qp tensors that are not 16-B aligned take the per-lane load path (no vector loads);
+    results must equal the aligned (staged) path bit for bit."""
+    from po_brax_amd import envs
+    B = 70  # ragged: the last wave holds 6 envs
+    env = envs.create(name, batch_size=B, episode_length=50)
+    s = env.reset(torch.from_numpy(_keys(B, 13)).cuda())
+
+    def shifted(t):  # same values, storage offset by one element -> 4-B aligned only
+        buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=t.device)
+        v = buf[1:].view(t.shape)
+        v.copy_(t)
+        return v
+
+    qp2 = type(s.qp)(shifted(s.qp.pos), shifted(s.qp.rot), shifted(s.qp.vel), shifted(s.qp.ang))
+    assert qp2.pos.data_ptr() % 16 != 0
+    s2 = s.replace(qp=qp2)
+    act = torch.rand((B, 8), device="cuda") * 2 - 1
+    a = env.step(s, act)
+    b2 = env.step(s2, act)
+    for f in QP:
+        assert torch.equal(getattr(a.qp, f), getattr(b2.qp, f)), f
+    assert torch.equal(a.obs, b2.obs) and torch.equal(a.reward, b2.reward)
