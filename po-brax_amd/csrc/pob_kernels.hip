@@ -409,10 +409,11 @@ POB_D void stage_store_dyn(float *X, size_t el0, int N, int nenv, const float *s
   }
 }
 
-// stage the per-leg table in LDS (all threads of the block; before any divergence)
+// stage the block table (leg rows, then wall rows) in LDS (all threads of the block;
+// before any divergence)
 POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
-  const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];  // [4][POB_LEG_FLOATS], contiguous
-  for (int i = (int)threadIdx.x; i < 4 * POB_LEG_FLOATS; i += (int)blockDim.x) legtab[i] = src[i];
+  const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];  // leg[4][..], wall_row[..][8]
+  for (int i = (int)threadIdx.x; i < POB_TAB_FLOATS; i += (int)blockDim.x) legtab[i] = src[i];
   __syncthreads();
 }
 template <int KIND, typename QT>
@@ -426,6 +427,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   const int b = gt >> 2;
   const int k = gt & 3;
   const float *LT = legtab + k * POB_LEG_FLOATS;
+  const float *WT = legtab + 4 * POB_LEG_FLOATS;
   const int kind = KIND != POB_MIXED ? KIND : S.kind;
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   const int sh = obs_shift(kind);
@@ -514,11 +516,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     const int iters = Sp->substeps / 2;
 #pragma nounroll
 #if defined(POB_EXP_NO_COLLIDE)
-    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
-    for (int it = 0; it < 0 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
 #else
-    for (int it = 0; it < 2 * iters; ++it) qpbd_substep(Sp, LT, bd, a, Ls, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0);
 #endif
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
@@ -676,7 +678,7 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
                                                                        const StatePtrs out, const uint32_t flags,
                                                                        const int L) {
   __shared__ float lds[QL_FLOATS * 256];
-  __shared__ float legtab[4 * POB_LEG_FLOATS];
+  __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
                            (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
@@ -708,7 +710,7 @@ template <typename QT>
 __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_mixed(const MixArgs A, const uint32_t flags,
                                                                         const int L) {
   __shared__ float lds[QL_FLOATS * 256];
-  __shared__ float legtab[4 * POB_LEG_FLOATS];
+  __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
   const int bx = (int)blockIdx.x;
   int seg = 0;
 #pragma unroll

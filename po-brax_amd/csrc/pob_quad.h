@@ -108,7 +108,44 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
   return c == 0 ? S.ground_r[0] : LT[POB_LEG_GROUND + 3];
 }
 
-POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
+// sphere_box (pob_physics.h) on a wall row staged in LDS (R = centre x, y, cos, sin,
+// half-extent x, y; z from the system).  Same operations in the same order.
+POB_D float qsphere_box(csys_t &S, const float *R, v3 p, float r, v3 &n) {
+  const float2 r01 = *reinterpret_cast<const float2 *>(R);
+  const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
+  const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
+  const float c = r23.x, s = r23.y;
+  const v3 h = V(r45.x, r45.y, S.wall_hz);
+  v3 d = vsub(p, V(r01.x, r01.y, S.wall_cz));
+  float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
+  float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
+  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
+  float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
+  float pen, nx, ny, nz;
+  if (d2 > 0.0f) {
+    float dist = pob_sqrt(d2);
+    const float inv = pob_rcp(dist);
+    pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
+  } else {
+    float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
+    nx = 0.0f; ny = 0.0f; nz = 0.0f;
+    if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
+    else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
+    else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
+  }
+  n = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
+  return pen;
+}
+
+// Contact detection of a collide substep on a lane quad.  Walls: every lane keeps a mask
+// of the walls whose grown box (pob_sys::wall_lo/hi) meets the AABB of its three body
+// centres, and walks ITS OWN mask in increasing wall order, so one pass over a wall row
+// serves lanes near different walls (a wave-uniform wall loop would run every wall any of
+// the 16 envs is near).  Culled pairs have penetration < 0 and the walk keeps the oracle's
+// (wall, end) order with the strict ">" -- the deepest contact is unchanged.
+// WALLS = false compiles the wall search out (the stock ant has no walls).
+template <bool WALLS>
+POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QContacts &ct) {
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     csys_t &S = *launder(Sp);
@@ -116,8 +153,8 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
     v3 pe = qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
     ct.pen[c] = qground_r(S, LT, c) - pe.z;
   }
-  uint32_t near_mask = 0u;
-  {
+  uint32_t lane_mask = 0u;
+  if (WALLS) {
     v3 mn = b.x[0], mx = b.x[0];
 #pragma unroll
     for (int l = 1; l < QNB; ++l) {
@@ -125,13 +162,18 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
       mx = V(fmaxf(mx.x, b.x[l].x), fmaxf(mx.y, b.x[l].y), fmaxf(mx.z, b.x[l].z));
     }
     csys_t &S = *launder(Sp);
+#ifdef POB_EXP_NO_WALLS
+    const int nw = 0;  // timing experiment only
+#else
     const int nw = S.n_walls;
+#endif
     for (int w = 0; w < nw; ++w) {
       const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
                         mx.y >= S.wall_lo[w][1] && mn.z <= S.wall_hi[w][2] && mx.z >= S.wall_lo[w][2];
-      if (__any(near)) near_mask |= 1u << w;
+      lane_mask |= near ? 1u << w : 0u;
     }
   }
+  const bool any_near = WALLS && __any(lane_mask != 0u);
 #pragma unroll
   for (int l = 0; l < QNB; ++l) {
     POB_FENCE();
@@ -140,19 +182,21 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const QBody &b, QContacts &ct) {
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
-    if (near_mask != 0u) {
+    if (any_near) {
       v3 pe[2];
 #pragma unroll
       for (int q = 0; q < nend; ++q) pe[q] = qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
       const float r = q_cap_r(S, LT, l);
-      const int nw = S.n_walls;
-      for (int w = 0; w < nw; ++w) {
-        if (!(near_mask & (1u << w))) continue;
+      uint32_t m = lane_mask;
+      while (__any(m != 0u)) {
+        const bool on = m != 0u;
+        const int w = on ? __builtin_ctz(m) : 0;
+        m &= m - 1u;
 #pragma unroll
         for (int q = 0; q < nend; ++q) {
           v3 n;
-          float pen = sphere_box(S, w, pe[q], r, n);
-          if (pen > best) { best = pen; bn = n; bsel = q == 1; }
+          float pen = qsphere_box(S, WT + POB_WALL_FLOATS * w, pe[q], r, n);
+          if (on && pen > best) { best = pen; bn = n; bsel = q == 1; }
         }
       }
     }
@@ -329,7 +373,8 @@ POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t, const float imp0) {
 }
 
 // One XPBD substep on a lane quad (see the header comment for the split).
-POB_D void qpbd_substep(csys_t *Sp, const float *LT, QBody &b, const float (&act)[QNJ], const Lds &L,
+template <bool WALLS>
+POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const Lds &L,
                         const bool COLLIDE) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
@@ -393,7 +438,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, QBody &b, const float (&act
       qtorso_add<3>(DX[0], DQ[0], tq, imp0);
     }
     if (COLLIDE) {
-      qdetect(Sp, LT, b, ct);
+      qdetect<WALLS>(Sp, LT, WT, b, ct);
       qcontact_position(Sp, LT, b, L, ct, DX, DQ);
     }
 #pragma unroll

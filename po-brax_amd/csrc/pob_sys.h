@@ -7,6 +7,7 @@
 // joints, parent(j) = j odd ? j : 0, child(j) = j + 1; ground contacts on bodies
 // 0,2,4,6,8); every number (offsets, axes, limits, masses, capsules, walls) is data.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #define POB_NDYN 9      // dynamic ant bodies
@@ -23,6 +24,11 @@
 #define POB_LEG_BODY(l) (32 + 8 * ((l) - 1))  // inv_mass cap_r cap_end[2][3]   (l = 1, 2)
 #define POB_LEG_GROUND 48               // ground_end(3) ground_r
 #define POB_LEG_FLOATS 52
+// wall rows staged behind the leg table: centre x, y, cos, sin, half-extent x, y (every
+// wall shares centre z and half-extent z: pob_sys::wall_cz / wall_hz).  4 leg rows + 8 wall
+// rows = 1 KiB, which keeps the quad kernel's LDS at 40 KiB per block (4 blocks per CU).
+#define POB_WALL_FLOATS 6
+#define POB_TAB_FLOATS (4 * POB_LEG_FLOATS + POB_MAXW * POB_WALL_FLOATS)
 
 struct pob_sys {
   int kind, N, D, n_obj;
@@ -45,6 +51,7 @@ struct pob_sys {
   // wave skips a wall when no lane's body centres fall inside it (exact: every culled
   // sphere-box pair has penetration < 0, so the deepest-contact search is unchanged)
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
+  float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
   float friction, s_pos, half_s_ang;
   // default_qp rows of the frozen bodies (index >= 9)
   float frozen_pos[POB_MAXB][3];
@@ -54,7 +61,10 @@ struct pob_sys {
   float tag_tag_radius, tag_visible_radius, tag_target_step, tag_min_spawn_distance;
   float tag_cage_xy[2], tag_dying_cost;
   float leg[4][POB_LEG_FLOATS];  // gathered copies of the per-leg rows above
+  float wall_row[POB_MAXW][POB_WALL_FLOATS];  // the walls again, one row each (follows leg)
   float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
   int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)
   const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env
 };
+static_assert(offsetof(pob_sys, wall_row) == offsetof(pob_sys, leg) + sizeof(float) * 4 * POB_LEG_FLOATS,
+              "the block table (leg rows, wall rows) is staged as one contiguous copy");

@@ -229,6 +229,13 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     for (int c = 0; c < 3; ++c) L[POB_LEG_GROUND + c] = s.ground_end[k + 1][c];
     L[POB_LEG_GROUND + 3] = s.ground_r[k + 1];
   }
+  s.wall_cz = 0.5f; s.wall_hz = 0.5f;
+  for (int w = 0; w < s.n_walls; ++w) {
+    if (s.wall_c[w][2] != s.wall_cz || s.wall_h[w][2] != s.wall_hz) return "walls: centre z / half height differ";
+    float *R = s.wall_row[w];
+    R[0] = s.wall_c[w][0]; R[1] = s.wall_c[w][1]; R[2] = s.wall_cos[w];
+    R[3] = s.wall_sin[w]; R[4] = s.wall_h[w][0]; R[5] = s.wall_h[w][1];
+  }
   // broadphase boxes: wall AABB + the largest distance from a body centre to any point of
   // its capsule (|end| + r) + 1e-3 margin (>> float rounding of the sphere-box distance)
   double reach = 0.0;
