@@ -108,9 +108,13 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
   return c == 0 ? S.ground_r[0] : LT[POB_LEG_GROUND + 3];
 }
 
-// sphere_box (pob_physics.h) on a wall row staged in LDS (R = centre x, y, cos, sin,
-// half-extent x, y; z from the system).  Same operations in the same order.
-POB_D float qsphere_box(csys_t &S, const float *R, v3 p, float r, v3 &n) {
+// sphere_box (pob_physics.h) of end point p against the wall row R staged in LDS
+// (centre x, y, cos, sin, half-extent x, y; z from the system), folded into the deepest-
+// contact search: same operations in the same order, but the square root, normal and
+// compare run only when d2 < T = r^2 (1 + 2^-20) (or d2 is NaN).  Exact: d2 >= T gives
+// sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
+POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
+                     bool &bsel) {
   const float2 r01 = *reinterpret_cast<const float2 *>(R);
   const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
   const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
@@ -121,20 +125,25 @@ POB_D float qsphere_box(csys_t &S, const float *R, v3 p, float r, v3 &n) {
   float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
   float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
-  float pen, nx, ny, nz;
-  if (d2 > 0.0f) {
-    float dist = pob_sqrt(d2);
-    const float inv = pob_rcp(dist);
-    pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
-  } else {
-    float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
-    nx = 0.0f; ny = 0.0f; nz = 0.0f;
-    if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
-    else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
-    else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
+  if (!(d2 >= T)) {
+    float pen, nx, ny, nz;
+    if (d2 > 0.0f) {
+      float dist = pob_sqrt(d2);
+      const float inv = pob_rcp(dist);
+      pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
+    } else {
+      float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
+      nx = 0.0f; ny = 0.0f; nz = 0.0f;
+      if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
+      else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
+      else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
+    }
+    if (on && pen > best) {
+      best = pen;
+      bn = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
+      bsel = q1;
+    }
   }
-  n = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
-  return pen;
 }
 
 // Contact detection of a collide substep on a lane quad.  Walls: every lane keeps a mask
@@ -155,11 +164,11 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
   }
   uint32_t lane_mask = 0u;
   if (WALLS) {
-    v3 mn = b.x[0], mx = b.x[0];
+    float mnx = b.x[0].x, mxx = b.x[0].x, mny = b.x[0].y, mxy = b.x[0].y;
 #pragma unroll
     for (int l = 1; l < QNB; ++l) {
-      mn = V(fminf(mn.x, b.x[l].x), fminf(mn.y, b.x[l].y), fminf(mn.z, b.x[l].z));
-      mx = V(fmaxf(mx.x, b.x[l].x), fmaxf(mx.y, b.x[l].y), fmaxf(mx.z, b.x[l].z));
+      mnx = fminf(mnx, b.x[l].x); mxx = fmaxf(mxx, b.x[l].x);
+      mny = fminf(mny, b.x[l].y); mxy = fmaxf(mxy, b.x[l].y);
     }
     csys_t &S = *launder(Sp);
 #ifdef POB_EXP_NO_WALLS
@@ -168,8 +177,9 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
     const int nw = S.n_walls;
 #endif
     for (int w = 0; w < nw; ++w) {
-      const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
-                        mx.y >= S.wall_lo[w][1] && mn.z <= S.wall_hi[w][2] && mx.z >= S.wall_lo[w][2];
+      // xy only: dropping the z test can only keep more walls (the cull stays exact)
+      const bool near = mnx <= S.wall_hi[w][0] && mxx >= S.wall_lo[w][0] && mny <= S.wall_hi[w][1] &&
+                        mxy >= S.wall_lo[w][1];
       lane_mask |= near ? 1u << w : 0u;
     }
   }
@@ -187,17 +197,14 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
 #pragma unroll
       for (int q = 0; q < nend; ++q) pe[q] = qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
       const float r = q_cap_r(S, LT, l);
+      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), rounded products
       uint32_t m = lane_mask;
       while (__any(m != 0u)) {
         const bool on = m != 0u;
         const int w = on ? __builtin_ctz(m) : 0;
         m &= m - 1u;
 #pragma unroll
-        for (int q = 0; q < nend; ++q) {
-          v3 n;
-          float pen = qsphere_box(S, WT + POB_WALL_FLOATS * w, pe[q], r, n);
-          if (on && pen > best) { best = pen; bn = n; bsel = q == 1; }
-        }
+        for (int q = 0; q < nend; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel);
       }
     }
     ct.pen[2 + l] = best;

@@ -307,3 +307,61 @@ def test_large_batch_properties():
     r, d = s.reward, s.done
     assert bool(((r != 0) <= (d != 0)).all())  # every non-zero reward ends the episode (HH)
     assert set(torch.unique(r).tolist()) <= {-2.0, -1.0, 0.0, 1.0}
+
+
+# ------------------------------------------------------------------- wall contacts
+def _walls(name):
+    """(centre xy, z-rotation deg, half-extent xy) of the arena walls, from the brax config
+    export (checked against SURVEY.md Appendix A in tests/test_export.py)."""
+    import ctypes as C
+    from po_brax_amd import _lib
+    from po_brax_amd.io.config import brax_config_of
+    p = _lib.pob_params()
+    assert _lib.lib.pob_default_params(C.byref(p)) == 0
+    arena = [b for b in brax_config_of(name, p)["bodies"] if b["name"] == "Arena"][0]
+    return [((c["position"]["x"], c["position"]["y"]), c["rotation"]["z"],
+             (c["box"]["halfsize"]["x"], c["box"]["halfsize"]["y"])) for c in arena["colliders"]]
+
+
+def _near_wall(xy, walls, reach):
+    """bool per point: within `reach` of some wall box (xy only)."""
+    hit = np.zeros(len(xy), bool)
+    for (cx, cy), rz, (hx, hy) in walls:
+        a = np.deg2rad(rz)
+        d = xy - np.array([cx, cy])
+        lx = d[:, 0] * np.cos(a) + d[:, 1] * np.sin(a)
+        ly = -d[:, 0] * np.sin(a) + d[:, 1] * np.cos(a)
+        ex = np.maximum(np.abs(lx) - hx, 0)
+        ey = np.maximum(np.abs(ly) - hy, 0)
+        hit |= np.hypot(ex, ey) < reach
+    return hit
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag"])
+def test_step_parity_against_walls(name):
+    """Ants teleported onto random points of the arena's bounding box (many start touching
+    or inside a wall): every sphere-box branch (outside, inside, deepest-end selection,
+    several walls per wave) runs; one-step parity for 8 steps."""
+    B, T = 512, 8
+    env = _envs().create(name, batch_size=B, episode_length=1000)
+    s = env.reset(torch.from_numpy(_keys(B, 5)).cuda())
+    walls = _walls(name)
+    ext = np.array([[abs(c[0]) + max(h), abs(c[1]) + max(h)] for c, _, h in walls]).max(0)
+    lo = np.array([-ext[0], min(c[1] - max(h) for c, _, h in walls)])
+    hi = np.array([ext[0], max(c[1] + max(h) for c, _, h in walls)])
+    rng = np.random.default_rng(7)
+    cand = rng.uniform(lo, hi, (64 * B, 2))
+    close_ = cand[_near_wall(cand, walls, 1.0)]
+    xy = np.concatenate([close_[: 3 * B // 4], cand[: B - 3 * B // 4]]).astype(np.float32)
+    xy = xy[rng.permutation(B)]
+    torso = _np(s.qp.pos)[:, 0, :2]
+    off = torch.from_numpy(xy - torso).cuda()
+    s.qp.pos[:, :9, :2] += off[:, None, :]  # the 9 ant bodies
+    near = _near_wall(xy.astype(np.float64), walls, 1.0)
+    assert near.sum() >= 3 * B // 4, near.sum()
+    o = orc.OracleEnv(name)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        so = o.step(_state_np(s), act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=1000)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} wall step {t}")
