@@ -365,3 +365,31 @@ def test_step_parity_against_walls(name):
         so = o.step(_state_np(s), act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=1000)
         s = env.step(s, torch.from_numpy(act).cuda())
         compare_states(s, so, f"{name} wall step {t}")
+
+
+# ---------------------------------------------------------------------- ragged batches
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("B", [1, 5, 17, 63])
+def test_ragged_batch_parity(name, B):
+    """Batches that leave a partial wave (16 envs / wave): the tail wave's staged loads and
+    stores and its idle lanes must not touch other rows.  Short episodes so autoreset runs."""
+    T = 12
+    env = _envs().create(name, batch_size=B, episode_length=5)
+    s = env.reset(torch.from_numpy(_keys(B, 11)).cuda())
+    o = orc.OracleEnv(name)
+    rng = np.random.default_rng(B)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        so = o.step(_state_np(s), act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=5)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} B={B} step {t}")
+
+
+def test_batch_size_zero_follows_reference():
+    """envs/__init__.py:64 (`if batch_size:`): create(batch_size=0) is the unbatched env;
+    create_gym_env rejects batch_size <= 0 with ValueError (:115-117)."""
+    envs = _envs()
+    s = envs.create("ant_heavenhell", batch_size=0).reset(torch.tensor([0, 0], dtype=torch.uint32))
+    assert s.obs.shape == (114,)
+    with pytest.raises(ValueError):
+        envs.create_gym_env("ant_heavenhell", batch_size=0)
