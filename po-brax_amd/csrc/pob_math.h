@@ -45,14 +45,22 @@ POB_D float pob_sqrt_fast(float x) {
 // the IEEE slow paths are out-of-line so that the compiler does not speculate them
 __device__ __attribute__((noinline)) float pob_rcp_ieee(float x) { return 1.0f / x; }
 __device__ __attribute__((noinline)) float pob_sqrt_ieee(float x) { return sqrtf(x); }
+// wave-uniform guard: the common case (every lane in range) is one compare and a
+// not-taken scalar branch, without exec-mask save/restore
 POB_D float pob_rcp(float x) {
   float r = pob_rcp_fast(x);
-  if (!pob_fast_range(x)) r = pob_rcp_ieee(x);
+  const bool slow = !pob_fast_range(x);
+  if (__builtin_expect(__any(slow), 0)) {
+    if (slow) r = pob_rcp_ieee(x);
+  }
   return r;
 }
 POB_D float pob_sqrt(float x) {
   float r = pob_sqrt_fast(x);
-  if (!pob_fast_range(x)) r = pob_sqrt_ieee(x);
+  const bool slow = !pob_fast_range(x);
+  if (__builtin_expect(__any(slow), 0)) {
+    if (slow) r = pob_sqrt_ieee(x);
+  }
   return r;
 }
 
