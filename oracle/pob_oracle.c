@@ -560,11 +560,11 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   ct->count = k;
 }
 
-static void qadd_half(q4 *acc, q4 d, float sign);
-
-/* position-level contact projection (normal + static friction) into DX/DQ */
+/* position-level contact projection (normal + static friction) into DX / DA (DA: the
+ * body's accumulated angular correction vector, turned into a rotation update once at the
+ * end of the projection) */
 static void contact_position(const orc_env *e, const body_t *b, const body_t *prev,
-                             const contacts_t *ct, v3 *DX, q4 *DQ) {
+                             const contacts_t *ct, v3 *DX, v3 *DA) {
   for (int k = 0; k < ct->count; ++k) {
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
@@ -577,9 +577,8 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     float w = im + vdot(cn, cn);
     float lam = pen / w;
     v3 P = vscl(n, lam);
-    q4 dq = qmul_vq(vcross(rr, P), b->q[i]);
     DX[i] = vfma(P, im, DX[i]);
-    qadd_half(&DQ[i], dq, 1.0f);
+    DA[i] = vadd(DA[i], vcross(rr, P));
     /* static friction against the motion of the contact point over the substep */
     v3 cprev = qrot_add(qrot(rr, qinv(b->q[i])), prev->q[i], prev->x[i]);
     v3 dp = vsub(cp, cprev);
@@ -595,9 +594,8 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
       if (lamt < e->friction * lam) {
         FL(8);
         v3 Pt = vscl(t, -lamt);
-        q4 dqt = qmul_vq(vcross(rr, Pt), b->q[i]);
         DX[i] = vfma(Pt, im, DX[i]);
-        qadd_half(&DQ[i], dqt, 1.0f);
+        DA[i] = vadd(DA[i], vcross(rr, Pt));
       }
     }
   }
@@ -641,13 +639,18 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
 /* ------------------------------------------------------------------ the PBD step */
 /* acc += sign * 0.5 * d as one fused multiply-add per component (sign * 0.5 exact) */
 static void qadd_half(q4 *acc, q4 d, float sign) {
-  FL(12);
+  FL(9);
   const float h = 0.5f * sign;
   acc->w = fmaf(h, d.w, acc->w); acc->x = fmaf(h, d.x, acc->x);
   acc->y = fmaf(h, d.y, acc->y); acc->z = fmaf(h, d.z, acc->z);
 }
 
-static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
+/* Jacobi joint projection.  Every angular correction of a body in one substep is applied
+ * through the SAME quaternion (the body's pose at the start of the projection), so the
+ * per-constraint rotation updates 0.5 [0, a_k] q are summed as vectors first
+ * (sum_k 0.5 [0, a_k] q = 0.5 [0, sum_k a_k] q): per joint, s = Pa + Pl, parent
+ * += (rp x P) + s, child -= (rc x P) + s; the quaternion product happens once per body. */
+static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
   for (int j = 0; j < NJ; ++j) {
     int p = jparent(j), c = jchild(j);
     float imp = e->inv_mass[p], imc = e->inv_mass[c];
@@ -667,14 +670,11 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
       P = vscl(n, lam);
     }
     DX[p] = vfma(P, imp, DX[p]);
-    qadd_half(&DQ[p], qmul_vq(vcross(rp, P), b->q[p]), 1.0f);
     DX[c] = vfma(P, -imc, DX[c]);
-    qadd_half(&DQ[c], qmul_vq(vcross(rc, P), b->q[c]), -1.0f);
+    v3 xp = vcross(rp, P), xc = vcross(rc, P);
     /* hinge axis alignment (unit inverse inertia: w_p = w_c = 1) */
     v3 ap = qrot(e->axis[j], b->q[p]), ac = qrot(e->axis[j], b->q[c]);
     v3 Pa = vscl(vcross(ap, ac), e->half_s_ang);
-    qadd_half(&DQ[p], qmul_vq(Pa, b->q[p]), 1.0f);
-    qadd_half(&DQ[c], qmul_vq(Pa, b->q[c]), -1.0f);
     /* angle limits (brax math.signed_angle about the parent's hinge axis) */
     v3 fp = qrot(e->ref[j], b->q[p]), fc = qrot(e->ref[j], b->q[c]);
     float psi = orc_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
@@ -683,8 +683,9 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, q4 *DQ) {
     else if (psi > e->lim_hi[j]) { FL(1); dl = psi - e->lim_hi[j]; }
     FL(1);
     v3 Pl = vscl(ap, dl * e->half_s_ang);
-    qadd_half(&DQ[p], qmul_vq(Pl, b->q[p]), 1.0f);
-    qadd_half(&DQ[c], qmul_vq(Pl, b->q[c]), -1.0f);
+    v3 s = vadd(Pa, Pl);
+    DA[p] = vadd(DA[p], vadd(xp, s));
+    DA[c] = vsub(DA[c], vadd(xc, s));
   }
 }
 
@@ -722,18 +723,17 @@ static void pbd_substep(const orc_env *e, body_t *b, const float *act, int colli
     b->q[i] = qnormalize(q);
   }
   /* 3. position projection (Jacobi over joints + contacts) */
-  v3 DX[NDYN]; q4 DQ[NDYN];
-  for (int i = 0; i < NDYN; ++i) { DX[i] = V(0, 0, 0); DQ[i].w = DQ[i].x = DQ[i].y = DQ[i].z = 0.0f; }
-  joints_position(e, b, DX, DQ);
+  v3 DX[NDYN], DA[NDYN];
+  for (int i = 0; i < NDYN; ++i) { DX[i] = V(0, 0, 0); DA[i] = V(0, 0, 0); }
+  joints_position(e, b, DX, DA);
   contacts_t ct; ct.count = 0;
   if (collide) {
     detect(e, b, &ct);
-    contact_position(e, b, &prev, &ct, DX, DQ);
+    contact_position(e, b, &prev, &ct, DX, DA);
   }
   for (int i = 0; i < NDYN; ++i) {
-    FL(4);
     b->x[i] = vadd(b->x[i], DX[i]);
-    b->q[i].w += DQ[i].w; b->q[i].x += DQ[i].x; b->q[i].y += DQ[i].y; b->q[i].z += DQ[i].z;
+    qadd_half(&b->q[i], qmul_vq(DA[i], b->q[i]), 1.0f);
   }
   /* 4. velocity projection */
   for (int i = 0; i < NDYN; ++i) {

@@ -53,10 +53,6 @@ POB_D float quad_bcast_b(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), J * 0x55, 0xf, 0xf, false));
 }
 template <int J> POB_D v3 quad_bcast3(v3 a) { return V(quad_bcast_b<J>(a.x), quad_bcast_b<J>(a.y), quad_bcast_b<J>(a.z)); }
-template <int J> POB_D q4 quad_bcast4(q4 a) {
-  q4 r; r.w = quad_bcast_b<J>(a.w); r.x = quad_bcast_b<J>(a.x); r.y = quad_bcast_b<J>(a.y); r.z = quad_bcast_b<J>(a.z);
-  return r;
-}
 
 // Leg tables: each block stages pob_sys::leg (4 legs x POB_LEG_FLOATS) in LDS, and a lane
 // reads its own leg's row through LT = leg table + k * POB_LEG_FLOATS (ds_read_b32; the
@@ -228,7 +224,7 @@ POB_D void qcontact_geom(csys_t &S, const float *LT, const QContacts &ct, int c,
 
 // contact processing order of one body = oracle order (ground contact first, then wall)
 POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const Lds &L, const QContacts &ct,
-                             v3 (&DX)[QNB], q4 (&DQ)[QNB]) {
+                             v3 (&DX)[QNB], v3 (&DA)[QNB]) {
 #pragma unroll
   for (int c = 0; c < 2 + QNB; ++c) {
     POB_FENCE();
@@ -247,9 +243,8 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       float w = im + vdot(cn, cn);
       float lam = pen / w;
       v3 P = vscl(n, lam);
-      q4 dq = qmul_vq(vcross(rr, P), b.q[l]);
       DX[l] = vfma(P, im, DX[l]);
-      qadd_half(DQ[l], dq, 1.0f);
+      DA[l] = vadd(DA[l], vcross(rr, P));
       v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
       v3 dp = vsub(cp, cprev);
       v3 dpt = vfma(n, -vdot(dp, n), dp);
@@ -261,9 +256,8 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
         float lamt = lt / wt;
         if (lamt < S.friction * lam) {
           v3 Pt = vscl(t, -lamt);
-          q4 dqt = qmul_vq(vcross(rr, Pt), b.q[l]);
           DX[l] = vfma(Pt, im, DX[l]);
-          qadd_half(DQ[l], dqt, 1.0f);
+          DA[l] = vadd(DA[l], vcross(rr, Pt));
         }
       }
     }
@@ -310,15 +304,16 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
 }
 
 // torso terms of the lane's hip joint (global 2k): the oracle adds P * imp to DX[0] and
-// +0.5 * (dqp, dqh, dql) to DQ[0], each as fused multiply-adds in joint order
+// t = (rp x P) + (Pa + Pl) to DA[0], in joint order
 struct QTorso {
-  v3 P;              // point-constraint impulse (zero if the anchors coincide)
-  q4 dqp, dqh, dql;  // point, hinge and limit rotation terms (raw quat_mul results)
+  v3 P;  // point-constraint impulse (zero if the anchors coincide)
+  v3 t;  // angular correction of the torso
 };
 
-// local joint jl's point / hinge / limit corrections into DX/DQ (local bodies); for the
-// hip (jl = 0) the torso terms go to *tt
-POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const int jl, v3 (&DX)[QNB], q4 (&DQ)[QNB],
+// local joint jl's point / hinge / limit corrections into DX / DA (local bodies; DA = the
+// angular correction vectors, applied as one rotation update per body -- oracle
+// joints_position); for the hip (jl = 0) the torso terms go to *tt
+POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const int jl, v3 (&DX)[QNB], v3 (&DA)[QNB],
                            QTorso *tt) {
   csys_t &S = *launder(Sp);
   const int p = jparent(jl), c = jchild(jl);
@@ -338,23 +333,15 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
     float lam = (L / wsum) * S.s_pos;
     P = vscl(n, lam);
   }
-  if (torso_parent) {
-    tt->P = P;
-    tt->dqp = qmul_vq(vcross(rp, P), b.q[p]);
-  } else {
-    DX[p] = vfma(P, imp, DX[p]);
-    qadd_half(DQ[p], qmul_vq(vcross(rp, P), b.q[p]), 1.0f);
-  }
+  if (torso_parent) tt->P = P;
+  else DX[p] = vfma(P, imp, DX[p]);
   DX[c] = vfma(P, -imc, DX[c]);
-  qadd_half(DQ[c], qmul_vq(vcross(rc, P), b.q[c]), -1.0f);
+  const v3 xp = vcross(rp, P), xc = vcross(rc, P);
   POB_FENCE();
   csys_t &S2 = *launder(Sp);
   const v3 axis = QJV(LT, jl, QJ_AXIS);
   v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
   v3 Pa = vscl(vcross(ap, ac), S2.half_s_ang);
-  if (torso_parent) tt->dqh = qmul_vq(Pa, b.q[p]);
-  else qadd_half(DQ[p], qmul_vq(Pa, b.q[p]), 1.0f);
-  qadd_half(DQ[c], qmul_vq(Pa, b.q[c]), -1.0f);
   POB_FENCE();
   csys_t &S3 = *launder(Sp);
   const v3 ref = QJV(LT, jl, QJ_REF);
@@ -365,18 +352,18 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   if (psi < lo) dl = psi - lo;
   else if (psi > hi) dl = psi - hi;
   v3 Pl = vscl(ap, dl * S3.half_s_ang);
-  if (torso_parent) tt->dql = qmul_vq(Pl, b.q[p]);
-  else qadd_half(DQ[p], qmul_vq(Pl, b.q[p]), 1.0f);
-  qadd_half(DQ[c], qmul_vq(Pl, b.q[c]), -1.0f);
+  const v3 s = vadd(Pa, Pl);
+  const v3 tp = vadd(xp, s);
+  if (torso_parent) tt->t = tp;
+  else DA[p] = vadd(DA[p], tp);
+  DA[c] = vsub(DA[c], vadd(xc, s));
 }
 
 // add quad lane J's hip terms onto the torso accumulators (global joint 2J)
 template <int J>
-POB_D void qtorso_add(v3 &dx, q4 &dq, const QTorso &t, const float imp0) {
+POB_D void qtorso_add(v3 &dx, v3 &da, const QTorso &t, const float imp0) {
   dx = vfma(quad_bcast3<J>(t.P), imp0, dx);
-  qadd_half(dq, quad_bcast4<J>(t.dqp), 1.0f);
-  qadd_half(dq, quad_bcast4<J>(t.dqh), 1.0f);
-  qadd_half(dq, quad_bcast4<J>(t.dql), 1.0f);
+  da = vadd(da, quad_bcast3<J>(t.t));
 }
 
 // One XPBD substep on a lane quad (see the header comment for the split).
@@ -427,31 +414,36 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   QContacts ct;
   {
     v3 DX[QNB];
-    q4 DQ[QNB];
+    v3 DA[QNB];
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) { DX[l] = V(0.0f, 0.0f, 0.0f); DQ[l].w = DQ[l].x = DQ[l].y = DQ[l].z = 0.0f; }
+    for (int l = 0; l < QNB; ++l) { DX[l] = V(0.0f, 0.0f, 0.0f); DA[l] = V(0.0f, 0.0f, 0.0f); }
     QTorso tq;
     POB_FENCE();
-    qjoint_position(Sp, LT, b, 0, DX, DQ, &tq);
+#ifdef POB_EXP_NO_JOINTS
+    tq.P = V(0.0f, 0.0f, 0.0f);  // timing experiment only
+    tq.t = tq.P;
+#else
+    qjoint_position(Sp, LT, b, 0, DX, DA, &tq);
     POB_FENCE();
-    qjoint_position(Sp, LT, b, 1, DX, DQ, nullptr);
+    qjoint_position(Sp, LT, b, 1, DX, DA, nullptr);
+#endif
     POB_FENCE();
     // torso: global joints 0, 2, 4, 6 (quad lanes 0..3) in order
     {
       const float imp0 = launder(Sp)->inv_mass[0];
-      qtorso_add<0>(DX[0], DQ[0], tq, imp0);
-      qtorso_add<1>(DX[0], DQ[0], tq, imp0);
-      qtorso_add<2>(DX[0], DQ[0], tq, imp0);
-      qtorso_add<3>(DX[0], DQ[0], tq, imp0);
+      qtorso_add<0>(DX[0], DA[0], tq, imp0);
+      qtorso_add<1>(DX[0], DA[0], tq, imp0);
+      qtorso_add<2>(DX[0], DA[0], tq, imp0);
+      qtorso_add<3>(DX[0], DA[0], tq, imp0);
     }
     if (COLLIDE) {
       qdetect<WALLS>(Sp, LT, WT, b, ct);
-      qcontact_position(Sp, LT, b, L, ct, DX, DQ);
+      qcontact_position(Sp, LT, b, L, ct, DX, DA);
     }
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.x[l] = vadd(b.x[l], DX[l]);
-      b.q[l].w += DQ[l].w; b.q[l].x += DQ[l].x; b.q[l].y += DQ[l].y; b.q[l].z += DQ[l].z;
+      qadd_half(b.q[l], qmul_vq(DA[l], b.q[l]), 1.0f);
     }
   }
   // 4. velocity projection
