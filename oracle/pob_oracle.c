@@ -83,6 +83,26 @@ static inline v3 qrot(v3 v, q4 q) {
   return V(fmaf(t2, u.x, fmaf(c, v.x, s2 * cr.x)), fmaf(t2, u.y, fmaf(c, v.y, s2 * cr.y)),
            fmaf(t2, u.z, fmaf(c, v.z, s2 * cr.z)));
 }
+/* rotation matrix of q from the same formula (R v = (s^2 - u.u) v + 2 (u.v) u + 2 s u x v):
+ * the joint projection rotates three vectors per body through it */
+typedef struct { float m00, m01, m02, m10, m11, m12, m20, m21, m22; } m3;
+static inline m3 qmat(q4 q) {
+  FL(5 + 2 + 4 + 3 + 18);
+  const float c = fmaf(q.w, q.w, -fmaf(q.z, q.z, fmaf(q.y, q.y, q.x * q.x)));
+  const float x2 = 2.0f * q.x, y2 = 2.0f * q.y, z2 = 2.0f * q.z, s2 = 2.0f * q.w;
+  const float sx = s2 * q.x, sy = s2 * q.y, sz = s2 * q.z;
+  m3 r;
+  r.m00 = fmaf(x2, q.x, c); r.m11 = fmaf(y2, q.y, c); r.m22 = fmaf(z2, q.z, c);
+  r.m01 = fmaf(x2, q.y, -sz); r.m10 = fmaf(x2, q.y, sz);
+  r.m02 = fmaf(x2, q.z, sy); r.m20 = fmaf(x2, q.z, -sy);
+  r.m12 = fmaf(y2, q.z, -sx); r.m21 = fmaf(y2, q.z, sx);
+  return r;
+}
+static inline v3 mrot(const m3 *R, v3 v) {
+  FL(15);
+  return V(fmaf(R->m02, v.z, fmaf(R->m01, v.y, R->m00 * v.x)), fmaf(R->m12, v.z, fmaf(R->m11, v.y, R->m10 * v.x)),
+           fmaf(R->m22, v.z, fmaf(R->m21, v.y, R->m20 * v.x)));
+}
 /* brax.math.quat_mul */
 static inline q4 qmul(q4 u, q4 v) {
   FL(28);
@@ -654,8 +674,12 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
   for (int j = 0; j < NJ; ++j) {
     int p = jparent(j), c = jchild(j);
     float imp = e->inv_mass[p], imc = e->inv_mass[c];
+    /* the joint's vectors in world frame through the bodies' rotation matrices */
+    const m3 Rp = qmat(b->q[p]), Rc = qmat(b->q[c]);
+    v3 rp = mrot(&Rp, e->off_p[j]), rc = mrot(&Rc, e->off_c[j]);
+    v3 ap = mrot(&Rp, e->axis[j]), ac = mrot(&Rc, e->axis[j]);
+    v3 fp = mrot(&Rp, e->ref[j]), fc = mrot(&Rc, e->ref[j]);
     /* point-to-point */
-    v3 rp = qrot(e->off_p[j], b->q[p]), rc = qrot(e->off_c[j], b->q[c]);
     v3 d = vsub(vadd(b->x[c], rc), vadd(b->x[p], rp));
     float L = sqrtf(vdot(d, d));
     FL(1);
@@ -673,10 +697,8 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
     DX[c] = vfma(P, -imc, DX[c]);
     v3 xp = vcross(rp, P), xc = vcross(rc, P);
     /* hinge axis alignment (unit inverse inertia: w_p = w_c = 1) */
-    v3 ap = qrot(e->axis[j], b->q[p]), ac = qrot(e->axis[j], b->q[c]);
     v3 Pa = vscl(vcross(ap, ac), e->half_s_ang);
     /* angle limits (brax math.signed_angle about the parent's hinge axis) */
-    v3 fp = qrot(e->ref[j], b->q[p]), fc = qrot(e->ref[j], b->q[c]);
     float psi = orc_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
     float dl = 0.0f;
     if (psi < e->lim_lo[j]) { FL(1); dl = psi - e->lim_lo[j]; }

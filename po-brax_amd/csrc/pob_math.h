@@ -81,6 +81,24 @@ POB_D v3 qrot(v3 v, q4 q) {
   return V(FMA(t2, u.x, FMA(c, v.x, s2 * cr.x)), FMA(t2, u.y, FMA(c, v.y, s2 * cr.y)),
            FMA(t2, u.z, FMA(c, v.z, s2 * cr.z)));
 }
+// rotation matrix of q from brax.math.rotate's formula, R v = (s^2 - u.u) v + 2 (u.v) u
+// + 2 s (u x v): several vectors rotated by one quaternion cost 9 operations each
+struct m3 { float m00, m01, m02, m10, m11, m12, m20, m21, m22; };
+POB_D m3 qmat(q4 q) {
+  const float c = FMA(q.w, q.w, -FMA(q.z, q.z, FMA(q.y, q.y, q.x * q.x)));
+  const float x2 = 2.0f * q.x, y2 = 2.0f * q.y, z2 = 2.0f * q.z, s2 = 2.0f * q.w;
+  const float sx = s2 * q.x, sy = s2 * q.y, sz = s2 * q.z;
+  m3 r;
+  r.m00 = FMA(x2, q.x, c); r.m11 = FMA(y2, q.y, c); r.m22 = FMA(z2, q.z, c);
+  r.m01 = FMA(x2, q.y, -sz); r.m10 = FMA(x2, q.y, sz);
+  r.m02 = FMA(x2, q.z, sy); r.m20 = FMA(x2, q.z, -sy);
+  r.m12 = FMA(y2, q.z, -sx); r.m21 = FMA(y2, q.z, sx);
+  return r;
+}
+POB_D v3 mrot(const m3 &R, v3 v) {
+  return V(FMA(R.m02, v.z, FMA(R.m01, v.y, R.m00 * v.x)), FMA(R.m12, v.z, FMA(R.m11, v.y, R.m10 * v.x)),
+           FMA(R.m22, v.z, FMA(R.m21, v.y, R.m20 * v.x)));
+}
 // brax.math.quat_mul
 POB_D q4 qmul(q4 u, q4 v) {
   q4 r;

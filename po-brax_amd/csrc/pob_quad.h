@@ -320,8 +320,30 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   const float imp = q_inv_mass(S, LT, p);
   const float imc = q_inv_mass(S, LT, c);
   const bool torso_parent = p == 0;
-  v3 rp = qrot(QJV(LT, jl, QJ_OFFP), b.q[p]);
-  v3 rc = qrot(QJV(LT, jl, QJ_OFFC), b.q[c]);
+  // the six joint vectors through the two bodies' rotation matrices (oracle joints_position)
+  v3 ap, ac, rp, rc;
+  float psi;
+  {
+    const m3 Rp = qmat(b.q[p]), Rc = qmat(b.q[c]);
+    const v3 axis = QJV(LT, jl, QJ_AXIS), ref = QJV(LT, jl, QJ_REF);
+    ap = mrot(Rp, axis);
+    const v3 fp = mrot(Rp, ref), fc = mrot(Rc, ref);
+    psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    ac = mrot(Rc, axis);
+    rp = mrot(Rp, QJV(LT, jl, QJ_OFFP));
+    rc = mrot(Rc, QJV(LT, jl, QJ_OFFC));
+  }
+  // hinge axis alignment and angle limits
+  const float lo = QJS(LT, jl, QJ_LO), hi = QJS(LT, jl, QJ_HI);
+  float dl = 0.0f;
+  if (psi < lo) dl = psi - lo;
+  else if (psi > hi) dl = psi - hi;
+  const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+  const v3 Pl = vscl(ap, dl * S.half_s_ang);
+  const v3 s = vadd(Pa, Pl);
+  POB_FENCE();
+  // point-to-point
+  csys_t &S2 = *launder(Sp);
   v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
   float L = pob_sqrt(vdot(d, d));
   // P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway
@@ -330,33 +352,16 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
     v3 n = vdivs(d, L);
     v3 cp = vcross(rp, n), cc = vcross(rc, n);
     float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
-    float lam = (L / wsum) * S.s_pos;
+    float lam = (L / wsum) * S2.s_pos;
     P = vscl(n, lam);
   }
   if (torso_parent) tt->P = P;
   else DX[p] = vfma(P, imp, DX[p]);
   DX[c] = vfma(P, -imc, DX[c]);
-  const v3 xp = vcross(rp, P), xc = vcross(rc, P);
-  POB_FENCE();
-  csys_t &S2 = *launder(Sp);
-  const v3 axis = QJV(LT, jl, QJ_AXIS);
-  v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
-  v3 Pa = vscl(vcross(ap, ac), S2.half_s_ang);
-  POB_FENCE();
-  csys_t &S3 = *launder(Sp);
-  const v3 ref = QJV(LT, jl, QJ_REF);
-  v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
-  float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-  const float lo = QJS(LT, jl, QJ_LO), hi = QJS(LT, jl, QJ_HI);
-  float dl = 0.0f;
-  if (psi < lo) dl = psi - lo;
-  else if (psi > hi) dl = psi - hi;
-  v3 Pl = vscl(ap, dl * S3.half_s_ang);
-  const v3 s = vadd(Pa, Pl);
-  const v3 tp = vadd(xp, s);
+  const v3 tp = vadd(vcross(rp, P), s);
   if (torso_parent) tt->t = tp;
   else DA[p] = vadd(DA[p], tp);
-  DA[c] = vsub(DA[c], vadd(xc, s));
+  DA[c] = vsub(DA[c], vadd(vcross(rc, P), s));
 }
 
 // add quad lane J's hip terms onto the torso accumulators (global joint 2J)
