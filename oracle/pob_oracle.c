@@ -679,23 +679,23 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
     v3 rp = mrot(&Rp, e->off_p[j]), rc = mrot(&Rc, e->off_c[j]);
     v3 ap = mrot(&Rp, e->axis[j]), ac = mrot(&Rc, e->axis[j]);
     v3 fp = mrot(&Rp, e->ref[j]), fc = mrot(&Rc, e->ref[j]);
-    /* point-to-point */
+    /* point-to-point: the XPBD step along n = d / L with generalized inverse masses
+     * w = im + |r x n|^2 and lambda = s_pos L / (w_p + w_c), written without the square
+     * root: P = n lambda = d k and r x P = (r x d) k with
+     * k = s_pos L^2 / (L^2 (im_p + im_c) + |rp x d|^2 + |rc x d|^2).
+     * P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway. */
     v3 d = vsub(vadd(b->x[c], rc), vadd(b->x[p], rp));
-    float L = sqrtf(vdot(d, d));
-    FL(1);
-    /* P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway */
-    v3 P = V(0.0f, 0.0f, 0.0f);
-    if (L > 0.0f) {
-      FL(5);
-      v3 n = vdivs(d, L);
-      v3 cp = vcross(rp, n), cc = vcross(rc, n);
-      float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
-      float lam = (L / wsum) * e->s_pos;
-      P = vscl(n, lam);
+    const float L2 = vdot(d, d);
+    v3 P = V(0.0f, 0.0f, 0.0f), xp = P, xc = P;
+    if (L2 > 0.0f) {
+      FL(1 + 2 + 1 + 1 + 1);
+      const v3 ep = vcross(rp, d), ec = vcross(rc, d);
+      const float den = fmaf(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
+      const float k = (L2 * e->s_pos) / den;
+      P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
     }
     DX[p] = vfma(P, imp, DX[p]);
     DX[c] = vfma(P, -imc, DX[c]);
-    v3 xp = vcross(rp, P), xc = vcross(rc, P);
     /* hinge axis alignment (unit inverse inertia: w_p = w_c = 1) */
     v3 Pa = vscl(vcross(ap, ac), e->half_s_ang);
     /* angle limits (brax math.signed_angle about the parent's hinge axis) */

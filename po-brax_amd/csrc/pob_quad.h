@@ -344,24 +344,24 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   POB_FENCE();
   // point-to-point
   csys_t &S2 = *launder(Sp);
+  // (oracle joints_position: P = d k, r x P = (r x d) k with k = s_pos L^2 / (L^2 (imp + imc)
+  // + |rp x d|^2 + |rc x d|^2); all zero when the anchors coincide)
   v3 d = vsub(vadd(b.x[c], rc), vadd(b.x[p], rp));
-  float L = pob_sqrt(vdot(d, d));
-  // P = 0 when the anchors coincide; the (zero) corrections are accumulated anyway
-  v3 P = V(0.0f, 0.0f, 0.0f);
-  if (L > 0.0f) {
-    v3 n = vdivs(d, L);
-    v3 cp = vcross(rp, n), cc = vcross(rc, n);
-    float wsum = (imp + vdot(cp, cp)) + (imc + vdot(cc, cc));
-    float lam = (L / wsum) * S2.s_pos;
-    P = vscl(n, lam);
+  const float L2 = vdot(d, d);
+  v3 P = V(0.0f, 0.0f, 0.0f), xp = P, xc = P;
+  if (L2 > 0.0f) {
+    const v3 ep = vcross(rp, d), ec = vcross(rc, d);
+    const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
+    const float k = (L2 * S2.s_pos) / den;
+    P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
   }
   if (torso_parent) tt->P = P;
   else DX[p] = vfma(P, imp, DX[p]);
   DX[c] = vfma(P, -imc, DX[c]);
-  const v3 tp = vadd(vcross(rp, P), s);
+  const v3 tp = vadd(xp, s);
   if (torso_parent) tt->t = tp;
   else DA[p] = vadd(DA[p], tp);
-  DA[c] = vsub(DA[c], vadd(vcross(rc, P), s));
+  DA[c] = vsub(DA[c], vadd(xc, s));
 }
 
 // add quad lane J's hip terms onto the torso accumulators (global joint 2J)
