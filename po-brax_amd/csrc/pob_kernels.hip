@@ -364,10 +364,16 @@ POB_D void stage_load<__half>(const float *X, size_t el0, int n_el, float *stg, 
 template <typename QT, int MAXI>
 struct ChunkLoad {
   float v[MAXI][4];
+  // ROWF = elements per env row (N * c), DYNF = those of the dynamic bodies (9 * c): a chunk
+  // that lies inside one env's frozen rows is not loaded (the task tail reads frozen rows
+  // from memory itself)
+  template <int ROWF, int DYNF>
   POB_D void issue(const float *X, size_t el0, int n_el, int lane) {
 #pragma unroll
     for (int m = 0; m < MAXI; ++m) {
       const int i = 4 * lane + 256 * m;
+      const int o = i % ROWF;
+      if (o >= DYNF && o + 4 <= ROWF) continue;
       if (i + 4 <= n_el) {
         if constexpr (sizeof(QT) == 4) {
           const float4 q = *reinterpret_cast<const float4 *>(X + el0 + i);
@@ -384,10 +390,13 @@ struct ChunkLoad {
       }
     }
   }
+  template <int ROWF, int DYNF>
   POB_D void put(float *stg, int n_el, int lane) const {
 #pragma unroll
     for (int m = 0; m < MAXI; ++m) {
       const int i = 4 * lane + 256 * m;
+      const int o = i % ROWF;
+      if (o >= DYNF && o + 4 <= ROWF) continue;
       if (i + 4 <= n_el) { stg[i] = v[m][0]; stg[i + 1] = v[m][1]; stg[i + 2] = v[m][2]; stg[i + 3] = v[m][3]; }
       else if (i < n_el) {
 #pragma unroll
@@ -403,9 +412,21 @@ struct ChunkLoad {
 template <typename QT, int C>
 POB_D void stage_store_dyn(float *X, size_t el0, int N, int nenv, const float *stg, int lane) {
   constexpr int C9 = POB_NDYN * C;
-  for (int i = lane; i < nenv * C9; i += 64) {
-    const int e = i / C9, j = i - e * C9;
-    Q<QT>::st(X, el0 + (size_t)e * N * C + j, stg[i]);
+  if (sizeof(QT) == 4 && (C == 3 || (reinterpret_cast<uintptr_t>(X) & 15) == 0)) {
+    // f32: one row (12 or 16 B) per lane and store instruction
+    struct alignas(4) f3 { float a, b, c; };
+    for (int r = lane; r < nenv * POB_NDYN; r += 64) {
+      const int e = r / POB_NDYN, g = r - e * POB_NDYN;
+      float *dst = X + el0 + (size_t)e * N * C + g * C;
+      const float *src = stg + r * C;
+      if constexpr (C == 4) *reinterpret_cast<float4 *>(dst) = *reinterpret_cast<const float4 *>(src);
+      else *reinterpret_cast<f3 *>(dst) = f3{src[0], src[1], src[2]};
+    }
+  } else {
+    for (int i = lane; i < nenv * C9; i += 64) {
+      const int e = i / C9, j = i - e * C9;
+      Q<QT>::st(X, el0 + (size_t)e * N * C + j, stg[i]);
+    }
   }
 }
 
@@ -422,6 +443,13 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
                           const float *legtab) {
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x & 63;
+#ifdef POB_EXP_TIMING
+  unsigned long long pob_ts[6];  // timing experiment only
+#define POB_TS(i) pob_ts[i] = __builtin_amdgcn_s_memtime()
+#else
+#define POB_TS(i) ((void)0)
+#endif
+  POB_TS(0);
   float *stg = lds + ((int)threadIdx.x >> 6) * POB_STAGE_FLOATS;  // this wave's region
   const Lds Ls{stg, 64, lane};
   const int b = gt >> 2;
@@ -444,17 +472,20 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   QBody bd;
   constexpr int NMAX = KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : (KIND == POB_ANT ? 10 : POB_MAXB));
   constexpr int MAXI = (16 * NMAX * 4 + 255) / 256;  // 16-B chunks per lane of one array
-  if ((flags & POB_F_STAGED) && NMAX <= 16 && 16 * N * 7 <= POB_STAGE_FLOATS) {
+  if ((flags & POB_F_STAGED) && NMAX <= 16 && N == NMAX && 16 * N * 7 <= POB_STAGE_FLOATS) {
     // pairs (pos, rot), (vel, ang): both arrays' loads in flight before either is consumed
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       const int c0 = 3, c1 = pr == 0 ? 4 : 3;
       const int n0 = nenv * N * c0, n1 = nenv * N * c1;
       ChunkLoad<QT, MAXI> A0, A1;
-      A0.issue(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, lane);
-      A1.issue(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, lane);
-      A0.put(stg, n0, lane);
-      A1.put(stg + n0, n1, lane);
+      // (N == NMAX on this path: HH / TAG / stock ant tables)
+      A0.template issue<NMAX * 3, POB_NDYN * 3>(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, lane);
+      if (pr == 0) A1.template issue<NMAX * 4, POB_NDYN * 4>(in.rot, (size_t)b_first * N * c1, n1, lane);
+      else A1.template issue<NMAX * 3, POB_NDYN * 3>(in.ang, (size_t)b_first * N * c1, n1, lane);
+      A0.template put<NMAX * 3, POB_NDYN * 3>(stg, n0, lane);
+      if (pr == 0) A1.template put<NMAX * 4, POB_NDYN * 4>(stg + n0, n1, lane);
+      else A1.template put<NMAX * 3, POB_NDYN * 3>(stg + n0, n1, lane);
       wave_lds_sync();
       if (act_lane) {
 #pragma unroll
@@ -502,6 +533,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     }
   }
 
+  POB_TS(1);
   // ---- physics (10 substeps in registers + the lane's LDS slots)
   float jang[QNJ], jvel[QNJ];
   v3 cvl[QNB], cal[QNB];
@@ -557,6 +589,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     }
   }
   wave_lds_sync();  // every LDS read of the physics slots is done: the region is staging now
+  POB_TS(2);
 
   // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
   float done = 0.0f;
@@ -608,10 +641,18 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     }
     wave_lds_sync();
     float *dst = out.obs + (size_t)(b_first + p0) * D;
-    for (int i = lane; i < pn * D; i += 64) dst[i] = stg[i];
+    const int n = pn * D;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {  // 16-B stores, then the tail
+      const int n4 = n >> 2;
+      for (int i = lane; i < n4; i += 64) reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(stg)[i];
+      for (int i = 4 * n4 + lane; i < n; i += 64) dst[i] = stg[i];
+    } else {
+      for (int i = lane; i < n; i += 64) dst[i] = stg[i];
+    }
     wave_lds_sync();
   }
 
+  POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
 #pragma unroll
@@ -640,6 +681,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     wave_lds_sync();
   }
 
+  POB_TS(4);
   // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
   if (act_lane && k == 0) {
     if (reset_rows) {  // frozen rows from first_qp
@@ -669,6 +711,13 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     const unsigned long long m = __ballot(act_lane && k == 0 && done != 0.0f);
     if (m != 0ull && lane == 0) atomicOr(out.any_done, 1u);
   }
+#ifdef POB_EXP_TIMING
+  POB_TS(5);
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1))
+    printf("POBTS blk %d load %llu phys %llu obs %llu dyn %llu tail %llu total %llu\n", (int)blockIdx.x,
+           pob_ts[1] - pob_ts[0], pob_ts[2] - pob_ts[1], pob_ts[3] - pob_ts[2], pob_ts[4] - pob_ts[3],
+           pob_ts[5] - pob_ts[4], pob_ts[5] - pob_ts[0]);
+#endif
 }
 
 template <int KIND, typename QT>
