@@ -437,6 +437,10 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
   for (int i = (int)threadIdx.x; i < POB_TAB_FLOATS; i += (int)blockDim.x) legtab[i] = src[i];
   __syncthreads();
 }
+#ifdef POB_EXP_TIMING
+#define POB_TS_WAVES 65536
+__device__ unsigned long long pob_ts_buf[POB_TS_WAVES * 8];  // timing experiment only
+#endif
 template <int KIND, typename QT>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
@@ -552,7 +556,19 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #elif defined(POB_EXP_NO_PHYSICS)
     for (int it = 0; it < 0 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
 #else
-    for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) {
+      // Issue priority falls with progress, so a SIMD's four waves (one per block) advance
+      // together: with the default oldest-first arbitration the first wave finishes early
+      // and the last one runs its final substeps alone, at one-wave latency (measured per
+      // wave with POB_EXP_TIMING: p0..max of the physics phase 94 K..211 K ticks before,
+      // 133 K..182 K with this; kernel 0.120 -> 0.112 ms at B = 65 536).
+      const int lvl = (it * 4) / (2 * iters);
+      if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+      else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0);
+    }
 #endif
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
@@ -713,10 +729,18 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   }
 #ifdef POB_EXP_TIMING
   POB_TS(5);
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1))
-    printf("POBTS blk %d load %llu phys %llu obs %llu dyn %llu tail %llu total %llu\n", (int)blockIdx.x,
-           pob_ts[1] - pob_ts[0], pob_ts[2] - pob_ts[1], pob_ts[3] - pob_ts[2], pob_ts[4] - pob_ts[3],
-           pob_ts[5] - pob_ts[4], pob_ts[5] - pob_ts[0]);
+  if ((threadIdx.x & 63) == 0) {
+    unsigned hwid, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w < POB_TS_WAVES) {
+      unsigned long long *r = pob_ts_buf + w * 8;
+      r[0] = hwid; r[1] = xcc;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) r[2 + i] = pob_ts[i];
+    }
+  }
 #endif
 }
 
@@ -1321,3 +1345,11 @@ int pob_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, fl
 }
 
 }  // extern "C"
+
+#ifdef POB_EXP_TIMING
+// timing experiment only: per wave [HW_ID, XCC_ID, t0..t5] of the last step launch
+extern "C" __attribute__((visibility("default"))) int pob_debug_timing(unsigned long long *host, int waves) {
+  if (waves > POB_TS_WAVES) waves = POB_TS_WAVES;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pob_ts_buf), sizeof(unsigned long long) * 8 * waves) == hipSuccess ? 0 : -1;
+}
+#endif

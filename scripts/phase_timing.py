@@ -1,0 +1,46 @@
+"""Per-wave phase timings of the step kernel (timing experiment, not a test).
+
+Needs a library built with -DPOB_EXP_TIMING (POB_LIB=...); prints the distribution of the
+per-wave phase durations (s_memtime ticks) of the last of a few HH steps.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "po-brax_amd"))
+from po_brax_amd import _lib, envs, jumpy  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+env = envs.create("ant_heavenhell", batch_size=B, episode_length=1000)
+key = jumpy.random_prngkey(0)
+s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
+act = torch.empty((B, 8), device="cuda")
+for _ in range(5):
+    jumpy.random_actions_(key, B, 0, act)
+    s = env.step_(s, act)
+torch.cuda.synchronize()
+W = (B * 4 + 63) // 64
+buf = np.zeros((W, 8), np.uint64)
+f = _lib.lib.pob_debug_timing
+f.argtypes = [C.c_void_p, C.c_int]
+assert f(buf.ctypes.data, W) == 0
+hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:].astype(np.int64)
+d = np.diff(t, axis=1)
+names = ["load", "phys", "obs", "dyn", "tail"]
+print(f"B={B} waves={W}")
+for i, n in enumerate(names):
+    print(f"{n:5s} ticks p0 {np.percentile(d[:, i], 0):9.0f} p50 {np.percentile(d[:, i], 50):9.0f} "
+          f"p90 {np.percentile(d[:, i], 90):9.0f} max {d[:, i].max():9.0f}")
+tot = t[:, 5] - t[:, 0]
+print(f"total p0 {tot.min()} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
+for x in np.unique(xcc):
+    m = xcc == x
+    st = t[m, 0] - t[m, 0].min()
+    en = t[m, 5] - t[m, 0].min()
+    print(f"xcc {x}: waves {m.sum()} start spread p50 {np.median(st):.0f} max {st.max()} end max {en.max()} "
+          f"phys p50 {np.median(d[m, 1]):.0f}")
+simd = (hw >> 4) & 3
+print("start offset vs duration corr", np.corrcoef((t[:, 0] - t[:, 0].min()), tot)[0, 1])
