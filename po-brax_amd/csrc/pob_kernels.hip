@@ -171,14 +171,20 @@ POB_D float ga_orientation(const q4 rot0) {
   q4 t = qmul(qmul(rot0, ob), qinv(rot0));
   return pob_atan2f(t.y, t.x);
 }
-POB_D void ga_reading_one(csys_t &S, int k, float ox, float oy, float dist, float ori, float *o_rd) {
+// reading of object k: the slot it writes (-1: none) and the value
+POB_D int ga_reading_slot(csys_t &S, int k, float ox, float oy, float dist, float ori, float &inten) {
   float angle = pob_atan2f(ox, oy) - ori;
   bool in_range = dist <= S.ga_sensor_range;
   int bin = (fabsf(angle) <= S.ga_half_span && in_range) ? (int)((angle + S.ga_half_span) / S.ga_bin_res) : -1;
   if (k >= S.ga_n_apples) bin = bin >= 0 ? bin + S.ga_n_apples : -1;
-  float inten = bin >= 0 ? 1.0f - dist / S.ga_sensor_range : 0.0f;
+  inten = bin >= 0 ? 1.0f - dist / S.ga_sensor_range : 0.0f;
   int slot = bin < 0 ? bin + 2 * S.ga_n_bins : bin;
-  if (slot >= 0 && slot < 2 * S.ga_n_bins) o_rd[slot] = inten;
+  return (slot >= 0 && slot < 2 * S.ga_n_bins) ? slot : -1;
+}
+POB_D void ga_reading_one(csys_t &S, int k, float ox, float oy, float dist, float ori, float *o_rd) {
+  float inten;
+  const int slot = ga_reading_slot(S, k, ox, oy, dist, ori, inten);
+  if (slot >= 0) o_rd[slot] = inten;
 }
 
 // stock ant costs (brax envs/ant.py step [ext]): .5 * sum(action^2) and
@@ -200,6 +206,9 @@ struct TaskOut {
   float reward, done, trunc, steps, m0, m1, m2;
   uint32_t rng0, rng1;
   float xb, ctrl, contact;  // stock ant inputs: torso x before the step, costs
+  // AntGather objects already handled by the env's four lanes (ga_quad_objects)
+  bool ga_done_quad, ga_any_a, ga_any_b, ga_all_wait;
+  int ga_na, ga_nb;
 };
 
 // Per-env POMDP logic after the physics (env.step minus System.step) + EpisodeWrapper:
@@ -235,10 +244,13 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
   } else if (KIND == POB_GATHER) {
     // ant_gather.py:125-150 (obs from pre-relocation positions)
     float *rd = o + base;
-    ga_readings_begin(S, rd);
-    const float ori = ga_orientation(q0);
     int na_hit = 0, nb_hit = 0;
     bool any_a = false, any_b = false, all_wait = true;
+    if (t.ga_done_quad) {
+      na_hit = t.ga_na; nb_hit = t.ga_nb; any_a = t.ga_any_a; any_b = t.ga_any_b; all_wait = t.ga_all_wait;
+    } else {
+    ga_readings_begin(S, rd);
+    const float ori = ga_orientation(q0);
     for (int k = 0; k < S.n_obj; ++k) {
       const size_t row = r3 + 3 * (11 + k);
       const float ox = QQ::ld(in.pos, row), oy = QQ::ld(in.pos, row + 1), oz = QQ::ld(in.pos, row + 2);
@@ -250,6 +262,7 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
       QQ::st(opos, row, nx); QQ::st(opos, row + 1, ny); QQ::st(opos, row + 2, nz);
       if (k < S.ga_n_apples) { any_a |= c; na_hit += c; } else { any_b |= c; nb_hit += c; }
       all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
+    }
     }
     reward = dead > 0.0f ? S.ga_dying_cost : 0.0f;
     if (any_a && dead == 0.0f) reward = 1.0f;
@@ -299,6 +312,64 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
   }
   t.reward = reward; t.done = done; t.trunc = trunc; t.steps = steps;
   t.m0 = m0; t.m1 = m1; t.m2 = m2; t.rng0 = rng0; t.rng1 = rng1;
+}
+
+// AntGather objects (ant_gather.py:125-181) on the env's four quad lanes: lane k takes
+// objects k, k + 4, k + 8, k + 12 (n_obj <= 16), so their loads are in flight together and
+// the sensor angles / catches / relocations run in parallel; the sensor scatter keeps the
+// reference's object order (last writer wins): lane 0 writes the readings of objects
+// 0, 1, 2, ... from DPP-gathered (slot, value) pairs.  Counts and flags are reduced over
+// the quad.  All four lanes must be active.
+#define POB_GA_QUAD_MAX 16
+template <typename QT>
+POB_D void ga_quad_objects(csys_t &S, const StatePtrs &in, const size_t r3, const v3 x0, const q4 q0, const int k,
+                           float *opos, float *rd, TaskOut &t) {
+  using QQ = Q<QT>;
+  const float ori = ga_orientation(q0);
+  int slot[4];
+  float val[4];
+  int na = 0, nb = 0;
+  bool any_a = false, any_b = false, all_wait = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int obj = k + 4 * j;
+    slot[j] = -1; val[j] = 0.0f;
+    if (obj < S.n_obj) {
+      const size_t row = r3 + 3 * (11 + obj);
+      const float ox = QQ::ld(in.pos, row), oy = QQ::ld(in.pos, row + 1), oz = QQ::ld(in.pos, row + 2);
+      const float dk = dist2d(x0.x, x0.y, ox, oy);
+      slot[j] = ga_reading_slot(S, obj, ox, oy, dk, ori, val[j]);
+      const bool c = dk <= S.ga_catch_range;
+      float nx = ox, ny = oy, nz = oz;
+      if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
+      QQ::st(opos, row, nx); QQ::st(opos, row + 1, ny); QQ::st(opos, row + 2, nz);
+      if (obj < S.ga_n_apples) { any_a |= c; na += c; } else { any_b |= c; nb += c; }
+      all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
+    }
+  }
+  if (k == 0) ga_readings_begin(S, rd);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s0 = quad_bcast<0>(__int_as_float(slot[j])), v0 = quad_bcast<0>(val[j]);
+    const float s1 = quad_bcast<1>(__int_as_float(slot[j])), v1 = quad_bcast<1>(val[j]);
+    const float s2 = quad_bcast<2>(__int_as_float(slot[j])), v2 = quad_bcast<2>(val[j]);
+    const float s3 = quad_bcast<3>(__int_as_float(slot[j])), v3_ = quad_bcast<3>(val[j]);
+    if (k == 0) {  // objects 4j, 4j + 1, 4j + 2, 4j + 3 in order
+      if (__float_as_int(s0) >= 0) rd[__float_as_int(s0)] = v0;
+      if (__float_as_int(s1) >= 0) rd[__float_as_int(s1)] = v1;
+      if (__float_as_int(s2) >= 0) rd[__float_as_int(s2)] = v2;
+      if (__float_as_int(s3) >= 0) rd[__float_as_int(s3)] = v3_;
+    }
+  }
+  const float fa = (float)na, fb = (float)nb;
+  const float flag = (any_a ? 1.0f : 0.0f) + (any_b ? 2.0f : 0.0f) + (all_wait ? 0.0f : 4.0f);
+  t.ga_na = (int)(((quad_bcast<0>(fa) + quad_bcast<1>(fa)) + quad_bcast<2>(fa)) + quad_bcast<3>(fa));
+  t.ga_nb = (int)(((quad_bcast<0>(fb) + quad_bcast<1>(fb)) + quad_bcast<2>(fb)) + quad_bcast<3>(fb));
+  const int f0 = (int)quad_bcast<0>(flag), f1 = (int)quad_bcast<1>(flag), f2 = (int)quad_bcast<2>(flag),
+            f3 = (int)quad_bcast<3>(flag);
+  const int fo = f0 | f1 | f2 | f3;
+  t.ga_any_a = (fo & 1) != 0; t.ga_any_b = (fo & 2) != 0; t.ga_all_wait = (fo & 4) == 0;
+  t.ga_done_quad = true;
 }
 
 // task tail of a fixed kind, or (POB_MIXED) of the kind recorded in the env's table
@@ -609,6 +680,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 
   // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
   float done = 0.0f;
+  t.ga_done_quad = false;
+  const bool ga_quad = (KIND == POB_GATHER || KIND == POB_MIXED) && kind == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
   const int P = POB_STAGE_FLOATS / D < 16 ? POB_STAGE_FLOATS / D : 16;
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
@@ -639,12 +712,15 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
         if (out.pos != in.pos) {  // functional mode: carry the frozen rows over (the task
           for (int i = POB_NDYN; i < N; ++i) {  // tail then moves GA objects / the TAG target)
-            cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+            if (!(ga_quad && i >= 11)) cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);  // (objects: below)
             cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
             cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
             cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
           }
         }
+      }
+      if (ga_quad) ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, o + 29 + 6 * N, t);
+      if (k == 0) {
         task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
         done = t.done;
       }

@@ -1,7 +1,7 @@
 """Per-wave phase timings of the step kernel (timing experiment, not a test).
 
 Needs a library built with -DPOB_EXP_TIMING (POB_LIB=...); prints the distribution of the
-per-wave phase durations (s_memtime ticks) of the last of a few HH steps.
+per-wave phase durations (s_memtime ticks) of the last of a few steps (argv: B, env name).
 """
 import ctypes as C
 import os
@@ -14,7 +14,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from po_brax_amd import _lib, envs, jumpy  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-env = envs.create("ant_heavenhell", batch_size=B, episode_length=1000)
+NAME = sys.argv[2] if len(sys.argv) > 2 else "ant_heavenhell"
+env = envs.create(NAME, batch_size=B, episode_length=1000)
 key = jumpy.random_prngkey(0)
 s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
 act = torch.empty((B, 8), device="cuda")
@@ -30,7 +31,7 @@ assert f(buf.ctypes.data, W) == 0
 hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:].astype(np.int64)
 d = np.diff(t, axis=1)
 names = ["load", "phys", "obs", "dyn", "tail"]
-print(f"B={B} waves={W}")
+print(f"{NAME} B={B} waves={W}")
 for i, n in enumerate(names):
     print(f"{n:5s} ticks p0 {np.percentile(d[:, i], 0):9.0f} p50 {np.percentile(d[:, i], 50):9.0f} "
           f"p90 {np.percentile(d[:, i], 90):9.0f} max {d[:, i].max():9.0f}")
