@@ -321,44 +321,32 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
 // 0, 1, 2, ... from DPP-gathered (slot, value) pairs.  Counts and flags are reduced over
 // the quad.  All four lanes must be active.
 #define POB_GA_QUAD_MAX 16
+struct GaQuad {
+  int slot[4];   // sensor slot written by this lane's object j (-1: none)
+  float val[4];  // and the value
+};
 template <typename QT>
 POB_D void ga_quad_objects(csys_t &S, const StatePtrs &in, const size_t r3, const v3 x0, const q4 q0, const int k,
-                           float *opos, float *rd, TaskOut &t) {
+                           float *opos, GaQuad &g, TaskOut &t) {
   using QQ = Q<QT>;
   const float ori = ga_orientation(q0);
-  int slot[4];
-  float val[4];
   int na = 0, nb = 0;
   bool any_a = false, any_b = false, all_wait = true;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int obj = k + 4 * j;
-    slot[j] = -1; val[j] = 0.0f;
+    g.slot[j] = -1; g.val[j] = 0.0f;
     if (obj < S.n_obj) {
       const size_t row = r3 + 3 * (11 + obj);
       const float ox = QQ::ld(in.pos, row), oy = QQ::ld(in.pos, row + 1), oz = QQ::ld(in.pos, row + 2);
       const float dk = dist2d(x0.x, x0.y, ox, oy);
-      slot[j] = ga_reading_slot(S, obj, ox, oy, dk, ori, val[j]);
+      g.slot[j] = ga_reading_slot(S, obj, ox, oy, dk, ori, g.val[j]);
       const bool c = dk <= S.ga_catch_range;
       float nx = ox, ny = oy, nz = oz;
       if (c) { nx = S.ga_waiting[0]; ny = S.ga_waiting[1]; nz = S.ga_waiting[2]; }
       QQ::st(opos, row, nx); QQ::st(opos, row + 1, ny); QQ::st(opos, row + 2, nz);
       if (obj < S.ga_n_apples) { any_a |= c; na += c; } else { any_b |= c; nb += c; }
       all_wait &= (nx == S.ga_waiting[0]) & (ny == S.ga_waiting[1]) & (nz == S.ga_waiting[2]);
-    }
-  }
-  if (k == 0) ga_readings_begin(S, rd);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float s0 = quad_bcast<0>(__int_as_float(slot[j])), v0 = quad_bcast<0>(val[j]);
-    const float s1 = quad_bcast<1>(__int_as_float(slot[j])), v1 = quad_bcast<1>(val[j]);
-    const float s2 = quad_bcast<2>(__int_as_float(slot[j])), v2 = quad_bcast<2>(val[j]);
-    const float s3 = quad_bcast<3>(__int_as_float(slot[j])), v3_ = quad_bcast<3>(val[j]);
-    if (k == 0) {  // objects 4j, 4j + 1, 4j + 2, 4j + 3 in order
-      if (__float_as_int(s0) >= 0) rd[__float_as_int(s0)] = v0;
-      if (__float_as_int(s1) >= 0) rd[__float_as_int(s1)] = v1;
-      if (__float_as_int(s2) >= 0) rd[__float_as_int(s2)] = v2;
-      if (__float_as_int(s3) >= 0) rd[__float_as_int(s3)] = v3_;
     }
   }
   const float fa = (float)na, fb = (float)nb;
@@ -370,6 +358,23 @@ POB_D void ga_quad_objects(csys_t &S, const StatePtrs &in, const size_t r3, cons
   const int fo = f0 | f1 | f2 | f3;
   t.ga_any_a = (fo & 1) != 0; t.ga_any_b = (fo & 2) != 0; t.ga_all_wait = (fo & 4) == 0;
   t.ga_done_quad = true;
+}
+// lane 0 writes the readings of objects 0, 1, 2, ... in order (all four lanes active)
+POB_D void ga_quad_scatter(csys_t &S, const GaQuad &g, const int k, float *rd) {
+  if (k == 0) ga_readings_begin(S, rd);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s0 = quad_bcast<0>(__int_as_float(g.slot[j])), v0 = quad_bcast<0>(g.val[j]);
+    const float s1 = quad_bcast<1>(__int_as_float(g.slot[j])), v1 = quad_bcast<1>(g.val[j]);
+    const float s2 = quad_bcast<2>(__int_as_float(g.slot[j])), v2 = quad_bcast<2>(g.val[j]);
+    const float s3 = quad_bcast<3>(__int_as_float(g.slot[j])), v3_ = quad_bcast<3>(g.val[j]);
+    if (k == 0) {  // objects 4j, 4j + 1, 4j + 2, 4j + 3
+      if (__float_as_int(s0) >= 0) rd[__float_as_int(s0)] = v0;
+      if (__float_as_int(s1) >= 0) rd[__float_as_int(s1)] = v1;
+      if (__float_as_int(s2) >= 0) rd[__float_as_int(s2)] = v2;
+      if (__float_as_int(s3) >= 0) rd[__float_as_int(s3)] = v3_;
+    }
+  }
 }
 
 // task tail of a fixed kind, or (POB_MIXED) of the kind recorded in the env's table
@@ -682,6 +687,12 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   float done = 0.0f;
   t.ga_done_quad = false;
   const bool ga_quad = (KIND == POB_GATHER || KIND == POB_MIXED) && kind == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
+  GaQuad gq;
+  if (ga_quad && act_lane) {
+    // functional mode: the object rows of out.pos are written here (the frozen-row copy
+    // below skips them)
+    ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
+  }
   const int P = POB_STAGE_FLOATS / D < 16 ? POB_STAGE_FLOATS / D : 16;
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
@@ -692,7 +703,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         o[sh + 7 + 2 * k + jl] = jang[jl];
         o[sh + 21 + 2 * k + jl] = jvel[jl];
       }
-      // cfrc rows: lane k rows 2k+1, 2k+2 (lane 0 also the torso row); lane 3 the zero rows
+      // cfrc rows: lane k rows 2k+1, 2k+2 (lane 0 also the torso row); the frozen bodies' zero
+      // rows split over the four lanes
       float *oc = o + (29 + sh);
 #pragma unroll
       for (int l = 0; l < QNB; ++l) {
@@ -701,9 +713,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         oc[3 * g] = clip1(cvl[l].x); oc[1 + 3 * g] = clip1(cvl[l].y); oc[2 + 3 * g] = clip1(cvl[l].z);
         oc[3 * N + 3 * g] = clip1(cal[l].x); oc[1 + 3 * N + 3 * g] = clip1(cal[l].y); oc[2 + 3 * N + 3 * g] = clip1(cal[l].z);
       }
-      if (k == 3) {
-        for (int q = 3 * POB_NDYN; q < 3 * N; ++q) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
-      }
+      for (int q = 3 * POB_NDYN + k; q < 3 * N; q += 4) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
       if (k == 0) {
         if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
         o[sh + 2] = bd.x[0].z;
@@ -719,7 +729,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
           }
         }
       }
-      if (ga_quad) ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, o + 29 + 6 * N, t);
+      if (ga_quad) ga_quad_scatter(S, gq, k, o + 29 + 6 * N);
       if (k == 0) {
         task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
         done = t.done;
