@@ -1,0 +1,186 @@
+"""Physics laws of the restated PBD step -- size-independent properties.
+
+brax's PBD step is not in the container, so the physics itself is parity-unpinned against
+brax.  These tests pin what the restatement must satisfy whatever brax's
+exact op order is:
+
+* linear momentum: joint projections, hinge/limit corrections and torque actuators are
+  internal (equal and opposite), so in free fall the ant's centre of mass follows the
+  substep integrator's ballistic path (x_k = x_0 - g h^2 k(k+1)/2) and keeps zero
+  horizontal velocity, under ANY actions;
+* angular momentum about the centre of mass is conserved up to PBD's first-order
+  rotation update (|sum L| / sum |L| small);
+* equivariance: a whole-ant rotation by 90 deg about z commutes with the step (gravity and
+  the ground plane are z-invariant, the actuators act about body-fixed axes);
+* a resting ant settles (joint gaps, ground penetration and speeds stay small) and a
+  random-action rollout stays bounded.
+
+The oracle runs on the CPU (not gpu); the GPU test checks the momentum laws on the HIP
+kernel at the headline batch (65 536 envs), where the oracle would be too slow.
+"""
+import numpy as np
+import pytest
+
+import orc
+import pob_np as P
+
+G, DT, SUB = 9.8, 0.05, 10
+H = DT / SUB
+MASS = np.array([b[1] for b in P.ANT_BODIES])
+
+
+def _rot(v, q):
+    s, u = q[..., :1], q[..., 1:]
+    return (2 * np.sum(u * v, -1, keepdims=True) * u + (s * s - np.sum(u * u, -1, keepdims=True)) * v
+            + 2 * s * np.cross(u, v))
+
+
+def _com(pos, vel):
+    m = MASS[None, :, None]
+    return (pos[:, :9] * m).sum(1) / MASS.sum(), (vel[:, :9] * m).sum(1) / MASS.sum()
+
+
+def _ang_momentum(pos, vel, ang):
+    """(sum L, sum |L|) about the centre of mass; unit inertia (brax ant config)."""
+    c, vc = _com(pos, vel)
+    orb = MASS[None, :, None] * np.cross(pos[:, :9] - c[:, None], vel[:, :9] - vc[:, None])
+    return orb.sum(1) + ang[:, :9].sum(1), np.abs(orb).sum(1) + np.abs(ang[:, :9]).sum(1)
+
+
+def _joint_gaps(pos, rot):
+    x, q = pos.astype(np.float64), rot.astype(np.float64)
+    g = [np.linalg.norm(x[:, p] + _rot(P.f32(op), q[:, p]) - x[:, c] - _rot(P.f32(oc), q[:, c]), axis=-1)
+         for p, c, op, oc, _, _ in P.ANT_JOINTS]
+    return np.stack(g, 1)
+
+
+def _lowest_point(pos, rot):
+    out = np.full(pos.shape[0], np.inf)
+    for i in range(9):
+        ends, r = P.capsule_ends(i)
+        for e in ends:
+            out = np.minimum(out, (pos[:, i] + _rot(e, rot[:, i].astype(np.float64)))[:, 2] - r)
+    return out
+
+
+def _lifted(name, B, dz, seed=0):
+    e = orc.OracleEnv(name)
+    s = e.reset(P.split(P.prngkey(seed), B + 1)[1:])
+    s["pos"][:, :9, 2] += dz
+    s["vel"][:] = 0
+    s["ang"][:] = 0
+    return e, s
+
+
+@pytest.mark.parametrize("name", ["ant", "ant_tag", "ant_heavenhell"])
+@pytest.mark.parametrize("amp", [0.0, 1.0])
+def test_free_fall_linear_momentum(name, amp):
+    B, T = 32, 3
+    e, s = _lifted(name, B, 2.0)
+    c0, _ = _com(s["pos"], s["vel"])
+    rng = np.random.default_rng(1)
+    for _ in range(T):
+        s = e.step(s, (amp * rng.uniform(-1, 1, (B, 8))).astype(np.float32), flags=0)
+    c, v = _com(s["pos"], s["vel"])
+    n = T * SUB
+    # v = (x - x_prev) / h in float32: one position ulp at the ant's |x| is ulp / h of speed
+    ulp_v = 2 * np.spacing(np.abs(s["pos"][:, :9]).max((1, 2))).astype(np.float64) / H
+    assert (np.abs(v[:, :2]).max(1) < ulp_v).all()  # no horizontal drift: internal forces cancel
+    np.testing.assert_allclose(v[:, 2], -G * H * n, rtol=1e-3)
+    np.testing.assert_allclose(c[:, 2] - c0[:, 2], -G * H * H * n * (n + 1) / 2, rtol=1e-3)
+    # the centre of mass stays put in xy up to a few position roundings per substep
+    assert (np.abs(c[:, :2] - c0[:, :2]).max(1) < 4 * n * ulp_v * H / 2).all()
+
+
+@pytest.mark.parametrize("amp", [0.1, 1.0])
+def test_free_fall_angular_momentum(amp):
+    B = 32
+    e, s = _lifted("ant", B, 2.0)
+    rng = np.random.default_rng(2)
+    for _ in range(3):
+        s = e.step(s, (amp * rng.uniform(-1, 1, (B, 8))).astype(np.float32), flags=0)
+    L, scale = _ang_momentum(s["pos"], s["vel"], s["ang"])
+    assert scale.min() > 0.1 * amp  # the actions did spin the legs
+    assert (np.linalg.norm(L, axis=1) / np.linalg.norm(scale, axis=1)).max() < 0.03
+
+
+def test_rotation_about_z_commutes_with_step():
+    """Rotating the whole ant (poses, velocities, angular velocities) by 90 deg about z
+    before 4 steps equals rotating after them, up to float32 rounding (measured ~1e-5 m;
+    contact branches make it chaotic over longer horizons)."""
+    B, T = 16, 4
+    e = orc.OracleEnv("ant")
+    s = e.reset(P.split(P.prngkey(3), B + 1)[1:])
+    r = {k: v.copy() for k, v in s.items()}
+    for k in ("pos", "vel", "ang"):  # (x, y) -> (-y, x)
+        r[k][..., 0], r[k][..., 1] = -s[k][..., 1], s[k][..., 0]
+    qz = np.array([np.cos(np.pi / 4), 0, 0, np.sin(np.pi / 4)])
+    r["rot"] = np.ascontiguousarray(np.stack([_qmul(qz, q) for q in s["rot"].reshape(-1, 4).astype(np.float64)])
+                                    .reshape(s["rot"].shape).astype(np.float32))
+    rng = np.random.default_rng(4)
+    for _ in range(T):
+        a = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        s = e.step(s, a, flags=0)
+        r = e.step(r, a, flags=0)
+    np.testing.assert_allclose(r["pos"][:, :9, 0], -s["pos"][:, :9, 1], atol=5e-5)
+    np.testing.assert_allclose(r["pos"][:, :9, 1], s["pos"][:, :9, 0], atol=5e-5)
+    np.testing.assert_allclose(r["pos"][:, :9, 2], s["pos"][:, :9, 2], atol=5e-5)
+    # joint angles and joint velocities (stock ant obs 5:13, 19:27) are rotation invariant
+    np.testing.assert_allclose(r["obs"][:, 5:13], s["obs"][:, 5:13], atol=2e-4)
+    np.testing.assert_allclose(r["obs"][:, 19:27], s["obs"][:, 19:27], rtol=1e-3, atol=1e-2)
+
+
+def _qmul(u, v):
+    w1, x1, y1, z1 = u
+    w2, x2, y2, z2 = v
+    return np.array([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                     w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2])
+
+
+@pytest.mark.parametrize("name", ["ant", "ant_heavenhell"])
+def test_resting_ant_settles_and_rollout_stays_bounded(name):
+    B = 64
+    e = orc.OracleEnv(name)
+    s = e.reset(P.split(P.prngkey(1), B + 1)[1:])
+    assert _joint_gaps(s["pos"], s["rot"]).max() < 1e-6  # reset = forward kinematics
+    assert abs(_lowest_point(s["pos"], s["rot"]).min()) < 1e-6  # min-z lift: touching the ground
+    for _ in range(60):
+        s = e.step(s, np.zeros((B, 8), np.float32), flags=0)
+    assert _joint_gaps(s["pos"], s["rot"]).max() < 1e-2
+    assert _lowest_point(s["pos"], s["rot"]).min() > -2e-3
+    assert np.abs(s["vel"][:, :9]).max() < 0.5 and np.abs(s["ang"][:, :9]).max() < 0.5
+    rng = np.random.default_rng(5)
+    for _ in range(60):
+        s = e.step(s, rng.uniform(-1, 1, (B, 8)).astype(np.float32), flags=0)
+    assert np.isfinite(s["pos"]).all() and np.isfinite(s["obs"]).all()
+    assert _joint_gaps(s["pos"], s["rot"]).max() < 0.15
+    assert np.abs(s["vel"][:, :9]).max() < 20
+
+
+@pytest.mark.gpu
+def test_gpu_free_fall_momentum_full_batch():
+    """The HIP step at the headline batch: the centre of mass of every one of 65 536 lifted
+    ants falls ballistically with no horizontal drift under random actions."""
+    import torch
+    from po_brax_amd import envs, jumpy
+    B, T = 65536, 3
+    env = envs.create("ant_heavenhell", batch_size=B, episode_length=1000)
+    key = jumpy.random_prngkey(0)
+    s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
+    s.qp.pos[:, :9, 2] += 3.0  # clear of the ground and of every wall top
+    s.qp.vel.zero_()
+    s.qp.ang.zero_()
+    pos0 = s.qp.pos.double().cpu().numpy()
+    c0, _ = _com(pos0, np.zeros_like(pos0))
+    act = torch.empty((B, 8), device="cuda")
+    for _ in range(T):
+        jumpy.random_actions_(key, B, 0, act)
+        s = env.step(s, act)
+    torch.cuda.synchronize()
+    pos, vel = s.qp.pos.double().cpu().numpy(), s.qp.vel.double().cpu().numpy()
+    c, v = _com(pos, vel)
+    n = T * SUB
+    ulp_v = 2 * np.spacing(np.abs(pos[:, :9]).max((1, 2)).astype(np.float32)).astype(np.float64) / H
+    assert (np.abs(v[:, :2]).max(1) < ulp_v).all()
+    np.testing.assert_allclose(v[:, 2], -G * H * n, rtol=1e-3)
+    np.testing.assert_allclose(c[:, 2] - c0[:, 2], -G * H * H * n * (n + 1) / 2, rtol=1e-3)
