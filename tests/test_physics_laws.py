@@ -164,7 +164,8 @@ def test_gpu_free_fall_momentum_full_batch():
     import torch
     from po_brax_amd import envs, jumpy
     B, T = 65536, 3
-    env = envs.create("ant_heavenhell", batch_size=B, episode_length=1000)
+    # no AutoResetWrapper: a lifted torso (z > 1) is "dead" and would be reset to first_qp
+    env = envs.create("ant_heavenhell", batch_size=B, episode_length=1000, auto_reset=False)
     key = jumpy.random_prngkey(0)
     s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
     s.qp.pos[:, :9, 2] += 3.0  # clear of the ground and of every wall top
