@@ -64,6 +64,11 @@ POB_D float pob_sqrt(float x) {
   return r;
 }
 
+#ifdef POB_EXP_RCPDIV
+#define POB_DIV(a, b) ((a) * pob_rcp(b))  // timing experiment only (not the oracle's spec)
+#else
+#define POB_DIV(a, b) ((a) / (b))
+#endif
 POB_D v3 vdivs(v3 a, float s) { float inv = pob_rcp(s); return V(a.x * inv, a.y * inv, a.z * inv); }
 POB_D float vdot(v3 a, v3 b) { return FMA(a.z, b.z, FMA(a.y, b.y, a.x * b.x)); }
 POB_D v3 vcross(v3 a, v3 b) {
@@ -148,7 +153,7 @@ POB_D float pob_atanf(float x) {
   float sign = 1.0f, y = 0.0f;
   if (x < 0.0f) { sign = -1.0f; x = -x; }
   if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -pob_rcp(x); }
-  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = (x - 1.0f) / (x + 1.0f); }
+  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = POB_DIV(x - 1.0f, x + 1.0f); }
   float z = x * x;
   y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -
             3.33329491539e-1f) * z * x + x);
@@ -163,7 +168,7 @@ POB_D float pob_atan2f(float y, float x) {
   if (y == 0.0f) return x < 0.0f ? 3.141592653589793f : 0.0f;
   float w = 0.0f;
   if (x < 0.0f) w = (y < 0.0f) ? -3.141592653589793f : 3.141592653589793f;
-  return w + pob_atanf(y / x);
+  return w + pob_atanf(POB_DIV(y, x));
 }
 // Cephes-form sinf/cosf (Cody-Waite reduction by pi/4)
 POB_D void pob_sincosf(float x, float *s, float *c) {

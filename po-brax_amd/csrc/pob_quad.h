@@ -241,7 +241,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 rr = vsub(cp, b.x[l]);
       v3 cn = vcross(rr, n);
       float w = im + vdot(cn, cn);
-      float lam = pen / w;
+      float lam = POB_DIV(pen, w);
       v3 P = vscl(n, lam);
       DX[l] = vfma(P, im, DX[l]);
       DA[l] = vadd(DA[l], vcross(rr, P));
@@ -253,7 +253,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
         v3 t = vdivs(dpt, lt);
         v3 ctn = vcross(rr, t);
         float wt = im + vdot(ctn, ctn);
-        float lamt = lt / wt;
+        float lamt = POB_DIV(lt, wt);
         if (lamt < S.friction * lam) {
           v3 Pt = vscl(t, -lamt);
           DX[l] = vfma(Pt, im, DX[l]);
@@ -287,7 +287,7 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
-        dv = vscl(vt, -(fr / lt));
+        dv = vscl(vt, -POB_DIV(fr, lt));
       }
       if (vn < 0.0f) dv = vfma(n, -vn, dv);
       float D = pob_sqrt(vdot(dv, dv));
@@ -341,7 +341,9 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
   const v3 Pl = vscl(ap, dl * S.half_s_ang);
   const v3 s = vadd(Pa, Pl);
+#ifndef POB_EXP_JOINT_ILP
   POB_FENCE();
+#endif
   // point-to-point
   csys_t &S2 = *launder(Sp);
   // (oracle joints_position: P = d k, r x P = (r x d) k with k = s_pos L^2 / (L^2 (imp + imc)
@@ -352,7 +354,7 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   if (L2 > 0.0f) {
     const v3 ep = vcross(rp, d), ec = vcross(rc, d);
     const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
-    const float k = (L2 * S2.s_pos) / den;
+    const float k = POB_DIV(L2 * S2.s_pos, den);
     P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
   }
   if (torso_parent) tt->P = P;
@@ -429,7 +431,9 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     tq.t = tq.P;
 #else
     qjoint_position(Sp, LT, b, 0, DX, DA, &tq);
+#ifndef POB_EXP_JOINT_ILP
     POB_FENCE();
+#endif
     qjoint_position(Sp, LT, b, 1, DX, DA, nullptr);
 #endif
     POB_FENCE();
