@@ -140,10 +140,16 @@ static inline v3 qrot_add(v3 v, q4 q, v3 x) {
   return V(fmaf(t2, u.x, fmaf(c, v.x, fmaf(s2, cr.x, x.x))), fmaf(t2, u.y, fmaf(c, v.y, fmaf(s2, cr.y, x.y))),
            fmaf(t2, u.z, fmaf(c, v.z, fmaf(s2, cr.z, x.z))));
 }
+/* Substep quaternion normalisation: with e = |q|^2 - 1 (exact, Sterbenz),
+ * 1/|q| = 1 - e/2 + 3e^2/8 - 5e^3/16 + O(e^4) (truncation <= 35/128 e^4 < 2^-27 for
+ * |e| <= 2^-6; rollouts stay below 2.4e-3); 1 / sqrt(|q|^2) outside that range.
+ * Same rule in the HIP kernels (pob_math.h qnormalize). */
 static inline q4 qnormalize(q4 q) {
-  FL(13);
-  float n = sqrtf(fmaf(q.z, q.z, fmaf(q.y, q.y, fmaf(q.x, q.x, q.w * q.w))));
-  float inv = 1.0f / n;
+  FL(15);
+  float n2 = fmaf(q.z, q.z, fmaf(q.y, q.y, fmaf(q.x, q.x, q.w * q.w)));
+  float e = n2 - 1.0f;
+  float inv = fmaf(fmaf(fmaf(-0.3125f, e, 0.375f), e, -0.5f), e, 1.0f);
+  if (!(fabsf(e) <= 0x1p-6f)) inv = 1.0f / sqrtf(n2);
   q4 r = {q.w * inv, q.x * inv, q.y * inv, q.z * inv};
   return r;
 }

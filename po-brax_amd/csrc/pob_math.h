@@ -135,9 +135,20 @@ POB_D v3 qrot_add(v3 v, q4 q, v3 x) {
   return V(FMA(t2, u.x, FMA(c, v.x, FMA(s2, cr.x, x.x))), FMA(t2, u.y, FMA(c, v.y, FMA(s2, cr.y, x.y))),
            FMA(t2, u.z, FMA(c, v.z, FMA(s2, cr.z, x.z))));
 }
+// Substep quaternion normalisation (spec, oracle qnormalize): with e = |q|^2 - 1 (exact by
+// Sterbenz), 1/|q| = 1 - e/2 + 3e^2/8 - 5e^3/16 + O(e^4), truncation error <= 35/128 e^4
+// < 2^-27 for |e| <= 2^-6; |e| stays below 2.4e-3 in rollouts (the integration and
+// correction steps move a unit q by far less), so the three-FMA polynomial replaces the
+// correctly rounded sqrt + reciprocal; outside that range (never in practice) the element
+// takes 1 / sqrt(|q|^2) as before, behind a wave-uniform guard.
 POB_D q4 qnormalize(q4 q) {
-  float n = pob_sqrt(FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w))));
-  float inv = pob_rcp(n);
+  const float n2 = FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w)));
+  const float e = n2 - 1.0f;
+  float inv = FMA(FMA(FMA(-0.3125f, e, 0.375f), e, -0.5f), e, 1.0f);
+  const bool far = !(fabsf(e) <= 0x1p-6f);
+  if (__builtin_expect(__any(far), 0)) {
+    if (far) inv = pob_rcp(pob_sqrt(n2));
+  }
   q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
   return r;
 }
