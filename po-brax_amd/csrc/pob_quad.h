@@ -86,6 +86,7 @@ struct QContacts {
   float pen[2 + QNB];
   v3 n[QNB];
   bool sel[QNB];
+  v3 pe[2 + QNB];  // the contact's sphere centre in world (x + rotate(e, q)), reused by the position pass
 };
 POB_D constexpr int qcontact_body(int c) { return c == 0 ? 0 : (c == 1 ? 2 : c - 2); }
 
@@ -110,7 +111,7 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 // compare run only when d2 < T = r^2 (1 + 2^-20) (or d2 is NaN).  Exact: d2 >= T gives
 // sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
 POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
-                     bool &bsel) {
+                     bool &bsel, v3 &bpe) {
   const float2 r01 = *reinterpret_cast<const float2 *>(R);
   const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
   const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
@@ -138,6 +139,7 @@ POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on,
       best = pen;
       bn = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
       bsel = q1;
+      bpe = p;
     }
   }
 }
@@ -157,6 +159,7 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
     const int l = qcontact_body(c);
     v3 pe = qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
     ct.pen[c] = qground_r(S, LT, c) - pe.z;
+    ct.pe[c] = pe;
   }
   uint32_t lane_mask = 0u;
   if (WALLS) {
@@ -188,6 +191,7 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
+    v3 bpe = bn;
     if (any_near) {
       v3 pe[2];
 #pragma unroll
@@ -200,12 +204,13 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
         const int w = on ? __builtin_ctz(m) : 0;
         m &= m - 1u;
 #pragma unroll
-        for (int q = 0; q < nend; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel);
+        for (int q = 0; q < nend; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
       }
     }
     ct.pen[2 + l] = best;
     ct.n[l] = bn;
     ct.sel[l] = bsel;
+    ct.pe[2 + l] = bpe;
   }
 }
 
@@ -236,7 +241,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       float rad;
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
-      v3 pe = qrot_add(e, b.q[l], b.x[l]);
+      const v3 pe = ct.pe[c];  // = qrot_add(e, b.q[l], b.x[l]) of the detection (same q, x)
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 cn = vcross(rr, n);
