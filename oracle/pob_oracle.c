@@ -154,29 +154,28 @@ static inline q4 qnormalize(q4 q) {
   return r;
 }
 
-/* Cephes-form atanf/atan2f (fixed polynomial; same form in the HIP kernels). */
-static float orc_atanf(float x) {
-  FL(11);
-  float sign = 1.0f, y = 0.0f;
-  if (x < 0.0f) { sign = -1.0f; x = -x; }
-  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -(1.0f / x); }
-  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = (x - 1.0f) / (x + 1.0f); }
-  float z = x * x;
-  y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -
-            3.33329491539e-1f) * z * x + x);
-  return sign * y;
-}
+/* atan2f: branch-free octant reduction t = min(|x|,|y|) * (1 / max(|x|,|y|)), atan t =
+ * t P(t^2) (degree-7 minimax on [0, 1], 7.2e-8 relative), pi/2 - r, pi - r and the sign of y
+ * by selects; <= 4 ulp against atan2.  Same form in the HIP kernels (pob_math.h). */
 static float orc_atan2f(float y, float x) {
-  if (x == 0.0f) {
-    if (y < 0.0f) return -1.5707963267948966f;
-    if (y == 0.0f) return 0.0f;
-    return 1.5707963267948966f;
-  }
-  if (y == 0.0f) return x < 0.0f ? 3.141592653589793f : 0.0f;
-  float w = 0.0f;
-  if (x < 0.0f) w = (y < 0.0f) ? -3.141592653589793f : 3.141592653589793f;
-  FL(2);
-  return w + orc_atanf(y / x);
+  FL(24);
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  float t = mn * (1.0f / mx);
+  t = mx > 0.0f ? t : 0.0f;
+  const float s = t * t;
+  float p = fmaf(s, -0.0047533135f, 0.024452504f);
+  p = fmaf(p, s, -0.059750218f);
+  p = fmaf(p, s, 0.09932368f);
+  p = fmaf(p, s, -0.14026737f);
+  p = fmaf(p, s, 0.19971494f);
+  p = fmaf(p, s, -0.33332205f);
+  p = fmaf(p, s, 0.99999994f);
+  float r = t * p;
+  r = ay > ax ? 1.5707964f - r : r;
+  r = x < 0.0f ? 3.1415927f - r : r;
+  r = copysignf(r, y);
+  return r + (x * 0.0f + y * 0.0f);
 }
 /* Cephes-form sinf/cosf with Cody-Waite reduction by pi/4. */
 static void orc_sincosf(float x, float *s, float *c) {

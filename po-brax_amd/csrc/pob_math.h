@@ -159,27 +159,29 @@ POB_D void qadd_half(q4 &acc, q4 d, float sign) {
   acc.y = FMA(h, d.y, acc.y); acc.z = FMA(h, d.z, acc.z);
 }
 
-// Cephes-form atanf / atan2f
-POB_D float pob_atanf(float x) {
-  float sign = 1.0f, y = 0.0f;
-  if (x < 0.0f) { sign = -1.0f; x = -x; }
-  if (x > 2.414213562373095f) { y = 1.5707963267948966f; x = -pob_rcp(x); }
-  else if (x > 0.4142135623730950f) { y = 0.7853981633974483f; x = POB_DIV(x - 1.0f, x + 1.0f); }
-  float z = x * x;
-  y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z -
-            3.33329491539e-1f) * z * x + x);
-  return sign * y;
-}
+// atan2f (spec, oracle orc_atan2f): branch-free octant reduction t = min(|x|,|y|) / max(|x|,|y|)
+// (correctly rounded reciprocal, then one multiply), atan t = t P(t^2) with a degree-7 minimax
+// polynomial on [0, 1] (7.2e-8 relative), then pi/2 - r, pi - r and the sign of y by selects:
+// <= 4 ulp against atan2 over the whole plane (no divergent branches, no division).  NaN
+// inputs give NaN.
 POB_D float pob_atan2f(float y, float x) {
-  if (x == 0.0f) {
-    if (y < 0.0f) return -1.5707963267948966f;
-    if (y == 0.0f) return 0.0f;
-    return 1.5707963267948966f;
-  }
-  if (y == 0.0f) return x < 0.0f ? 3.141592653589793f : 0.0f;
-  float w = 0.0f;
-  if (x < 0.0f) w = (y < 0.0f) ? -3.141592653589793f : 3.141592653589793f;
-  return w + pob_atanf(POB_DIV(y, x));
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  float t = mn * pob_rcp(mx);
+  t = mx > 0.0f ? t : 0.0f;
+  const float s = t * t;
+  float p = FMA(s, -0.0047533135f, 0.024452504f);
+  p = FMA(p, s, -0.059750218f);
+  p = FMA(p, s, 0.09932368f);
+  p = FMA(p, s, -0.14026737f);
+  p = FMA(p, s, 0.19971494f);
+  p = FMA(p, s, -0.33332205f);
+  p = FMA(p, s, 0.99999994f);
+  float r = t * p;
+  r = ay > ax ? 1.5707964f - r : r;
+  r = x < 0.0f ? 3.1415927f - r : r;
+  r = __builtin_copysignf(r, y);
+  return r + (x * 0.0f + y * 0.0f);  // + 0, or NaN for NaN / infinite inputs
 }
 // Cephes-form sinf/cosf (Cody-Waite reduction by pi/4)
 POB_D void pob_sincosf(float x, float *s, float *c) {
