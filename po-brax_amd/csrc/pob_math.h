@@ -75,6 +75,9 @@ POB_D v3 vcross(v3 a, v3 b) {
   return V(FMA(a.y, b.z, -(a.z * b.y)), FMA(a.z, b.x, -(a.x * b.z)), FMA(a.x, b.y, -(a.y * b.x)));
 }
 POB_D v3 vload(const float *p) { return V(p[0], p[1], p[2]); }
+// min(max(x, -h), h) for h >= 0 as one v_med3_f32 (equal to the oracle's fminf(fmaxf(..))
+// for every non-NaN x; no canonicalising moves)
+POB_D float clamp_sym(float x, float h) { return __builtin_amdgcn_fmed3f(x, -h, h); }
 
 // brax.math.rotate(v, q) = 2 (u.v) u + (s^2 - u.u) v + 2 s (u x v)
 POB_D v3 qrot(v3 v, q4 q) {

@@ -74,7 +74,7 @@ POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
   const v3 h = SV(S.wall_h[w]);
   v3 d = vsub(p, SV(S.wall_c[w]));
   float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
-  float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
+  float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
   float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
   float pen, nx, ny, nz;

@@ -119,7 +119,7 @@ POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on,
   const v3 h = V(r45.x, r45.y, S.wall_hz);
   v3 d = vsub(p, V(r01.x, r01.y, S.wall_cz));
   float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
-  float qx = fminf(fmaxf(lx, -h.x), h.x), qy = fminf(fmaxf(ly, -h.y), h.y), qz = fminf(fmaxf(lz, -h.z), h.z);
+  float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
   float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
   if (!(d2 >= T)) {
@@ -157,7 +157,8 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
   for (int c = 0; c < 2; ++c) {
     csys_t &S = *launder(Sp);
     const int l = qcontact_body(c);
-    v3 pe = qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
+    // the torso sphere's contact point is its centre (qrot_add of the zero vector == x)
+    const v3 pe = (c == 0 && S.torso_point) ? b.x[0] : qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
     ct.pen[c] = qground_r(S, LT, c) - pe.z;
     ct.pe[c] = pe;
   }
@@ -195,7 +196,8 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
     if (any_near) {
       v3 pe[2];
 #pragma unroll
-      for (int q = 0; q < nend; ++q) pe[q] = qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
+      for (int q = 0; q < nend; ++q)
+        pe[q] = (l == 0 && S.torso_point) ? b.x[0] : qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
       const float r = q_cap_r(S, LT, l);
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), rounded products
       uint32_t m = lane_mask;

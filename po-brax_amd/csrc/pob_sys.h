@@ -64,6 +64,8 @@ struct pob_sys {
   float wall_row[POB_MAXW][POB_WALL_FLOATS];  // the walls again, one row each (follows leg)
   float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
   int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)
+  int torso_point;    // body 0's capsule end and ground end are the body origin (the Ant torso
+                      // sphere): its contact points are x itself, no rotation needed
   const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env
 };
 static_assert(offsetof(pob_sys, wall_row) == offsetof(pob_sys, leg) + sizeof(float) * 4 * POB_LEG_FLOATS,

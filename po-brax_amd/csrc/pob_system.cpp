@@ -254,6 +254,10 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
       s.wall_hi[w][k] = (float)(s.wall_c[w][k] + ex[k] + reach);
     }
   }
+  s.torso_point = 1;
+  for (int q = 0; q < 2; ++q)
+    for (int c = 0; c < 3; ++c) s.torso_point &= s.cap_end[0][q][c] == 0.0f;
+  for (int c = 0; c < 3; ++c) s.torso_point &= s.ground_end[0][c] == 0.0f;
   return nullptr;
 }
 

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Interleaved A/B timing of libpob.so builds (default + build_variants/*.so), R rounds each,
+# one bench.py process per (round, lib); prints the per-lib median kernel ms.
+#   R=3 BS="65536" ENVS="ant_heavenhell" bash scripts/ab_bench.sh
+set -o pipefail
+shopt -s nullglob
+mkdir -p gpurun_out/ab
+R=${R:-3}
+libs="po-brax_amd/po_brax_amd/libpob.so $(ls build_variants/*.so 2>/dev/null)"
+for env in ${ENVS:-ant_heavenhell}; do
+  for B in ${BS:-65536}; do
+    for r in $(seq $R); do
+      for lib in $libs; do
+        tag=$(basename $lib .so)
+        POB_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps 200 --env $env --batch $B \
+          > gpurun_out/ab/$tag.$env.$B.$r.json 2>/dev/null || exit 1
+      done
+    done
+  done
+done
+python - <<'PY'
+import glob, json, collections, statistics
+d = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/ab/*.json"):
+    tag, env, B, r = f.split("/")[-1][:-5].rsplit(".", 3)
+    d[(env, B, tag)].append(json.load(open(f))["roofline"]["kernel_ms"])
+for k in sorted(d):
+    print(*k, "median %.4f" % statistics.median(d[k]), "runs", " ".join("%.4f" % x for x in sorted(d[k])))
+PY
