@@ -600,7 +600,7 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     v3 cn = vcross(rr, n);
     FL(2 + 8);
     float w = im + vdot(cn, cn);
-    float lam = pen / w;
+    float lam = pen * (1.0f / w);
     v3 P = vscl(n, lam);
     DX[i] = vfma(P, im, DX[i]);
     DA[i] = vadd(DA[i], vcross(rr, P));
@@ -614,7 +614,7 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
       v3 t = vdivs(dpt, lt);
       v3 ctn = vcross(rr, t);
       float wt = im + vdot(ctn, ctn);
-      float lamt = lt / wt;
+      float lamt = lt * (1.0f / wt);
       FL(3);
       if (lamt < e->friction * lam) {
         FL(8);
@@ -644,7 +644,7 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
     if (lt > 0.0f) {
       FL(4);
       float fr = fminf(e->friction * pen * e->inv_h, lt);
-      dv = vscl(vt, -(fr / lt));
+      dv = vscl(vt, -(fr * (1.0f / lt)));
     }
     if (vn < 0.0f) dv = vfma(n, -vn, dv);
     float D = sqrtf(vdot(dv, dv));
@@ -696,7 +696,7 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
       FL(1 + 2 + 1 + 1 + 1);
       const v3 ep = vcross(rp, d), ec = vcross(rc, d);
       const float den = fmaf(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
-      const float k = (L2 * e->s_pos) / den;
+      const float k = (L2 * e->s_pos) * (1.0f / den);
       P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
     }
     DX[p] = vfma(P, imp, DX[p]);

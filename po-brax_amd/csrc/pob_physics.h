@@ -186,7 +186,7 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
-        dv = vscl(vt, -(fr / lt));
+        dv = vscl(vt, -POB_DIV(fr, lt));
       }
       if (vn < 0.0f) dv = vfma(n, -vn, dv);
       float D = pob_sqrt(vdot(dv, dv));
