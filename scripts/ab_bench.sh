@@ -12,7 +12,7 @@ for env in ${ENVS:-ant_heavenhell}; do
     for r in $(seq $R); do
       for lib in $libs; do
         tag=$(basename $lib .so)
-        POB_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps 200 --env $env --batch $B \
+        POB_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-200} --env $env --batch $B \
           > gpurun_out/ab/$tag.$env.$B.$r.json 2>/dev/null || exit 1
       done
     done
