@@ -401,6 +401,10 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
     double q[4], ex[3] = {1, 0, 0}, ez[3] = {0, 0, 1}, a[3], r[3];
     d_euler_to_quat(J + 6, q);
     d_rotate(ex, q, a); d_rotate(ez, q, r);
+    /* components that are zero up to the euler rounding (|c| < 1e-9, e.g. cos 90 deg) are
+     * exactly zero: the hinge frames are then the exact axis-aligned / in-plane vectors the
+     * kernels exploit (pob_system.cpp does the same) */
+    for (int c = 0; c < 3; ++c) { if (fabs(a[c]) < 1e-9) a[c] = 0.0; if (fabs(r[c]) < 1e-9) r[c] = 0.0; }
     e->axis[j] = V((float)a[0], (float)a[1], (float)a[2]);
     e->ref[j] = V((float)r[0], (float)r[1], (float)r[2]);
     e->lim_lo[j] = (float)(J[9] * M_PI / 180.0);

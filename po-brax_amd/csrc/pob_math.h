@@ -105,6 +105,28 @@ POB_D v3 mrot(const m3 &R, v3 v) {
   return V(FMA(R.m02, v.z, FMA(R.m01, v.y, R.m00 * v.x)), FMA(R.m12, v.z, FMA(R.m11, v.y, R.m10 * v.x)),
            FMA(R.m22, v.z, FMA(R.m21, v.y, R.m20 * v.x)));
 }
+// mrot / qrot for the Ant's joint frames (pob_system.cpp checks the pattern): the products
+// with exactly-zero components dropped, which leaves every result unchanged (up to the sign
+// of a zero).  v in the xy-plane (v.z == 0):
+POB_D v3 mrot_xy(const m3 &R, v3 v) {
+  return V(FMA(R.m01, v.y, R.m00 * v.x), FMA(R.m11, v.y, R.m10 * v.x), FMA(R.m21, v.y, R.m20 * v.x));
+}
+POB_D v3 mcol0(const m3 &R) { return V(R.m00, R.m10, R.m20); }  // R (1, 0, 0)
+POB_D v3 mcol2(const m3 &R) { return V(R.m02, R.m12, R.m22); }  // R (0, 0, 1)
+// qrot((0, 0, 1), q)
+POB_D v3 qrot_ez(q4 q) {
+  const float t2 = 2.0f * q.z, c = FMA(q.w, q.w, -FMA(q.z, q.z, FMA(q.y, q.y, q.x * q.x)));
+  const float s2 = 2.0f * q.w;
+  return V(FMA(t2, q.x, s2 * q.y), FMA(t2, q.y, -(s2 * q.x)), FMA(t2, q.z, c));
+}
+// qrot(v, q) with v.z == 0
+POB_D v3 qrot_xy(v3 v, q4 q) {
+  const float t2 = 2.0f * FMA(q.y, v.y, q.x * v.x);
+  const float c = FMA(q.w, q.w, -FMA(q.z, q.z, FMA(q.y, q.y, q.x * q.x)));
+  const float s2 = 2.0f * q.w;
+  const v3 cr = V(-(q.z * v.y), q.z * v.x, FMA(q.x, v.y, -(q.y * v.x)));
+  return V(FMA(t2, q.x, FMA(c, v.x, s2 * cr.x)), FMA(t2, q.y, FMA(c, v.y, s2 * cr.y)), FMA(t2, q.z, s2 * cr.z));
+}
 // brax.math.quat_mul
 POB_D q4 qmul(q4 u, q4 v) {
   q4 r;

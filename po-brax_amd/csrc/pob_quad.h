@@ -331,14 +331,21 @@ POB_D void qjoint_position(csys_t *Sp, const float *LT, const QBody &b, const in
   v3 ap, ac, rp, rc;
   float psi;
   {
+    // Ant joint frames (checked by pob_system.cpp): offsets in the body xy-plane; the hip's
+    // axis is +z and reference -x, the knee's axis lies in the xy-plane and reference is +z
     const m3 Rp = qmat(b.q[p]), Rc = qmat(b.q[c]);
-    const v3 axis = QJV(LT, jl, QJ_AXIS), ref = QJV(LT, jl, QJ_REF);
-    ap = mrot(Rp, axis);
-    const v3 fp = mrot(Rp, ref), fc = mrot(Rc, ref);
+    v3 fp, fc;
+    if (jl == 0) {
+      ap = mcol2(Rp); ac = mcol2(Rc);
+      fp = vscl(mcol0(Rp), -1.0f); fc = vscl(mcol0(Rc), -1.0f);
+    } else {
+      const v3 axis = QJV(LT, jl, QJ_AXIS);
+      ap = mrot_xy(Rp, axis); ac = mrot_xy(Rc, axis);
+      fp = mcol2(Rp); fc = mcol2(Rc);
+    }
     psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
-    ac = mrot(Rc, axis);
-    rp = mrot(Rp, QJV(LT, jl, QJ_OFFP));
-    rc = mrot(Rc, QJV(LT, jl, QJ_OFFC));
+    rp = mrot_xy(Rp, QJV(LT, jl, QJ_OFFP));
+    rc = mrot_xy(Rc, QJV(LT, jl, QJ_OFFC));
   }
   // hinge axis alignment and angle limits
   const float lo = QJS(LT, jl, QJ_LO), hi = QJS(LT, jl, QJ_HI);
@@ -392,7 +399,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
       const int p = jparent(jl), c = jchild(jl);
-      v3 a = qrot(QJV(LT, jl, QJ_AXIS), b.q[p]);
+      const v3 a = jl == 0 ? qrot_ez(b.q[p]) : qrot_xy(QJV(LT, jl, QJ_AXIS), b.q[p]);
       v3 t = vscl(a, act[jl] * QJS(LT, jl, QJ_STRENGTH));
       v3 d = vscl(vsub(b.w[p], b.w[c]), QJS(LT, jl, QJ_DAMP));
       tt[jl] = vadd(t, d);

@@ -132,6 +132,12 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     d_euler_to_quat(J + 6, q);
     d_rotate(ex, q, a);
     d_rotate(ez, q, r);
+    // components that are zero up to the euler rounding (cos 90 deg = 6e-17) are exactly
+    // zero (oracle: same rule), so the hinge frames are the exact vectors pob_quad.h assumes
+    for (int c = 0; c < 3; ++c) {
+      if (fabs(a[c]) < 1e-9) a[c] = 0.0;
+      if (fabs(r[c]) < 1e-9) r[c] = 0.0;
+    }
     for (int c = 0; c < 3; ++c) { s.axis[j][c] = (float)a[c]; s.ref[j][c] = (float)r[c]; }
     s.lim_lo[j] = (float)(J[9] * M_PI / 180.0);
     s.lim_hi[j] = (float)(J[10] * M_PI / 180.0);
@@ -253,6 +259,18 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
       s.wall_lo[w][k] = (float)(s.wall_c[w][k] - ex[k] - reach);
       s.wall_hi[w][k] = (float)(s.wall_c[w][k] + ex[k] + reach);
     }
+  }
+  // joint frames the step kernel specialises (pob_quad.h qjoint_position): every offset lies in
+  // the body xy-plane; hips (joints 0, 2, 4, 6): axis = +z, reference = -x; knees: axis in the
+  // xy-plane, reference = +z
+  for (int j = 0; j < POB_NJ; ++j) {
+    bool ok = s.off_p[j][2] == 0.0f && s.off_c[j][2] == 0.0f;
+    if (j % 2 == 0)
+      ok = ok && s.axis[j][0] == 0.0f && s.axis[j][1] == 0.0f && s.axis[j][2] == 1.0f && s.ref[j][0] == -1.0f &&
+           s.ref[j][1] == 0.0f && s.ref[j][2] == 0.0f;
+    else
+      ok = ok && s.axis[j][2] == 0.0f && s.ref[j][0] == 0.0f && s.ref[j][1] == 0.0f && s.ref[j][2] == 1.0f;
+    if (!ok) return "joint frames differ from the Ant's (the step kernel assumes them)";
   }
   s.torso_point = 1;
   for (int q = 0; q < 2; ++q)
