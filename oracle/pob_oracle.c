@@ -140,6 +140,9 @@ static inline v3 qrot_add(v3 v, q4 q, v3 x) {
   return V(fmaf(t2, u.x, fmaf(c, v.x, fmaf(s2, cr.x, x.x))), fmaf(t2, u.y, fmaf(c, v.y, fmaf(s2, cr.y, x.y))),
            fmaf(t2, u.z, fmaf(c, v.z, fmaf(s2, cr.z, x.z))));
 }
+/* world point of a body-frame contact point: x + rotate(e, q) (rotation first, then the
+ * translation: the kernels share one rotation between a capsule's end points +-e) */
+static inline v3 cpoint(v3 e, q4 q, v3 x) { return vadd(x, qrot(e, q)); }
 /* Substep quaternion normalisation: with e = |q|^2 - 1 (exact, Sterbenz),
  * 1/|q| = 1 - e/2 + 3e^2/8 - 5e^3/16 + O(e^4) (truncation <= 35/128 e^4 < 2^-27 for
  * |e| <= 2^-6; rollouts stay below 2.4e-3); 1 / sqrt(|q|^2) outside that range.
@@ -418,6 +421,7 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
     d_rotate(ez, q, a);
     double r = f32d(ANT_CAP[i][0]), len = f32d(ANT_CAP[i][1]);
     double seg = len / 2 - r;
+    for (int c = 0; c < 3; ++c) if (fabs(a[c]) < 1e-9) a[c] = 0.0; /* as the joint frames */
     e->cap_r[i] = (float)r;
     int end = (int)ANT_CAP[i][2];
     if (seg == 0.0) { e->cap_nend[i] = 1; e->cap_end[i][0] = V(0, 0, 0); }
@@ -570,7 +574,7 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   int k = 0;
   for (int g = 0; g < e->n_ground; ++g, ++k) {
     int i = e->ground_body[g];
-    v3 pe = qrot_add(e->ground_end[g], b->q[i], b->x[i]);
+    v3 pe = cpoint(e->ground_end[g], b->q[i], b->x[i]);
     FL(1);
     ct->pen[k] = e->ground_r[g] - pe.z;
     ct->n[k] = V(0.0f, 0.0f, 1.0f);
@@ -580,7 +584,7 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
     float best = 0.0f; v3 bn = V(0, 0, 0), be = e->cap_end[i][0];
     for (int w = 0; w < e->n_walls; ++w)
       for (int q = 0; q < e->cap_nend[i]; ++q) {
-        v3 pe = qrot_add(e->cap_end[i][q], b->q[i], b->x[i]);
+        v3 pe = cpoint(e->cap_end[i][q], b->q[i], b->x[i]);
         v3 n; float pen = sphere_box(e, w, pe, e->cap_r[i], &n);
         if (pen > best) { best = pen; bn = n; be = e->cap_end[i][q]; }
       }
@@ -598,7 +602,7 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = qrot_add(ct->e[k], b->q[i], b->x[i]);
+    v3 pe = cpoint(ct->e[k], b->q[i], b->x[i]);
     v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 cn = vcross(rr, n);
@@ -636,7 +640,7 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = qrot_add(ct->e[k], b->q[i], b->x[i]);
+    v3 pe = cpoint(ct->e[k], b->q[i], b->x[i]);
     v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 vr = vadd(b->v[i], vcross(b->w[i], rr));

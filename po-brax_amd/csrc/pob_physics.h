@@ -100,7 +100,7 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
   for (int g = 0; g < POB_NGROUND; ++g) {
     csys_t &S = *launder(Sp);
     const int i = ground_body(g);
-    v3 pe = qrot_add(SV(S.ground_end[g]), b.q[i], b.x[i]);
+    v3 pe = vadd(b.x[i], qrot(SV(S.ground_end[g]), b.q[i]));
     ct.pen[g] = S.ground_r[g] - pe.z;
   }
   // wave-uniform broadphase: bit w set iff some lane's body-centre AABB meets wall w's grown box
@@ -127,7 +127,7 @@ POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
     const int nend = (i == 0) ? 1 : 2;
     v3 pe[2];
 #pragma unroll
-    for (int q = 0; q < nend; ++q) pe[q] = qrot_add(SV(S.cap_end[i][q]), b.q[i], b.x[i]);
+    for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[i], qrot(SV(S.cap_end[i][q]), b.q[i]));
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
@@ -176,7 +176,7 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       float rad;
       contact_geom(S, ct, k, e, n, rad);
       const float im = S.inv_mass[i];
-      v3 pe = qrot_add(e, b.q[i], b.x[i]);
+      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[i]);
       v3 vr = vadd(b.v[i], vcross(b.w[i], rr));

@@ -151,16 +151,22 @@ POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on,
 // the 16 envs is near).  Culled pairs have penetration < 0 and the walk keeps the oracle's
 // (wall, end) order with the strict ">" -- the deepest contact is unchanged.
 // WALLS = false compiles the wall search out (the stock ant has no walls).
+// Contact points are x + rotate(e, q) (oracle cpoint).  The Ant's capsules (checked by
+// pob_system.cpp) have opposite end points +-e0 in the body xy-plane, so one rotation
+// rv = rotate(e0, q) serves both (rotate(-e0) = -rv exactly), and a lower leg's ground point
+// is its end 1 (x - rv).  The torso sphere's points are its centre x (rotate(0) = 0).
 template <bool WALLS>
 POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QContacts &ct) {
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  v3 rv_leg;
+  {
     csys_t &S = *launder(Sp);
-    const int l = qcontact_body(c);
-    // the torso sphere's contact point is its centre (qrot_add of the zero vector == x)
-    const v3 pe = (c == 0 && S.torso_point) ? b.x[0] : qrot_add(qground_end(S, LT, c), b.q[l], b.x[l]);
-    ct.pen[c] = qground_r(S, LT, c) - pe.z;
-    ct.pe[c] = pe;
+    rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
+    const v3 pe0 = S.torso_point ? b.x[0] : vadd(b.x[0], qrot(qground_end(S, LT, 0), b.q[0]));
+    const v3 pe1 = vsub(b.x[2], rv_leg);
+    ct.pen[0] = qground_r(S, LT, 0) - pe0.z;
+    ct.pen[1] = qground_r(S, LT, 1) - pe1.z;
+    ct.pe[0] = pe0;
+    ct.pe[1] = pe1;
   }
   uint32_t lane_mask = 0u;
   if (WALLS) {
@@ -195,9 +201,13 @@ POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b,
     v3 bpe = bn;
     if (any_near) {
       v3 pe[2];
-#pragma unroll
-      for (int q = 0; q < nend; ++q)
-        pe[q] = (l == 0 && S.torso_point) ? b.x[0] : qrot_add(qcap_end(S, LT, l, q), b.q[l], b.x[l]);
+      if (l == 0) {
+        pe[0] = S.torso_point ? b.x[0] : vadd(b.x[0], qrot(qcap_end(S, LT, 0, 0), b.q[0]));
+      } else {
+        const v3 rv = l == 2 ? rv_leg : qrot_xy(qcap_end(S, LT, 1, 0), b.q[1]);
+        pe[0] = vadd(b.x[l], rv);
+        pe[1] = vsub(b.x[l], rv);
+      }
       const float r = q_cap_r(S, LT, l);
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), rounded products
       uint32_t m = lane_mask;
@@ -243,7 +253,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       float rad;
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
-      const v3 pe = ct.pe[c];  // = qrot_add(e, b.q[l], b.x[l]) of the detection (same q, x)
+      const v3 pe = ct.pe[c];  // = x + rotate(e, q) of the detection (same q, x)
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 cn = vcross(rr, n);
@@ -284,7 +294,7 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       float rad;
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
-      v3 pe = qrot_add(e, b.q[l], b.x[l]);
+      v3 pe = l == 0 ? vadd(b.x[0], qrot(e, b.q[0])) : vadd(b.x[l], qrot_xy(e, b.q[l]));
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 vr = vadd(b.v[l], vcross(b.w[l], rr));

@@ -151,6 +151,8 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     d_rotate(ez, q, a);
     double r = f32d(kCapsule[i][0]), len = f32d(kCapsule[i][1]);
     double seg = len / 2 - r;
+    for (int c = 0; c < 3; ++c)
+      if (fabs(a[c]) < 1e-9) a[c] = 0.0;  // as the joint frames (oracle: same rule)
     int end = (int)kCapsule[i][2];
     s.cap_r[i] = (float)r;
     if ((i == 0) != (seg == 0.0)) return "ant topology: only the torso capsule is a sphere";
@@ -272,6 +274,15 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
       ok = ok && s.axis[j][2] == 0.0f && s.ref[j][0] == 0.0f && s.ref[j][1] == 0.0f && s.ref[j][2] == 1.0f;
     if (!ok) return "joint frames differ from the Ant's (the step kernel assumes them)";
   }
+  // capsules the contact passes specialise: end points in the body xy-plane, the two ends of
+  // a capsule opposite (one rotation serves both), a lower leg's ground point = its end 1
+  for (int i = 1; i < POB_NDYN; ++i)
+    for (int c = 0; c < 3; ++c)
+      if (s.cap_end[i][0][2] != 0.0f || s.cap_end[i][1][c] != -s.cap_end[i][0][c])
+        return "capsules differ from the Ant's (the step kernel assumes them)";
+  for (int g = 1; g < POB_NGROUND; ++g)
+    for (int c = 0; c < 3; ++c)
+      if (s.ground_end[g][c] != s.cap_end[2 * g][1][c]) return "ground contact points differ from the Ant's";
   s.torso_point = 1;
   for (int q = 0; q < 2; ++q)
     for (int c = 0; c < 3; ++c) s.torso_point &= s.cap_end[0][q][c] == 0.0f;
