@@ -50,7 +50,7 @@ POB_D float quad_bcast(float x) {
 // and schedules the moves, instead of one s_nop per asm statement.
 template <int J>
 POB_D float quad_bcast_b(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), J * 0x55, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), J * 0x55, 0xf, 0xf, true));
 }
 template <int J> POB_D v3 quad_bcast3(v3 a) { return V(quad_bcast_b<J>(a.x), quad_bcast_b<J>(a.y), quad_bcast_b<J>(a.z)); }
 
@@ -486,8 +486,10 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     b.q[l] = qnormalize(b.q[l]);
     b.v[l] = vscl(vsub(b.x[l], L.get3(QL_PX(l))), S.inv_h);
     q4 dq = qmul(b.q[l], qinv(L.get4(QL_PQ(l))));
-    float sg = dq.w >= 0.0f ? 1.0f : -1.0f;
-    b.w[l] = V(sg * ((2.0f * dq.x) * S.inv_h), sg * ((2.0f * dq.y) * S.inv_h), sg * ((2.0f * dq.z) * S.inv_h));
+    // sg ((2 dq) inv_h) == dq (sg 2 inv_h) bit for bit (scaling by 2 and by +-1 is exact)
+    const float k2 = 2.0f * S.inv_h;
+    const float kw = dq.w >= 0.0f ? k2 : -k2;
+    b.w[l] = V(dq.x * kw, dq.y * kw, dq.z * kw);
   }
   // 5. velocity-level contacts
   if (COLLIDE) {
