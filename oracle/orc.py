@@ -84,6 +84,7 @@ def _declare(_lib):
         _lib.orc_randint.argtypes = [_UP, C.c_int, C.c_int]
         _lib.orc_choice_idx.argtypes = [_UP, C.c_int, C.c_int, C.POINTER(C.c_int)]
         _lib.orc_flops_read_and_reset.restype = C.c_longlong
+        _lib.orc_math_check.argtypes = [C.c_int, C.c_int, _FP, _FP, _FP]
     return _lib
 
 
@@ -213,3 +214,14 @@ def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_E
     for _ in range(steps):
         s = e.step(s, rng.uniform(-1, 1, (B, 8)).astype(np.float32), flags=flags, nthreads=1, inplace=True)
     return e._L.orc_flops_read_and_reset() / float(B * steps)
+
+
+def math_check(op: int, a: np.ndarray, b: np.ndarray = None) -> np.ndarray:
+    """The spec's atan2f (op 0: atan2f(a, b)) or substep quaternion normalisation (op 1:
+    rows of a (n, 4)) as the oracle computes them."""
+    a = np.ascontiguousarray(a, np.float32)
+    n = a.shape[0]
+    b = np.ascontiguousarray(b if b is not None else np.zeros(n), np.float32)
+    out = np.zeros_like(a)
+    lib().orc_math_check(op, n, _p(a), _p(b), _p(out))
+    return out

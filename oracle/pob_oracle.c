@@ -180,6 +180,19 @@ static float orc_atan2f(float y, float x) {
   r = copysignf(r, y);
   return r + (x * 0.0f + y * 0.0f);
 }
+/* Test hook for the spec's elementary functions (tests/test_oracle_golden.py):
+ * op 0: out[i] = orc_atan2f(a[i], b[i]); op 1: the substep normalisation of the quaternions
+ * a[4i..4i+3] into out[4i..4i+3]. */
+void orc_math_check(int op, int n, const float *a, const float *b, float *out) {
+  for (int i = 0; i < n; ++i) {
+    if (op == 0) out[i] = orc_atan2f(a[i], b[i]);
+    else {
+      q4 q = {a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
+      q4 r = qnormalize(q);
+      out[4 * i] = r.w; out[4 * i + 1] = r.x; out[4 * i + 2] = r.y; out[4 * i + 3] = r.z;
+    }
+  }
+}
 /* Cephes-form sinf/cosf with Cody-Waite reduction by pi/4. */
 static void orc_sincosf(float x, float *s, float *c) {
   FL(26);

@@ -68,6 +68,8 @@ void orc_env_dims(const orc_env *e, int *n_bodies, int *obs_dim, int *act_dim);
 
 /* algorithmic FLOP counter (only in the -DORC_COUNT_FLOPS build; else -1) */
 long long orc_flops_read_and_reset(void);
+/* test hook: op 0 atan2f(a, b); op 1 substep quaternion normalisation of a (n x 4) */
+void orc_math_check(int op, int n, const float *a, const float *b, float *out);
 
 /* RNG (jax threefry, pre-partitionable) */
 void orc_threefry2x32(const uint32_t key[2], uint32_t x0, uint32_t x1, uint32_t out[2]);
