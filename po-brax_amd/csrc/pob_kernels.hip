@@ -1196,13 +1196,18 @@ static void launch_reset(int kind, dim3 g, hipStream_t st, const void *sp, int B
   }
 }
 template <typename QT>
-static void launch_step_quad(int kind, dim3 g, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+static void launch_step_quad(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                              const float *act, const StatePtrs &po, uint32_t flags, int L) {
+  // Batches of at most one wave per CU launch one-wave blocks, so each wave gets a CU (its
+  // scalar unit, LDS and instruction cache) to itself instead of four waves sharing 1/4 of
+  // the CUs; larger batches use 256-thread blocks (the kernel is block-size agnostic)
+  const int bs = 4 * B <= 64 * 256 ? 64 : 256;
+  const dim3 g = grid_for(4 * B, bs), b(bs);
   switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_TAG: hipLaunchKernelGGL((k_step_quad<POB_TAG, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
-    default: hipLaunchKernelGGL((k_step_quad<POB_ANT, QT>), g, dim3(256), 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_quad<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_quad<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
 }
 extern "C" {
@@ -1321,9 +1326,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const dim3 g = grid_for(4 * B, 256);
-  if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
-  else launch_step_quad<float>(e->sys.kind, g, st, sp, B, pi, act, po, flags, episode_length);
+  if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else launch_step_quad<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");
 }
 
