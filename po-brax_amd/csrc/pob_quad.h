@@ -254,6 +254,33 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       qcontact_geom(S, LT, ct, c, e, n, rad);
       const float im = q_inv_mass(S, LT, l);
       const v3 pe = ct.pe[c];  // = x + rotate(e, q) of the detection (same q, x)
+      if (c < 2) {
+        // ground contact, n = (0, 0, 1): the expressions below with the products by the
+        // normal's exact zeros dropped (same values up to the sign of a zero)
+        const v3 cp = V(pe.x, pe.y, pe.z - rad);
+        const v3 rr = vsub(cp, b.x[l]);
+        const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
+        const float lam = POB_DIV(pen, w);
+        DX[l].z = FMA(lam, im, DX[l].z);  // P = (0, 0, lam)
+        DA[l] = V(DA[l].x + rr.y * lam, DA[l].y + -(rr.x * lam), DA[l].z);  // rr x P
+        const v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
+        const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
+        const float lt = pob_sqrt(FMA(dpy, dpy, dpx * dpx));
+        if (lt > 0.0f) {
+          const float inv = pob_rcp(lt);
+          const float tx = dpx * inv, ty = dpy * inv;
+          const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
+          const float wt = im + vdot(ctn, ctn);
+          const float lamt = POB_DIV(lt, wt);
+          if (lamt < S.friction * lam) {
+            const float px = tx * -lamt, py = ty * -lamt;
+            DX[l].x = FMA(px, im, DX[l].x);
+            DX[l].y = FMA(py, im, DX[l].y);
+            DA[l] = vadd(DA[l], V(-(rr.z * py), rr.z * px, FMA(rr.x, py, -(rr.y * px))));  // rr x Pt
+          }
+        }
+        continue;
+      }
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 cn = vcross(rr, n);
@@ -298,15 +325,27 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 cp = vfma(n, -rad, pe);
       v3 rr = vsub(cp, b.x[l]);
       v3 vr = vadd(b.v[l], vcross(b.w[l], rr));
-      float vn = vdot(vr, n);
-      v3 vt = vfma(n, -vn, vr);
-      float lt = pob_sqrt(vdot(vt, vt));
       v3 dv = V(0.0f, 0.0f, 0.0f);
-      if (lt > 0.0f) {
-        float fr = fminf(S.friction * pen * S.inv_h, lt);
-        dv = vscl(vt, -POB_DIV(fr, lt));
+      if (c < 2) {
+        // ground, n = (0, 0, 1) (zero products dropped, as in the position pass)
+        const float vn = vr.z;
+        const float lt = pob_sqrt(FMA(vr.y, vr.y, vr.x * vr.x));
+        if (lt > 0.0f) {
+          const float fr = fminf(S.friction * pen * S.inv_h, lt);
+          const float k = -POB_DIV(fr, lt);
+          dv = V(vr.x * k, vr.y * k, 0.0f);
+        }
+        if (vn < 0.0f) dv.z = -vn;
+      } else {
+        float vn = vdot(vr, n);
+        v3 vt = vfma(n, -vn, vr);
+        float lt = pob_sqrt(vdot(vt, vt));
+        if (lt > 0.0f) {
+          float fr = fminf(S.friction * pen * S.inv_h, lt);
+          dv = vscl(vt, -POB_DIV(fr, lt));
+        }
+        if (vn < 0.0f) dv = vfma(n, -vn, dv);
       }
-      if (vn < 0.0f) dv = vfma(n, -vn, dv);
       float D = pob_sqrt(vdot(dv, dv));
       if (D > 0.0f) {
         v3 dh = vdivs(dv, D);
