@@ -9,16 +9,24 @@ POMDP logic, obs, episode counter, autoreset).  Synthetic inputs as the survey p
 ``key, k = split(key)``, ``action = uniform(k, (B_total, 8), -1, 1)`` -- all generated on the
 device by the threefry kernels BEFORE the timed region (inputs resident in HBM).
 
-Multi-GPU: one process per GPU (torchrun), each rank owns B envs (weak scaling, no
-collective on the data path); barrier + synchronize bracket the K timed steps and the
-max over ranks is reported.  Rank 0 prints ONE JSON line.
+Modes (other BASELINE configs):
+  --batch B              envs per GPU (weak scaling, the default: B = 65 536 per GPU)
+  --global-batch G       G envs split over the ranks (strong scaling): config 4 is
+                         ``--env ant_tag --global-batch 65536 --gather-obs`` and config 5
+                         ``--env mixed --qp-dtype f16 --global-batch 262144``
+  --gather-obs           RCCL all-gather of the observation batch inside every timed step
+  --gym                  the create_gym_env path (AutoresetVmapGymWrapper: step kernel,
+                         cross-rank any-done all-reduce, masked gym reset kernel)
+
+Multi-GPU: one process per GPU (torchrun); barrier + synchronize bracket the K timed steps
+and the max over ranks is reported.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
-import platform
 import sys
 import time
 
@@ -37,6 +45,10 @@ _TASK_READ = {"ant_heavenhell": 6, "ant_gather": 48, "ant_tag": 2, "ant": 0}
 _TASK_WRITE = {"ant_heavenhell": 0, "ant_gather": 48, "ant_tag": 3, "ant": 0}
 _OBS = {"ant_heavenhell": 114, "ant_gather": 211, "ant_tag": 103, "ant": 87}
 MIXED = ("ant_heavenhell", "ant_gather", "ant_tag")  # --env mixed (BASELINE.json config 5)
+VALU_PEAK_TF = 157.3   # FP32 vector peak, MI355X_MICROARCH.md (chip-level parameters)
+HBM_PEAK_GBS = 8000.0  # HBM3E spec peak
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+CLK_MAX_GHZ = 2.4      # max shader clock; a wave64 VALU instruction holds its SIMD 2 cycles
 
 
 def bytes_per_env_step(name: str, qp_bytes: int = 4) -> int:
@@ -60,12 +72,15 @@ def main() -> int:
                     help="'mixed' = HH + GA + TAG batches (B split 3 ways) in one launch per step")
     ap.add_argument("--qp-dtype", default="f32", choices=["f32", "f16"],
                     help="qp storage (f16 = binary16 qp, float32 arithmetic)")
-    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total envs split over the ranks (strong scaling); overrides --batch")
     ap.add_argument("--episode-length", type=int, default=1000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
+    ap.add_argument("--gym", action="store_true", help="create_gym_env path (gym-side autoreset)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-obs", action="store_true",
-                    help="also time an RCCL all-gather of the final obs batch (N>1)")
+                    help="RCCL all-gather of the obs batch inside every timed step (N>1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -78,16 +93,25 @@ def main() -> int:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if args.gym and args.env == "mixed":
+        ap.error("--gym runs one env kind")
 
     from po_brax_amd import envs, jumpy
-    from po_brax_amd.sharding import shard_keys, shard_range
+    from po_brax_amd.sharding import Shard, gather_obs, gather_obs_ragged, shard_keys
 
-    B = args.batch
-    total = B * world
-    lo, hi = shard_range(total, world, rank)
+    strong = args.global_batch > 0
+    total = args.global_batch if strong else args.batch * world
+    shard = Shard(total, world, rank)
+    lo, B = shard.lo, shard.size
     qp_dtype = torch.float16 if args.qp_dtype == "f16" else torch.float32
     key = jumpy.random_prngkey(0, device=dev)
-    if args.env == "mixed":
+    gym = None
+    if args.gym:
+        gym = envs.create_gym_env(args.env, batch_size=total, seed=0, episode_length=args.episode_length,
+                                  device=dev, qp_dtype=qp_dtype, shard=shard if world > 1 else None)
+        gym.reset()
+        state = None
+    elif args.env == "mixed":
         # rank r owns global envs [lo, hi); within it the kinds follow one another
         env = envs.create_mixed(MIXED, episode_length=args.episode_length, device=dev, qp_dtype=qp_dtype)
         sizes = mixed_sizes(B)
@@ -116,46 +140,60 @@ def main() -> int:
         jumpy.random_actions_(act_key, total, lo, acts[0])
         return acts[0]
 
+    def obs_of():
+        if gym is not None:
+            return gym._state.obs
+        return torch.cat([s.obs.reshape(-1) for s in state]) if args.env == "mixed" else state.obs
+
+    do_gather = args.gather_obs and world > 1 and args.env != "mixed"
+    equal = total % world == 0
+
+    def one_step(t):
+        if gym is not None:
+            gym.step(act_at(t))
+        else:
+            env.step_(state, act_at(t))
+
+    def gather():
+        o = obs_of()
+        return gather_obs(o) if equal else gather_obs_ragged(o, total)
+
     for t in range(args.warmup):
-        env.step_(state, act_at(t))
+        one_step(t)
+        if do_gather:
+            gather()
     torch.cuda.synchronize()
 
-    # timed region: K steps, per-step events bracket the one fused kernel of each step
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    # timed region: K steps; events bracket the step's kernels (and, with --gather-obs, the
+    # all-gather that follows them) on torch's current stream, which the kernels use
+    ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_c = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if do_gather else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evs[0].record()
     for k in range(args.steps):
-        env.step_(state, act_at(args.warmup + k))
-        evs[k + 1].record()
+        ev_a[k].record()
+        one_step(args.warmup + k)
+        ev_b[k].record()
+        if do_gather:
+            gather()
+            ev_c[k].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    gpu_ms = evs[0].elapsed_time(evs[-1])
-    per = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
-    elapsed = torch.tensor([wall, gpu_ms], dtype=torch.float64, device=dev)
+    per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
+    kern_ms = sum(per) / len(per)
+    gather_ms = (sum(ev_b[k].elapsed_time(ev_c[k]) for k in range(args.steps)) / args.steps) if do_gather else None
+    elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    wall, gpu_ms = float(elapsed[0]), float(elapsed[1])
+    wall, kern_ms_max = float(elapsed[0]), float(elapsed[1])
     ms_per_step = 1e3 * wall / args.steps
     value = total * args.steps / wall
-    obs_last = torch.cat([s.obs.reshape(-1) for s in state]) if args.env == "mixed" else state.obs
-    finite = bool(torch.isfinite(obs_last).all())
-
-    gather_ms = None
-    if args.gather_obs and world > 1:
-        from po_brax_amd.sharding import gather_obs
-        gather_obs(obs_last)
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
-        for _ in range(5):
-            gather_obs(obs_last)
-        torch.cuda.synchronize()
-        gather_ms = 1e3 * (time.perf_counter() - g0) / 5
+    finite = bool(torch.isfinite(obs_of()).all())
 
     if rank != 0:
         if world > 1:
@@ -163,56 +201,81 @@ def main() -> int:
             dist.destroy_process_group()
         return 0
 
-    # roofline of the dominant kernel (k_step): algorithmic bytes and FLOPs per launch
+    # roofline of the dominant kernel (k_step) on this rank: algorithmic FLOPs per launch
+    # (the path is FP32-VALU bound, not HBM or MFMA) and bytes per launch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    kern_ms = sum(per) / len(per)
     qb = 2 if args.qp_dtype == "f16" else 4
     kinds = list(zip(MIXED, mixed_sizes(B))) if args.env == "mixed" else [(args.env, B)]
     bpe = sum(bytes_per_env_step(n, qb) * b for n, b in kinds) / B
     try:
         import orc  # test-infrastructure oracle: FLOP count of the restated algorithm only
-        fpe = sum(orc.flops_per_env_step(n, B=64, steps=10) * b for n, b in kinds) / B
+        f_ref = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_REF_PAIRS) * b for n, b in kinds) / B
+        f_exe = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_EXECUTED) * b for n, b in kinds) / B
     except Exception as ex:  # pragma: no cover
         print(f"flop count unavailable: {ex}", file=sys.stderr)
-        fpe = float("nan")
-    hbm_gbs = bpe * B / (kern_ms * 1e-3) / 1e9
-    tflops = fpe * B / (kern_ms * 1e-3) / 1e12
+        f_ref = f_exe = float("nan")
+    ks = kern_ms * 1e-3
+    hbm_gbs = bpe * B / ks / 1e9
+    tflops = f_ref * B / ks / 1e12
+    kname = "k_step_mixed" if args.env == "mixed" else f"k_step_quad<{args.env}>"
     roofline = {
-        "bound": "valu", "achieved": round(tflops, 3), "peak": 157.3, "unit": "TFLOP/s",
-        "frac": round(tflops / 157.3, 5), "traffic": None,
-        "kernel": "k_step_mixed" if args.env == "mixed" else f"k_step_quad<{args.env}>",
-        "kernel_ms": round(kern_ms, 4),
-        "flops_per_env_step": round(fpe, 1), "bytes_per_env_step": round(bpe, 1),
-        "hbm": {"achieved": round(hbm_gbs, 2), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(hbm_gbs / 8000.0, 6)},
+        "bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TF, "unit": "TFLOP/s",
+        "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
+        "kernel": kname + (" + gym any-done + k_reset(where done)" if gym is not None else ""),
+        "kernel_ms": round(kern_ms, 4), "units_per_launch": B,
+        "flops_per_env_step": round(f_ref, 1),
+        "flops_basis": "instrumented CPU restatement (oracle/pob_oracle.c, ORC_COUNT_FLOPS), executed branches, "
+                       "every capsule x wall x end pair evaluated as in the reference (brax evaluates all pairs)",
+        "flops_executed_per_env_step": round(f_exe, 1),
+        "frac_executed": round(f_exe * B / ks / 1e12 / VALU_PEAK_TF, 5),
+        "bytes_per_env_step": round(bpe, 1),
+        "hbm": {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
     }
-
-    tr = committed_traffic(args.env, B, args.qp_dtype)
-    if tr is not None:
-        roofline["traffic"] = tr["traffic_bytes"]
-        roofline["traffic_source"] = (f"profiles/{tr['source']}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
-                                      f"WRITE_SIZE per launch of the same kernel and config")
+    prof = committed_profile(args.env, B, args.qp_dtype)
+    if prof is not None and gym is None:
+        if prof.get("traffic_bytes"):
+            roofline["traffic"] = prof["traffic_bytes"]
+            roofline["traffic_source"] = (f"profiles/{prof['source']}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + "
+                                          f"WRITE_SIZE per launch of the same kernel and config")
+        if prof.get("valu_insts"):
+            vi = prof["valu_insts"]
+            roofline["valu_insts_per_launch"] = vi
+            # a wave64 VALU instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md)
+            roofline["valu_issue_frac"] = round(2.0 * vi / (SIMDS * ks * CLK_MAX_GHZ * 1e9), 4)
+            if prof.get("grbm_gui_active"):
+                cyc = prof["grbm_gui_active"] / 8.0  # GRBM sums the 8 XCDs
+                roofline["valu_issue_frac_profiled_clock"] = round(2.0 * vi / (SIMDS * cyc), 4)
+            roofline["valu_source"] = (f"profiles/{prof['source']}: SQ_INSTS_VALU per launch x 2 cycles / "
+                                       f"({SIMDS} SIMDs x live kernel time x {CLK_MAX_GHZ} GHz); "
+                                       "profiled_clock: / (SIMDs x GRBM_GUI_ACTIVE/8) of the profiled launch")
 
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, args.cpu_seconds)
+    if not args.no_cpu_baseline and world == 1 and gym is None:
+        cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, B, args.cpu_seconds)
 
+    par = f"env-shard x{world}" + (" (strong: global batch split)" if strong else " (weak: batch per GPU)")
     line = {
-        "metric": f"env-steps/sec {args.env} batch {B}/GPU",
+        "metric": f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU"),
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{args.env} B={B}/GPU, create(batch_size=B, episode_length="
-                               f"{args.episode_length}) autoreset chain, PBD 10 substeps, random "
+        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.env} B={B}/GPU (global {total}), "
+                               + ("create_gym_env (AutoresetVmapGymWrapper, gym-side autoreset)"
+                                  if gym is not None else "create(batch_size=B) autoreset chain")
+                               + f", episode_length {args.episode_length}, PBD 10 substeps, random "
                                "uniform(-1,1) actions (threefry)"
-                               + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else ""),
-                   "env": args.env, "global_batch": total, "episode_length": args.episode_length,
-                   "qp_storage": args.qp_dtype, "parallelism": f"env-shard x{world}"},
-        "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+                               + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else "")
+                               + (", RCCL obs all-gather per step" if do_gather else ""),
+                   "env": args.env, "global_batch": total, "batch_per_gpu": B,
+                   "episode_length": args.episode_length, "qp_storage": args.qp_dtype, "parallelism": par,
+                   "path": "gym" if gym is not None else "brax"},
+        "gpu_event_ms_per_step": round(kern_ms_max + (float(elapsed[2]) if do_gather else 0.0), 4),
         "roofline": roofline, "cpu_baseline": cpu, "obs_finite": finite,
     }
-    if gather_ms is not None:
-        line["obs_allgather_ms"] = round(gather_ms, 3)
+    if do_gather:
+        line["obs_allgather_ms"] = round(float(elapsed[2]), 4)
+        line["obs_allgather_bytes"] = total * obs_of().shape[-1] * 4
     print(json.dumps(line))
     if world > 1:
         dist.barrier()
@@ -220,10 +283,9 @@ def main() -> int:
     return 0
 
 
-def committed_traffic(env: str, B: int, qp: str):
-    """HBM bytes per launch from the newest committed PMC profile of this exact config
+def committed_profile(env: str, B: int, qp: str):
+    """Counters per launch from the newest committed PMC profile of this exact config
     (profiles/*_traffic.json, written by profiles/summarize.py); None if there is none."""
-    import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
         try:
@@ -236,34 +298,42 @@ def committed_traffic(env: str, B: int, qp: str):
     return best
 
 
-def cpu_baseline(name: str, seconds: float) -> dict:
-    """The C oracle (kind "port": CPU restatement, same algorithm) on the host cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def cpu_baseline(name: str, B: int, seconds: float) -> dict:
+    """The C restatement (kind "port": same algorithm, oracle/pob_oracle.c) compiled
+    -O3 -march=native on this host, timed on the same workload (this GPU's batch B):
+    one thread and all host threads (OpenMP over envs).  Time-boxed samples."""
     import numpy as np
     import orc
     import pob_np as P
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    Bc = 4096
-    e = orc.OracleEnv(name)
-    s = e.reset(P.split(P.prngkey(0), Bc + 1)[1:], first=True, nthreads=cores)
-    rng = np.random.default_rng(0)
-    acts = rng.uniform(-1, 1, (4, Bc, 8)).astype(np.float32)
-    e.step(s, acts[0], flags=3, nthreads=cores, inplace=True)  # warm the thread pool
-    n, t0 = 0, time.perf_counter()
-    while True:
-        e.step(s, acts[n % 4], flags=3, nthreads=cores, inplace=True)
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(Bc * n / dt, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{name} B={Bc}, {n} steps ({dt:.1f} s) of the same fused step with OpenMP "
-                      f"over envs, gcc -O2 (oracle/pob_oracle.c)",
-            "cpu": platform.processor() or platform.machine()}
+        aff = os.cpu_count() or 1
+    # the process's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box
+    # sets 16), else every core this process may run on
+    cores = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff)))
+    e = orc.OracleEnv(name, native=True)
+    s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=cores)
+    acts = np.random.default_rng(0).uniform(-1, 1, (2, B, 8)).astype(np.float32)
+    out = {}
+    for leg, nt in (("all", cores), ("single", 1)):
+        e.step(s, acts[0], flags=3, nthreads=nt, inplace=True)  # warm caches / the thread pool
+        n, t0 = 0, time.perf_counter()
+        while True:
+            e.step(s, acts[n % 2], flags=3, nthreads=nt, inplace=True)
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        out[leg] = (B * n / dt, n, dt)
+    v, n, dt = out["all"]
+    v1, n1, dt1 = out["single"]
+    return {"value": round(v, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "single_thread_value": round(v1, 1),
+            "sample": f"{name} B={B} (the GPU workload's batch): {n} steps in {dt:.1f} s on {cores} threads, "
+                      f"{n1} steps in {dt1:.1f} s on 1 thread; the same fused step (oracle/pob_oracle.c) "
+                      "gcc -O3 -march=native, OpenMP over envs",
+            "cpu": orc.cpu_model(), "nproc": os.cpu_count(), "affinity_cores": aff}
 
 
 if __name__ == "__main__":

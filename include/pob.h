@@ -21,10 +21,14 @@
  *                       batch each) fused into ONE kernel launch (BASELINE.json config 5)
  *   pob_reset_where_done AutoresetVmapGymWrapper.step tail wrappers.py:245-262 and
  *                       RandomizedAutoResetWrapperNaive/OnTerminal wrappers.py:30-80
+ *   pob_reset_where_done_shard  the same tail for one rank's shard of the gym batch
+ *                       (global keys split(gym_key, B_total + 1), all-reduced any-done)
  *   pob_default_qp      System.default_qp(joint_angle, joint_velocity) [ext], called at
  *                       ant_heavenhell.py:95, ant_gather.py:116, ant_tag.py:72
  *   pob_random_*        brax.jumpy.random_split / random_uniform under jit ->
- *                       jax.random.split / uniform (threefry2x32) [ext]; more_jp.py:57-77
+ *                       jax.random.split / uniform (threefry2x32) [ext]; more_jp.py:57-77;
+ *                       pob_random_split_batch = the per-env split of
+ *                       RandomizedAutoResetWrapperCached.step wrappers.py:103
  *   pob_obs_gather      obs[:, idx] with the index sets of
  *                       po_brax/standard_observability_masks.py:5-67
  *
@@ -44,7 +48,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 2
+#define POB_ABI_VERSION 3
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -128,11 +132,20 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
                    int episode_length, void *stream);
 int pob_reset_where_done(pob_env *env, int B, int mode, const uint32_t *gym_key_in,
                          uint32_t *gym_key_out, const pob_state *s, void *stream);
+/* The same for a shard: this env batch holds rows [first, first + B) of a global batch of
+ * `total` envs split over ranks (AutoresetVmapGymWrapper under index sharding).  Gym mode
+ * keys are split(gym_key, total + 1)[1 + first + b]; s->any_done must then hold the GLOBAL
+ * any-done flag (the caller all-reduces it, MAX, across ranks before this call). */
+int pob_reset_where_done_shard(pob_env *env, int B, int total, int first, int mode,
+                               const uint32_t *gym_key_in, uint32_t *gym_key_out, const pob_state *s,
+                               void *stream);
 int pob_default_qp(pob_env *env, int B, const float *qpos, const float *qvel, float *pos, float *rot,
                    float *vel, float *ang, void *stream);
 
 /* jax.random on device: split(key, num) rows [first, first+count) -> out (count,2) */
 int pob_random_split(const uint32_t *key, int num, int first, int count, uint32_t *out, void *stream);
+/* vmap(split)(keys, num): keys (B,2) -> out (B,num,2)  (jax.vmap(jax.random.split)) */
+int pob_random_split_batch(const uint32_t *keys, int B, int num, uint32_t *out, void *stream);
 /* uniform(key, (n,), lo, hi) elements [first, first+count) */
 int pob_random_uniform(const uint32_t *key, int n, int first, int count, float lo, float hi, float *out,
                        void *stream);

@@ -20,18 +20,42 @@ F_EPISODE, F_AUTORESET = 1, 2
 FLOPS_LIB_PATH = os.path.join(HERE, "build", "libpob_oracle_flops.so")
 
 
-def build(force: bool = False, count_flops: bool = False) -> str:
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def native_lib_path() -> str:
+    """-O3 -march=native build for the CPU baseline, keyed by the host CPU model (built on
+    the machine that runs it: a -march=native binary may not run on another CPU)."""
+    import hashlib
+    tag = hashlib.sha1(cpu_model().encode()).hexdigest()[:10]
+    return os.path.join(HERE, "build", f"libpob_oracle_native_{tag}.so")
+
+
+def build(force: bool = False, count_flops: bool = False, native: bool = False) -> str:
     """Compile the oracle with gcc (-ffp-contract=off keeps IEEE op order).  The
-    ``count_flops`` variant defines ORC_COUNT_FLOPS (algorithmic FLOP counter)."""
+    ``count_flops`` variant defines ORC_COUNT_FLOPS (algorithmic FLOP counter); the
+    ``native`` variant (-O3 -march=native) is the timed CPU baseline.
+    Every variant computes the same bits: explicit fmaf, no contraction, no fast-math."""
     src = os.path.join(HERE, "pob_oracle.c")
-    path = FLOPS_LIB_PATH if count_flops else LIB_PATH
+    path = native_lib_path() if native else (FLOPS_LIB_PATH if count_flops else LIB_PATH)
     if force or not os.path.exists(path) or os.path.getmtime(path) < max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(HERE, "pob_oracle.h"))):
         os.makedirs(os.path.dirname(path), exist_ok=True)
         extra = ["-DORC_COUNT_FLOPS"] if count_flops else []
+        opt = ["-O3", "-march=native"] if native else ["-O2", "-mfma"]
+        tmp = f"{path}.{os.getpid()}.tmp"
         subprocess.check_call([
-            "gcc", "-O2", "-std=c99", "-D_GNU_SOURCE", "-ffp-contract=off", "-fno-fast-math", "-mfma",
-            "-fopenmp", "-fPIC", "-shared", *extra, "-o", path, src, "-lm"])
+            "gcc", *opt, "-std=c99", "-D_GNU_SOURCE", "-ffp-contract=off", "-fno-fast-math",
+            "-fopenmp", "-fPIC", "-shared", *extra, "-o", tmp, src, "-lm"])
+        os.replace(tmp, path)
     return path
 
 
@@ -64,6 +88,7 @@ class State(C.Structure):
 
 _lib = None
 _flib = None
+_nlib = None
 
 
 def _declare(_lib):
@@ -84,6 +109,7 @@ def _declare(_lib):
         _lib.orc_randint.argtypes = [_UP, C.c_int, C.c_int]
         _lib.orc_choice_idx.argtypes = [_UP, C.c_int, C.c_int, C.POINTER(C.c_int)]
         _lib.orc_flops_read_and_reset.restype = C.c_longlong
+        _lib.orc_flops_set_mode.argtypes = [C.c_int]
         _lib.orc_math_check.argtypes = [C.c_int, C.c_int, _FP, _FP, _FP]
     return _lib
 
@@ -100,6 +126,13 @@ def flops_lib():
     if _flib is None:
         _flib = _declare(C.CDLL(build(count_flops=True)))
     return _flib
+
+
+def native_lib():
+    global _nlib
+    if _nlib is None:
+        _nlib = _declare(C.CDLL(build(native=True)))
+    return _nlib
 
 
 def _p(a, t=_FP):
@@ -125,9 +158,9 @@ def default_params(**kw) -> Params:
 class OracleEnv:
     """One env kind; state dicts of numpy arrays in the reference layout."""
 
-    def __init__(self, name: str, count_flops: bool = False, **params):
+    def __init__(self, name: str, count_flops: bool = False, native: bool = False, **params):
         self.name = name
-        self._L = flops_lib() if count_flops else lib()
+        self._L = flops_lib() if count_flops else (native_lib() if native else lib())
         self.params = default_params(**params)
         self.h = self._L.orc_env_create(KINDS[name], C.byref(self.params))
         n, d, a = C.c_int(), C.c_int(), C.c_int()
@@ -202,18 +235,29 @@ def split(key, n):
     return out
 
 
+FLOPS_REF_PAIRS, FLOPS_EXECUTED = 0, 1
+
+
 def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_EPISODE | F_AUTORESET,
-                       seed: int = 0) -> float:
+                       seed: int = 0, mode: int = FLOPS_REF_PAIRS) -> float:
     """Algorithmic FLOPs of one fused env-step (physics + POMDP + obs), counted by the
-    instrumented restatement on a random-action rollout (single-threaded)."""
+    instrumented restatement on a random-action rollout (single-threaded).
+
+    mode FLOPS_REF_PAIRS: every capsule x wall x end pair is evaluated (the reference's
+    algorithm); FLOPS_EXECUTED: only the pairs the HIP kernel evaluates after its exact
+    culls (same results).  Executed branches only in both (an inactive contact is free)."""
     import pob_np as P
     e = OracleEnv(name, count_flops=True)
     s = e.reset(P.split(P.prngkey(seed), B + 1)[1:], first=True)
     rng = np.random.default_rng(seed)
+    e._L.orc_flops_set_mode(mode)
     e._L.orc_flops_read_and_reset()
-    for _ in range(steps):
-        s = e.step(s, rng.uniform(-1, 1, (B, 8)).astype(np.float32), flags=flags, nthreads=1, inplace=True)
-    return e._L.orc_flops_read_and_reset() / float(B * steps)
+    try:
+        for _ in range(steps):
+            s = e.step(s, rng.uniform(-1, 1, (B, 8)).astype(np.float32), flags=flags, nthreads=1, inplace=True)
+        return e._L.orc_flops_read_and_reset() / float(B * steps)
+    finally:
+        e._L.orc_flops_set_mode(FLOPS_REF_PAIRS)
 
 
 def math_check(op: int, a: np.ndarray, b: np.ndarray = None) -> np.ndarray:

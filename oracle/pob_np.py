@@ -108,7 +108,11 @@ def choice_noreplace(key, a, k):
 
 
 def prngkey(seed):
-    return np.array([(seed >> 32) & 0xFFFFFFFF, seed & 0xFFFFFFFF], U32)
+    """jax.random.PRNGKey(seed), x64 off: int32 seed, high word = logical shift by 32 = 0."""
+    seed = int(seed)
+    if not -(1 << 31) <= seed < (1 << 31):
+        raise OverflowError(seed)
+    return np.array([0, seed & 0xFFFFFFFF], U32)
 
 
 # ------------------------------------------------------------ brax.jumpy numpy path

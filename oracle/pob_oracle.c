@@ -43,6 +43,11 @@
  * costs nothing), which is the algorithmic work, not the SIMT work the GPU issues. */
 #ifdef ORC_COUNT_FLOPS
 static long long g_flops = 0;
+/* 0: every capsule x wall x end pair (the reference's algorithm: brax evaluates all static
+ *    collider pairs); 1: only the pairs the HIP step kernel evaluates (per-lane xy
+ *    broadphase of pob_quad.h qdetect, and the square root / normal only when
+ *    d2 < r^2 (1 + 2^-20)) -- same results, fewer operations */
+static int g_flop_mode = 0;
 #define FL(n) (g_flops += (n))
 #else
 #define FL(n) ((void)0)
@@ -52,6 +57,13 @@ long long orc_flops_read_and_reset(void) {
   long long f = g_flops; g_flops = 0; return f;
 #else
   return -1;
+#endif
+}
+int orc_flops_set_mode(int mode) {
+#ifdef ORC_COUNT_FLOPS
+  g_flop_mode = mode; return 0;
+#else
+  (void)mode; return -1;
 #endif
 }
 
@@ -581,6 +593,54 @@ static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
   return pen;
 }
 
+#ifdef ORC_COUNT_FLOPS
+/* FLOP-count mode 1 only (no effect on any result).  The HIP kernel's per-lane broadphase
+ * (pob_quad.h qdetect, boxes from pob_system.cpp): lane k of an env holds the torso, Aux
+ * k+1 and lower leg k; it walks wall w iff the xy AABB of those three body centres meets
+ * the wall's xy box grown by the largest capsule reach (|end| + r) + 1e-3. */
+static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4]) {
+  double reach = 0.0;
+  for (int i = 0; i < NDYN; ++i)
+    for (int q = 0; q < e->cap_nend[i]; ++q) {
+      const v3 c = e->cap_end[i][q];
+      reach = fmax(reach, sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z) + e->cap_r[i]);
+    }
+  reach += 1e-3;
+  for (int k = 0; k < 4; ++k) {
+    const int l[3] = {0, 2 * k + 1, 2 * k + 2};
+    float mnx = b->x[0].x, mxx = mnx, mny = b->x[0].y, mxy = mny;
+    for (int t = 1; t < 3; ++t) {
+      mnx = fminf(mnx, b->x[l[t]].x); mxx = fmaxf(mxx, b->x[l[t]].x);
+      mny = fminf(mny, b->x[l[t]].y); mxy = fmaxf(mxy, b->x[l[t]].y);
+    }
+    mask[k] = 0u;
+    for (int w = 0; w < e->n_walls; ++w) {
+      const double c = fabs((double)e->wall_cos[w]), sn = fabs((double)e->wall_sin[w]);
+      const double ex = c * e->wall_h[w].x + sn * e->wall_h[w].y, ey = sn * e->wall_h[w].x + c * e->wall_h[w].y;
+      const float lox = (float)(e->wall_c[w].x - ex - reach), hix = (float)(e->wall_c[w].x + ex + reach);
+      const float loy = (float)(e->wall_c[w].y - ey - reach), hiy = (float)(e->wall_c[w].y + ey + reach);
+      if (mnx <= hix && mxx >= lox && mny <= hiy && mxy >= loy) mask[k] |= 1u << w;
+    }
+  }
+}
+/* operations of one broadphase-surviving sphere-box pair in the kernel (pob_quad.h
+ * qwall_end): centre offset, local frame, clamp, distance^2 always; square root, normal
+ * and its rotation only when d2 < r^2 (1 + 2^-20) (or the sphere centre is inside) */
+static long long pair_flops_executed(const orc_env *e, int w, v3 p, float r) {
+  const float c = e->wall_cos[w], s = e->wall_sin[w];
+  const v3 h = e->wall_h[w];
+  const float dx = p.x - e->wall_c[w].x, dy = p.y - e->wall_c[w].y, dz = p.z - e->wall_c[w].z;
+  const float lx = fmaf(dy, s, dx * c), ly = fmaf(dy, c, -(dx * s)), lz = dz;
+  const float ex = lx - fminf(fmaxf(lx, -h.x), h.x), ey = ly - fminf(fmaxf(ly, -h.y), h.y);
+  const float ez = lz - fminf(fmaxf(lz, -h.z), h.z);
+  const float d2 = fmaf(ez, ez, fmaf(ey, ey, ex * ex));
+  const float T = (r * r) * 1.00000095367431640625f;
+  long long f = 3 + 6 + 6 + 3 + 5;
+  if (!(d2 >= T)) f += (d2 > 0.0f ? 5 : 4) + 6;
+  return f;
+}
+#endif
+
 /* contact detection for the collide substep (ground: CapsulePlane; walls: deepest
  * sphere-box over capsule end points x walls, one contact per capsule). */
 static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
@@ -593,12 +653,27 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
     ct->n[k] = V(0.0f, 0.0f, 1.0f);
     ct->e[k] = e->ground_end[g]; ct->r[k] = e->ground_r[g]; ct->body[k] = i;
   }
+#ifdef ORC_COUNT_FLOPS
+  uint32_t lane_mask[4] = {0u, 0u, 0u, 0u};
+  if (g_flop_mode == 1) kernel_wall_masks(e, b, lane_mask);
+#endif
   for (int i = 0; i < NDYN; ++i, ++k) {
     float best = 0.0f; v3 bn = V(0, 0, 0), be = e->cap_end[i][0];
+    v3 pe[2]; /* the capsule's end points in world (independent of the wall) */
+    for (int q = 0; q < e->cap_nend[i]; ++q) pe[q] = cpoint(e->cap_end[i][q], b->q[i], b->x[i]);
     for (int w = 0; w < e->n_walls; ++w)
       for (int q = 0; q < e->cap_nend[i]; ++q) {
-        v3 pe = cpoint(e->cap_end[i][q], b->q[i], b->x[i]);
-        v3 n; float pen = sphere_box(e, w, pe, e->cap_r[i], &n);
+#ifdef ORC_COUNT_FLOPS
+        const long long f0 = g_flops;
+#endif
+        v3 n; float pen = sphere_box(e, w, pe[q], e->cap_r[i], &n);
+#ifdef ORC_COUNT_FLOPS
+        if (g_flop_mode == 1) {
+          const uint32_t m = i == 0 ? (lane_mask[0] | lane_mask[1] | lane_mask[2] | lane_mask[3])
+                                    : lane_mask[(i - 1) / 2];
+          g_flops = f0 + (((m >> w) & 1u) ? pair_flops_executed(e, w, pe[q], e->cap_r[i]) : 0);
+        }
+#endif
         if (pen > best) { best = pen; bn = n; be = e->cap_end[i][q]; }
       }
     ct->pen[k] = best; ct->n[k] = bn; ct->e[k] = be; ct->r[k] = e->cap_r[i]; ct->body[k] = i;

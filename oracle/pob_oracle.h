@@ -68,6 +68,9 @@ void orc_env_dims(const orc_env *e, int *n_bodies, int *obs_dim, int *act_dim);
 
 /* algorithmic FLOP counter (only in the -DORC_COUNT_FLOPS build; else -1) */
 long long orc_flops_read_and_reset(void);
+/* counter mode: 0 every collider pair (reference algorithm), 1 the pairs the HIP kernel
+ * evaluates (its exact culls); returns -1 when the counter is not built */
+int orc_flops_set_mode(int mode);
 /* test hook: op 0 atan2f(a, b); op 1 substep quaternion normalisation of a (n x 4) */
 void orc_math_check(int op, int n, const float *a, const float *b, float *out);
 

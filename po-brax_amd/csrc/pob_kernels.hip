@@ -1060,10 +1060,15 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
   }
 }
 
+// gym mode: this batch is rows [first, first + B) of a global batch of `total` envs (index
+// sharding over ranks, sharding.py): keys = split(gym_key, total + 1)[1 + first + b], and
+// the gym key advances to split(gym_key, total + 1)[0] when *any_flag (the GLOBAL any-done,
+// all-reduced across ranks by the caller) is set
 template <int KIND, int BS, typename QT>
 __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, const int mode,
                                               const uint32_t *__restrict__ keys, const uint32_t *gym_in,
-                                              uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s) {
+                                              uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s,
+                                              const int total, const int first) {
   __shared__ uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
   __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
   csys_t &S = *(csys_t *)(size_t)sysp;
@@ -1072,7 +1077,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     const bool any = *any_flag != 0u;
     if (b == 0 && gym_out) {
       uint32_t g0 = gym_in[0], g1 = gym_in[1];
-      if (any) tf_split(gym_in[0], gym_in[1], (uint32_t)B + 1u, 0u, g0, g1);
+      if (any) tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, 0u, g0, g1);
       gym_out[0] = g0; gym_out[1] = g1;
     }
     if (!any) return;
@@ -1082,7 +1087,8 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
   else {
     if (s.done[b] == 0.0f) return;
-    if (mode == RESET_GYM) tf_split(gym_in[0], gym_in[1], (uint32_t)B + 1u, (uint32_t)b + 1u, k0, k1);
+    if (mode == RESET_GYM)
+      tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
     else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
   }
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
@@ -1146,6 +1152,15 @@ __global__ void k_split(const uint32_t *key, int num, int first, int count, uint
   tf_split(key[0], key[1], (uint32_t)num, (uint32_t)(first + i), o0, o1);
   out[2 * i] = o0; out[2 * i + 1] = o1;
 }
+// vmap(split)(keys, num): out[b, i] = split(keys[b], num)[i]
+__global__ void k_split_batch(const uint32_t *keys, int B, int num, uint32_t *out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * num) return;
+  const int b = t / num, i = t - b * num;
+  uint32_t o0, o1;
+  tf_split(keys[2 * b], keys[2 * b + 1], (uint32_t)num, (uint32_t)i, o0, o1);
+  out[2 * t] = o0; out[2 * t + 1] = o1;
+}
 __global__ void k_uniform(const uint32_t *key, int n, int first, int count, float lo, float hi, float *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
@@ -1187,12 +1202,14 @@ static inline dim3 grid_for(int n, int bs) { return dim3((unsigned)((n + bs - 1)
 // host-side launch helpers (kind / storage dispatch)
 template <typename QT>
 static void launch_reset(int kind, dim3 g, hipStream_t st, const void *sp, int B, int mode, const uint32_t *keys,
-                         const uint32_t *gin, uint32_t *gout, const uint32_t *flag, const StatePtrs &p) {
+                         const uint32_t *gin, uint32_t *gout, const uint32_t *flag, const StatePtrs &p,
+                         int total = 0, int first = 0) {
+  if (total <= 0) total = B;
   switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
-    case POB_TAG: hipLaunchKernelGGL((k_reset<POB_TAG, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
-    default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p); break;
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
+    case POB_TAG: hipLaunchKernelGGL((k_reset<POB_TAG, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
+    default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
   }
 }
 template <typename QT>
@@ -1364,8 +1381,15 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
 
 int pob_reset_where_done(pob_env *e, int B, int mode, const uint32_t *gym_in, uint32_t *gym_out, const pob_state *s,
                          void *stream) {
+  return pob_reset_where_done_shard(e, B, B, 0, mode, gym_in, gym_out, s, stream);
+}
+
+int pob_reset_where_done_shard(pob_env *e, int B, int total, int first, int mode, const uint32_t *gym_in,
+                               uint32_t *gym_out, const pob_state *s, void *stream) {
   if (!e) return fail(POB_EINVAL, "env is NULL");
   if (B <= 0) return fail(POB_EINVAL, "batch size must be positive");
+  if (first < 0 || total < B || (long long)first + B > total || total >= INT_MAX)
+    return fail(POB_EINVAL, "shard [first, first + B) must lie in [0, total)");
   if (int rc = check_state(s, true)) return rc;
   if (mode != POB_RESET_GYM && mode != POB_RESET_OWN) return fail(POB_EINVAL, "unknown reset mode");
   if (mode == POB_RESET_GYM && (!gym_in || !gym_out)) return fail(POB_EINVAL, "gym mode needs gym_key_in/out");
@@ -1380,9 +1404,11 @@ int pob_reset_where_done(pob_env *e, int B, int mode, const uint32_t *gym_in, ui
   }
   const int kmode = mode == POB_RESET_GYM ? RESET_GYM : RESET_OWN;
   if (e->sys.qp_f16)
-    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p);
+    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
+                         first);
   else
-    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p);
+    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
+                        first);
   return hip_check(hipGetLastError(), "k_reset(where done) launch");
 }
 
@@ -1407,6 +1433,14 @@ int pob_random_split(const uint32_t *key, int num, int first, int count, uint32_
   if (count == 0) return POB_OK;
   hipLaunchKernelGGL(k_split, grid_for(count, 256), dim3(256), 0, (hipStream_t)stream, key, num, first, count, out);
   return hip_check(hipGetLastError(), "k_split launch");
+}
+
+int pob_random_split_batch(const uint32_t *keys, int B, int num, uint32_t *out, void *stream) {
+  if (!keys || !out) return fail(POB_EINVAL, "NULL argument");
+  if (B < 0 || num <= 0 || (long long)B * num >= INT_MAX) return fail(POB_EINVAL, "bad batched split shape");
+  if (B == 0) return POB_OK;
+  hipLaunchKernelGGL(k_split_batch, grid_for(B * num, 256), dim3(256), 0, (hipStream_t)stream, keys, B, num, out);
+  return hip_check(hipGetLastError(), "k_split_batch launch");
 }
 
 int pob_random_uniform(const uint32_t *key, int n, int first, int count, float lo, float hi, float *out, void *stream) {

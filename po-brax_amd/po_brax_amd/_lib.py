@@ -21,7 +21,7 @@ RESET_GYM, RESET_OWN = 0, 1
 KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 QP_F32, QP_F16 = 0, 1
 MIX_MAX = 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class pob_params(C.Structure):
@@ -54,8 +54,8 @@ class pob_state(C.Structure):
 EXPORTS = (
     "pob_abi_version", "pob_last_error", "pob_default_params", "pob_env_create",
     "pob_env_destroy", "pob_env_dims", "pob_env_default_angle", "pob_reset", "pob_step",
-    "pob_step_mixed", "pob_reset_where_done", "pob_default_qp", "pob_random_split", "pob_random_uniform",
-    "pob_random_actions", "pob_obs_gather",
+    "pob_step_mixed", "pob_reset_where_done", "pob_reset_where_done_shard", "pob_default_qp",
+    "pob_random_split", "pob_random_split_batch", "pob_random_uniform", "pob_random_actions", "pob_obs_gather",
 )
 
 
@@ -83,8 +83,11 @@ def _load():
     lib.pob_step_mixed.argtypes = [C.c_int, C.POINTER(_VP), C.POINTER(C.c_int), C.POINTER(pob_state),
                                    C.POINTER(_VP), C.POINTER(pob_state), C.c_uint32, C.c_int, _VP]
     lib.pob_reset_where_done.argtypes = [_VP, C.c_int, C.c_int, _VP, _VP, C.POINTER(pob_state), _VP]
+    lib.pob_reset_where_done_shard.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP,
+                                               C.POINTER(pob_state), _VP]
     lib.pob_default_qp.argtypes = [_VP, C.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
     lib.pob_random_split.argtypes = [_VP, C.c_int, C.c_int, C.c_int, _VP, _VP]
+    lib.pob_random_split_batch.argtypes = [_VP, C.c_int, C.c_int, _VP, _VP]
     lib.pob_random_uniform.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _VP, _VP]
     lib.pob_random_actions.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP]
     lib.pob_obs_gather.argtypes = [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP, _VP]

@@ -85,17 +85,24 @@ def create_gym_env(env_name: str,
                    seed: int = 0,
                    backend: Optional[str] = None,
                    **kwargs):
-    """Creates a gym Env / VectorEnv with gym-side autoreset (:98-121)."""
+    """Creates a gym Env / VectorEnv with gym-side autoreset (:98-121).
+
+    Engine extension: ``shard=po_brax_amd.sharding.Shard(batch_size, world, rank, group)``
+    runs this process's slice of the batch (one process per GPU) with the reference's
+    global key chain and a cross-rank any-done (sharding.py)."""
     kwargs['auto_reset'] = False
     eval_metrics = kwargs.pop('eval_metrics', False)
     discount = kwargs.pop('discount', 1.)
+    shard = kwargs.pop('shard', None)
     environment = create(env_name=env_name, batch_size=batch_size, **kwargs)
     if batch_size is None:
+        if shard is not None:
+            raise ValueError('`shard` needs a batched env (batch_size)')
         e = AutoresetGymWrapper(environment, seed=seed, backend=backend)
     else:
         if batch_size <= 0:
             raise ValueError('`batch_size` should either be None or a positive integer.')
-        e = AutoresetVmapGymWrapper(environment, batch_size, seed=seed, backend=backend)
+        e = AutoresetVmapGymWrapper(environment, batch_size, seed=seed, backend=backend, shard=shard)
     if eval_metrics:
         e = EvalGymWrapper(e, discount=discount)
     return e

@@ -274,21 +274,32 @@ class PoBraxEnv(Env):
         return s
 
     def _bufs_of(self, state: State) -> dict:
-        """Engine buffers of a State (reusing its float32 aux buffers when present)."""
+        """Engine buffers of a State.  A public field (done, metrics, truncation) whose
+        tensor is still the one this engine returned maps back onto its float32 engine
+        buffer in ``aux``; a field the caller replaced (``state.replace(done=...)``, a new
+        metrics dict entry) is converted from the public tensor instead, so brax-style
+        edits between steps are honoured."""
         a = state.aux
+        pub = a.get("pub", {})
+
+        def engine(key, public, slot):
+            t = a.get(slot)
+            if public is None:
+                return t
+            if t is not None and (public is t or public is pub.get(key)):
+                return t
+            return public.to(torch.float32).contiguous()
+
         b = dict(pos=state.qp.pos, rot=state.qp.rot, vel=state.qp.vel, ang=state.qp.ang,
                  obs=state.obs, reward=state.reward,
-                 done=a.get("done", state.done.to(torch.float32)),
+                 done=engine("done", state.done, "done"),
                  rng=state.info["rng"] if "rng" in state.info else a["rng"])
         for k in range(3):
             name = self.slot_names[k] if k < len(self.slot_names) else None
-            t = a.get(f"m{k}")
-            if t is None and name in state.metrics:
-                t = state.metrics[name].to(torch.float32).contiguous()
-            b[f"m{k}"] = t
+            b[f"m{k}"] = engine(f"m{k}", state.metrics.get(name) if name else None, f"m{k}")
         if "steps" in state.info:
             b["steps"] = state.info["steps"]
-            b["truncation"] = a.get("truncation", state.info["truncation"].to(torch.float32))
+            b["truncation"] = engine("truncation", state.info["truncation"], "truncation")
         if "first_qp" in state.info:
             fq = state.info["first_qp"]
             b.update(first_pos=fq.pos, first_rot=fq.rot, first_vel=fq.vel, first_ang=fq.ang,
@@ -324,6 +335,10 @@ class PoBraxEnv(Env):
         if "first_pos" in b:
             info["first_qp"] = QP(b["first_pos"], b["first_rot"], b["first_vel"], b["first_ang"])
             info["first_obs"] = b["first_obs"]
+        # the public tensors handed out, so _bufs_of can tell them from caller replacements
+        aux["pub"] = {"done": done, **{f"m{self.slot_names.index(n)}": t for n, t in metrics.items()}}
+        if "truncation" in info:
+            aux["pub"]["truncation"] = info["truncation"]
         st = State(QP(b["pos"], b["rot"], b["vel"], b["ang"]), b["obs"], b["reward"], done,
                    metrics, info, aux)
         if squeeze:
@@ -394,11 +409,16 @@ class PoBraxEnv(Env):
         return self._state_of(bout, True, squeeze)
 
     # helpers for the gym / randomized-autoreset wrappers
-    def _reset_where_done(self, state: State, mode: int, gym_in=None, gym_out=None) -> None:
+    def _reset_where_done(self, state: State, mode: int, gym_in=None, gym_out=None, total: int = 0,
+                          first: int = 0) -> None:
+        """Masked reset of the done envs.  ``total`` / ``first``: this batch is rows
+        [first, first + B) of a sharded global batch of ``total`` envs (gym mode keys)."""
         b = self._bufs_of(state)
         cs = self._cstate(b)
-        check(lib.pob_reset_where_done(self._handle, b["pos"].shape[0], mode, _lib.ptr(gym_in),
-                                       _lib.ptr(gym_out), C.byref(cs), _lib.stream_handle(self.device)))
+        B = b["pos"].shape[0]
+        check(lib.pob_reset_where_done_shard(self._handle, B, int(total) if total else B, int(first), mode,
+                                             _lib.ptr(gym_in), _lib.ptr(gym_out), C.byref(cs),
+                                             _lib.stream_handle(self.device)))
 
 
 # set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here

@@ -189,13 +189,23 @@ class Box:
 
 
 class VmapGymWrapper:
-    """wrappers.py:126-172: gym VectorEnv API for a batched env (device tensors in/out)."""
+    """wrappers.py:126-172: gym VectorEnv API for a batched env (device tensors in/out).
 
-    def __init__(self, env: Env, batch_size: int, seed: int = 0, backend: Optional[str] = None):
+    ``shard`` (engine extension, po_brax_amd.sharding.Shard): this process runs rows
+    [shard.lo, shard.hi) of a global batch of ``batch_size`` envs; reset keys are that
+    slice of ``split(key, batch_size + 1)[1:]`` and the gym key follows the global chain, so
+    the ranks together reproduce the single-process run bit for bit."""
+
+    def __init__(self, env: Env, batch_size: int, seed: int = 0, backend: Optional[str] = None,
+                 shard=None):
         self._env = env
         self.metadata = {"render.modes": ["human", "rgb_array"],
                          "video.frames_per_second": 1 / self._env.sys.config.dt}
-        self.num_envs = int(batch_size)
+        if shard is not None and shard.total != int(batch_size):
+            raise ValueError(f"shard.total {shard.total} != batch_size {batch_size}")
+        self._shard = shard
+        self.total_envs = int(batch_size)
+        self.num_envs = shard.size if shard is not None else int(batch_size)
         self.backend = backend
         self.device = env.unwrapped.device
         self._state = None
@@ -211,9 +221,14 @@ class VmapGymWrapper:
         self._key = jp.random_prngkey(seed, device=self.device)
 
     def _reset(self, key):
-        keys = jp.random_split(key, self.num_envs + 1)
-        state = self._env._chain_reset(keys[1:].contiguous(), False, False)
-        return state, state.obs, keys[0].contiguous()
+        if self._shard is None:
+            keys = jp.random_split(key, self.num_envs + 1)
+            state = self._env._chain_reset(keys[1:].contiguous(), False, False)
+            return state, state.obs, keys[0].contiguous()
+        num, first, count = self._shard.gym_key_rows()
+        keys = jp.random_split_rows(key, num, first, count)
+        state = self._env._chain_reset(keys, False, False)
+        return state, state.obs, jp.random_split_rows(key, num, 0, 1)[0].contiguous()
 
     def reset(self):
         self._state, obs, self._key = self._reset(self._key)
@@ -236,7 +251,9 @@ class VmapGymWrapper:
 class AutoresetVmapGymWrapper(VmapGymWrapper):
     """wrappers.py:240-262, with the ``if done.any()`` decided on the device: the step
     kernel ORs into an any-done word, the masked reset kernel re-samples the done envs from
-    ``split(gym_key, B+1)[1:]`` and advances the gym key only when something was done."""
+    ``split(gym_key, B+1)[1:]`` and advances the gym key only when something was done.
+    Sharded (``shard``), the any-done word is all-reduced (MAX) over the ranks first and the
+    keys are this rank's rows of ``split(gym_key, B_total + 1)`` (sharding.py)."""
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
@@ -244,12 +261,26 @@ class AutoresetVmapGymWrapper(VmapGymWrapper):
         self._key2 = torch.empty(2, dtype=torch.uint32, device=self.device)
 
     def step(self, action):
+        from ..sharding import all_reduce_any_done
+        self._step_local(action)
+        sh = self._shard
+        if sh is not None and sh.world > 1:
+            all_reduce_any_done(self._any, sh.group)
+        return self._autoreset()
+
+    # the two halves of step (the cross-rank any-done reduction goes between them)
+    def _step_local(self, action):
         s = self._state
         self._any.zero_()
         s.aux["any_done"] = self._any
         self._state = s = self._env._chain_step(s, action, 0, 0, True)
         s.aux["any_done"] = self._any
-        self._env.unwrapped._reset_where_done(s, _lib.RESET_GYM, self._key, self._key2)
+        return s
+
+    def _autoreset(self):
+        s, sh = self._state, self._shard
+        self._env.unwrapped._reset_where_done(s, _lib.RESET_GYM, self._key, self._key2,
+                                              total=self.total_envs, first=sh.lo if sh is not None else 0)
         self._key, self._key2 = self._key2, self._key
         return s.obs, s.reward, s.done, s.metrics
 
@@ -296,17 +327,26 @@ class AutoresetGymWrapper:
 
 
 class EvalGymWrapper:
-    """wrappers.py:175-229: episode return / discounted return / length statistics, kept as
-    device-side sums (no per-step host sync); ``get_stats`` = nanmean over completed
-    episodes, as the reference's queues seeded with NaN."""
+    """wrappers.py:175-229: episode return / discounted return / length statistics.
 
-    def __init__(self, env, discount: float = 1.0):
+    The reference appends every finished episode's return, discounted return and length to
+    the queues ``r_q``, ``dr_q``, ``l_q`` (each seeded with NaN) after a host-side
+    ``if d.any(): d.nonzero()`` per step, and ``get_stats`` is the nanmean of each queue.
+    Here the queues are device buffers filled without a host sync: the finished episodes'
+    values are scattered in env order (the order of ``d.nonzero()``) to
+    ``count + cumsum(d) - 1``, the other envs to a discard slot past the end.  The host reads
+    the device count only when the buffer might overflow (at most ``num_envs`` entries per
+    step), i.e. once per ``capacity / num_envs`` steps.  Returns are float32 like the
+    reference's ``zeros_like(obs[..., -1])`` buffers; lengths are int32."""
+
+    def __init__(self, env, discount: float = 1.0, capacity: int = 1 << 16):
         self.env = env
         self._discount = float(discount)
         self.num_envs = getattr(env, "num_envs", 1)
+        self._cap0 = int(capacity)
 
     def __getattr__(self, name):
-        if name.startswith("__"):
+        if name.startswith("__") or name in ("env", "num_envs"):
             raise AttributeError(name)
         return getattr(self.env, name)
 
@@ -314,36 +354,75 @@ class EvalGymWrapper:
         o = self.env.reset(**kwargs)
         like = torch.atleast_1d(o[..., -1])
         dev = like.device
+        n = like.shape[0]
         self.episode_returns = torch.zeros_like(like, dtype=torch.float32)
         self.discounted_episode_returns = torch.zeros_like(like, dtype=torch.float32)
-        self.episode_lengths = torch.zeros_like(like, dtype=torch.int64)
+        self.episode_lengths = torch.zeros_like(like, dtype=torch.int32)
         self.current_discount = torch.ones_like(like, dtype=torch.float32)
-        self._sum = torch.zeros(3, dtype=torch.float64, device=dev)   # return, disc. return, length
-        self._count = torch.zeros((), dtype=torch.float64, device=dev)
+        cap = max(self._cap0, 4 * n)
+        self._q = torch.zeros((3, cap + 1), dtype=torch.float32, device=dev)  # + discard slot
+        self._lq = torch.zeros(cap + 1, dtype=torch.int32, device=dev)
+        self._count = torch.zeros((), dtype=torch.int64, device=dev)
+        self._known, self._since = 0, 0  # host lower bound of the count, steps since read
         return o
+
+    def _ensure_room(self, n: int) -> None:
+        cap = self._lq.shape[0] - 1
+        if self._known + (self._since + 1) * n <= cap:
+            return
+        self._known, self._since = int(self._count), 0  # host sync (rare)
+        if self._known + n > cap:
+            new = max(2 * cap, self._known + n)
+            q = torch.zeros((3, new + 1), dtype=self._q.dtype, device=self._q.device)
+            lq = torch.zeros(new + 1, dtype=self._lq.dtype, device=self._lq.device)
+            q[:, :self._known] = self._q[:, :self._known]
+            lq[:self._known] = self._lq[:self._known]
+            self._q, self._lq = q, lq
 
     def step(self, action):
         o, r, d, info = self.env.step(action)
         r = torch.atleast_1d(r).to(torch.float32)
-        df = torch.atleast_1d(d).to(torch.float32)
+        db = torch.atleast_1d(d) != 0
+        n = db.shape[0]
         self.episode_returns += r
         self.episode_lengths += 1
         self.discounted_episode_returns += r * self.current_discount
         self.current_discount *= self._discount
-        self._sum[0] += (self.episode_returns * df).sum().double()
-        self._sum[1] += (self.discounted_episode_returns * df).sum().double()
-        self._sum[2] += (self.episode_lengths.to(torch.float32) * df).sum().double()
-        self._count += df.sum().double()
-        keep = 1.0 - df
+        self._ensure_room(n)
+        cap = self._lq.shape[0] - 1
+        slot = torch.where(db, self._count + torch.cumsum(db, 0, dtype=torch.int64) - 1,
+                           torch.full_like(self._count, cap).expand(n))
+        self._q[0].scatter_(0, slot, self.episode_returns)
+        self._q[1].scatter_(0, slot, self.discounted_episode_returns)
+        self._lq.scatter_(0, slot, self.episode_lengths)
+        self._count += db.sum()
+        self._since += 1
+        keep = ~db
         self.episode_returns *= keep
         self.discounted_episode_returns *= keep
-        self.episode_lengths *= keep.to(torch.int64)
-        self.current_discount = self.current_discount * keep + df
+        self.episode_lengths *= keep
+        self.current_discount = torch.where(db, torch.ones_like(self.current_discount), self.current_discount)
         return o, r, d, info
 
+    def _queues(self):
+        c = int(self._count)
+        return self._q[0, :c].cpu().numpy(), self._q[1, :c].cpu().numpy(), self._lq[:c].cpu().numpy()
+
+    @property
+    def r_q(self):
+        return [math.nan] + list(self._queues()[0])
+
+    @property
+    def dr_q(self):
+        return [math.nan] + list(self._queues()[1])
+
+    @property
+    def l_q(self):
+        return [math.nan] + list(self._queues()[2])
+
     def get_stats(self):
-        c = float(self._count)
-        mean = (self._sum / self._count).cpu().numpy() if c > 0 else np.full(3, math.nan)
-        return {"charts/mean_episodic_return": np.array(mean[0]),
-                "charts/mean_discounted_episodic_return": np.array(mean[1]),
-                "charts/mean_episodic_length": np.array(mean[2])}
+        r, dr, ln = self._queues()
+        mean = lambda v: np.float32(np.mean(v.astype(np.float64))) if len(v) else np.float32(np.nan)  # noqa: E731
+        return {"charts/mean_episodic_return": np.array(mean(r)),
+                "charts/mean_discounted_episodic_return": np.array(mean(dr)),
+                "charts/mean_episodic_length": np.array(mean(ln))}

@@ -14,9 +14,14 @@ from ._lib import lib, check
 
 
 def random_prngkey(seed: int, device=None) -> torch.Tensor:
-    """jax.random.PRNGKey(seed) = [seed >> 32, seed & 0xFFFFFFFF]."""
+    """jax.random.PRNGKey(seed) with jax's default 32-bit mode (x64 off): the seed is
+    converted to int32 (values outside the int32 range are rejected, as jax raises
+    OverflowError) and the key is [0, seed & 0xFFFFFFFF] -- the high word is a LOGICAL
+    shift of the 32-bit seed, so PRNGKey(-1) = [0, 4294967295]."""
     seed = int(seed)
-    k = torch.tensor([(seed >> 32) & 0xFFFFFFFF, seed & 0xFFFFFFFF], dtype=torch.uint32)
+    if not -(1 << 31) <= seed < (1 << 31):
+        raise OverflowError(f"seed {seed} does not fit in int32 (jax PRNGKey with x64 disabled)")
+    k = torch.tensor([0, seed & 0xFFFFFFFF], dtype=torch.uint32)
     return k.to(device if device is not None else "cuda")
 
 
@@ -37,16 +42,26 @@ def random_split(key: torch.Tensor, num: int = 2) -> torch.Tensor:
     return out
 
 
+def random_split_rows(key: torch.Tensor, num: int, first: int, count: int) -> torch.Tensor:
+    """Rows [first, first + count) of jax.random.split(key, num) -> (count, 2) (a shard's
+    slice of a global split, computed without the other rows)."""
+    key = _dev_key(key)
+    out = torch.empty((count, 2), dtype=torch.uint32, device=key.device)
+    check(lib.pob_random_split(key.data_ptr(), int(num), int(first), int(count), out.data_ptr(),
+                               _lib.stream_handle(key.device)))
+    return out
+
+
 def random_split_batch(keys: torch.Tensor, num: int = 2) -> torch.Tensor:
     """vmap(split)(keys): (B, 2) -> (B, num, 2)."""
     return _split_many(_dev_key(keys).reshape(-1, 2), num)
 
 
 def _split_many(keys, num):
+    keys = keys.contiguous()
     out = torch.empty((keys.shape[0], num, 2), dtype=torch.uint32, device=keys.device)
-    for i in range(keys.shape[0]):  # rare path (Cached wrapper refresh); keeps the ABI small
-        check(lib.pob_random_split(keys[i].data_ptr(), num, 0, num, out[i].data_ptr(),
-                                   _lib.stream_handle(keys.device)))
+    check(lib.pob_random_split_batch(keys.data_ptr(), keys.shape[0], num, out.data_ptr(),
+                                     _lib.stream_handle(keys.device)))
     return out
 
 

@@ -6,14 +6,23 @@ rollout is bit-identical to the single-GPU one:
 
 * reset keys:  ``split(key, B_total + 1)[1 + lo : 1 + hi]``  (VmapGymWrapper reset closure,
   wrappers.py:160-164) -- computed per rank with ``pob_random_split(first=1 + lo)``;
-* actions:     ``uniform(split(key)[1], (B_total, A), -1, 1)[lo:hi]``  (pob_random_actions).
+* actions:     ``uniform(split(key)[1], (B_total, A), -1, 1)[lo:hi]``  (pob_random_actions);
+* gym autoreset (``AutoresetVmapGymWrapper.step``, wrappers.py:245-262): the reference
+  advances ONE gym key whenever ANY env of the whole batch is done.  Sharded, each rank's
+  step kernel sets a local any-done word, ``all_reduce_any_done`` takes the MAX over
+  ranks (one 4-byte RCCL all-reduce per step, stream-ordered, no host sync), and the
+  masked reset draws rank-local rows ``split(gym_key, B_total + 1)[1 + lo + b]``
+  (``pob_reset_where_done_shard``).
 
-No collective is on the data path; ``gather_obs`` (RCCL all-gather over xGMI) assembles
-the final observation batch on every rank when a learner needs it.
+The plain brax path has no collective on the data path; ``gather_obs`` (RCCL all-gather
+over xGMI) assembles the observation batch on every rank when a learner needs it.  The
+helpers work with any torch.distributed backend ("nccl" = RCCL on ROCm; "gloo" on CPU
+tensors in the tests).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from dataclasses import dataclass
+from typing import Any, Optional, Tuple
 
 
 def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
@@ -24,6 +33,45 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     lo = rank * base + min(rank, rem)
     hi = lo + base + (1 if rank < rem else 0)
     return lo, hi
+
+
+@dataclass(frozen=True)
+class Shard:
+    """This process's slice of a global env batch (``total`` envs over ``world`` ranks)."""
+    total: int
+    world: int = 1
+    rank: int = 0
+    group: Any = None
+
+    def __post_init__(self):
+        if self.total <= 0:
+            raise ValueError("total batch must be positive")
+        shard_range(self.total, self.world, self.rank)  # validates world / rank
+
+    @property
+    def lo(self) -> int:
+        return shard_range(self.total, self.world, self.rank)[0]
+
+    @property
+    def hi(self) -> int:
+        return shard_range(self.total, self.world, self.rank)[1]
+
+    @property
+    def size(self) -> int:
+        lo, hi = shard_range(self.total, self.world, self.rank)
+        return hi - lo
+
+    def gym_key_rows(self) -> Tuple[int, int, int]:
+        """(num, first, count) of this rank's rows of split(gym_key, total + 1)."""
+        return self.total + 1, 1 + self.lo, self.size
+
+    @classmethod
+    def current(cls, total: int, group=None) -> "Shard":
+        """The shard of this process under torch.distributed (world 1 when not initialised)."""
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return cls(total, dist.get_world_size(group), dist.get_rank(group), group)
+        return cls(total)
 
 
 def shard_keys(key, total: int, world: int, rank: int):
@@ -39,6 +87,19 @@ def shard_keys(key, total: int, world: int, rank: int):
     return out
 
 
+def all_reduce_any_done(flag, group=None):
+    """In place: this rank's any-done word (``flag[0]``, uint32 0/1, written by the step
+    kernel) becomes the MAX over all ranks.  A no-op outside torch.distributed or at
+    world size 1.  4 bytes per call; on RCCL it is stream-ordered (no host sync)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return flag
+    v = flag[:1].view(torch.int32) if flag.dtype == torch.uint32 else flag[:1]
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    return flag
+
+
 def gather_obs(obs, group=None):
     """All-gather the (B_local, D) observation shards of every rank -> (B_total, D).
 
@@ -50,3 +111,17 @@ def gather_obs(obs, group=None):
     out = torch.empty((world * obs.shape[0],) + tuple(obs.shape[1:]), dtype=obs.dtype, device=obs.device)
     dist.all_gather_into_tensor(out, obs.contiguous(), group=group)
     return out
+
+
+def gather_obs_ragged(obs, total: int, group=None):
+    """gather_obs for unequal shards (shard_range of ``total``): every rank's rows padded to
+    the largest shard, gathered, and the padding dropped -> (total, D)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    m = max(hi - lo for lo, hi in (shard_range(total, world, r) for r in range(world)))
+    pad = torch.zeros((m,) + tuple(obs.shape[1:]), dtype=obs.dtype, device=obs.device)
+    pad[:obs.shape[0]] = obs
+    full = gather_obs(pad, group)
+    return torch.cat([full[r * m: r * m + (hi - lo)]
+                      for r, (lo, hi) in enumerate(shard_range(total, world, r) for r in range(world))])

@@ -52,9 +52,14 @@ def main(src, dst_prefix):
         if os.path.exists(p) and os.path.getsize(p):
             bench = json.loads(open(p).read().strip().splitlines()[-1])
         cfg = bench.get("config", {})
+        mean = lambda k: (sum(counters[k]) / len(counters[k])) if counters.get(k) else None  # noqa: E731
         traffic = {"kernel": next((r["Name"] for r in stats if "k_step" in r["Name"]), None),
-                   "env": cfg.get("env"), "batch": cfg.get("global_batch"), "qp_storage": cfg.get("qp_storage"),
+                   "env": cfg.get("env"), "batch": cfg.get("batch_per_gpu", cfg.get("global_batch")),
+                   "qp_storage": cfg.get("qp_storage"),
                    "fetch_bytes_raw": f, "write_bytes": w, "traffic_bytes": 2 * f + w,
+                   "valu_insts": mean("SQ_INSTS_VALU"), "grbm_gui_active": mean("GRBM_GUI_ACTIVE"),
+                   "waves": mean("SQ_WAVES"),
+                   "kernel_avg_ns": next((float(r["AverageNs"]) for r in stats if "k_step" in r["Name"]), None),
                    "source": os.path.basename(dst_prefix) + "_summary.md"}
         json.dump(traffic, open(dst_prefix + "_traffic.json", "w"), indent=1)
     for j in ("trace.bench.json",):

@@ -1,0 +1,140 @@
+"""GPU parity at the BASELINE.json batch sizes, on the launch paths the bench takes.
+
+``launch_step_quad`` (po-brax_amd/csrc/pob_kernels.hip) launches one-wave (64-thread)
+blocks for B <= 4096 and 256-thread blocks above that; the mixed launch is always
+256-thread blocks.  The small-batch parity tests (test_gpu_parity.py, B <= 512) all take
+the one-wave path, so this file checks, against the CPU oracle (OpenMP over envs):
+
+* the headline config: AntHeavenHell B = 65 536 (config 1 of the bench),
+* AntTag B = 65 536 (config 4's total batch on one GPU), AntGather B = 16 384 (config 3),
+* AntHeavenHell B = 4 096 (config 2, the last one-wave-block batch) and B = 4 097 (the
+  first 256-thread-block batch, ragged: its last wave holds one env),
+* the mixed launch with binary16 qp storage, HH + GA + TAG over B = 32 768 (config 5's
+  per-GPU batch),
+* a wall-stress case on the 256-thread path (ants teleported onto the arena walls).
+
+Each is reset parity plus per-step parity (the oracle restarts from the GPU's state each
+step), bit-exact on every field.  Episode length 3 makes step 3 autoreset every env.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import orc
+import pob_np as P
+from test_gpu_parity import _keys, _near_wall, _state_np, _walls, compare_states
+from test_gpu_variants import _assert_fp16_step, _state_np32
+
+pytestmark = pytest.mark.gpu
+FLAGS = orc.F_EPISODE | orc.F_AUTORESET
+NT = max(1, min(16, len(os.sched_getaffinity(0))))  # the box's CPU share is 16
+
+
+def _envs():
+    from po_brax_amd import envs
+    return envs
+
+
+def _actions(seed, B, T):
+    rng = np.random.default_rng(seed)
+    return [rng.uniform(-1, 1, (B, 8)).astype(np.float32) for _ in range(T)]
+
+
+def _per_step(name, B, T=4, L=3, seed=0):
+    env = _envs().create(name, batch_size=B, episode_length=L)
+    keys = _keys(B, seed)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name)
+    compare_states(s, o.reset(keys, first=True, nthreads=NT), f"{name} B={B} reset")
+    n_done = 0
+    for t, act in enumerate(_actions(seed + 1, B, T)):
+        so = o.step(_state_np(s), act, flags=FLAGS, episode_length=L, nthreads=NT)
+        s = env.step_(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} B={B} step {t}")
+        n_done += int(so["done"].sum())
+    assert n_done >= B  # step L autoresets every env: the first_qp / first_obs rows ran
+
+
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 65536), ("ant_tag", 65536), ("ant_gather", 16384),
+                                    ("ant_heavenhell", 4096), ("ant_heavenhell", 4097), ("ant_gather", 4097),
+                                    ("ant_tag", 4097), ("ant", 4097)])
+def test_per_step_parity_bench_sizes(name, B):
+    _per_step(name, B)
+
+
+def test_block_switch_prefix_identical():
+    """The first 4 096 envs of a B = 4 097 run (256-thread blocks) equal a B = 4 096 run
+    (one-wave blocks) bit for bit, fp32 and fp16 storage, for every kind."""
+    envs = _envs()
+    for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
+        for qp_dtype in (torch.float32, torch.float16):
+            keys = torch.from_numpy(_keys(4097, 3)).cuda()
+            ea = envs.create(name, batch_size=4096, episode_length=5, qp_dtype=qp_dtype)
+            eb = envs.create(name, batch_size=4097, episode_length=5, qp_dtype=qp_dtype)
+            sa, sb = ea.reset(keys[:4096].contiguous()), eb.reset(keys)
+            for act in _actions(7, 4097, 8):
+                a = torch.from_numpy(act).cuda()
+                sa = ea.step_(sa, a[:4096].contiguous())
+                sb = eb.step_(sb, a)
+            for f in ("pos", "rot", "vel", "ang"):
+                assert torch.equal(getattr(sa.qp, f), getattr(sb.qp, f)[:4096]), (name, qp_dtype, f)
+            assert torch.equal(sa.obs, sb.obs[:4096]), (name, qp_dtype)
+            assert torch.equal(sa.reward, sb.reward[:4096]), (name, qp_dtype)
+            assert torch.equal(sa.aux["done"], sb.aux["done"][:4096]), (name, qp_dtype)
+
+
+def test_mixed_fp16_config5_parity():
+    """BASELINE config 5 per GPU: HH + GA + TAG mixed, B = 32 768, binary16 qp storage, one
+    launch per step.  Each kind's segment against the oracle: the float32 step of the
+    decoded fp16 state, rounded to fp16, equals the GPU's fp16 qp bit for bit."""
+    envs = _envs()
+    from po_brax_amd import jumpy
+    names = ["ant_heavenhell", "ant_gather", "ant_tag"]
+    B = 32768
+    sizes = [B // 3 + (1 if i < B % 3 else 0) for i in range(3)]
+    L = 3
+    mix = envs.create_mixed(names, episode_length=L, qp_dtype=torch.float16)
+    key = jumpy.random_prngkey(0)
+    ms = mix.reset(key, sizes)
+    oes = [orc.OracleEnv(n) for n in names]
+    keys = P.split(P.prngkey(0), B + 1)[1:]
+    for n, s, o, off, b in zip(names, ms, oes, mix.offsets(), sizes):
+        ro = o.reset(keys[off:off + b], first=True, nthreads=NT)
+        for f in ("pos", "rot", "vel", "ang"):
+            np.testing.assert_array_equal(getattr(s.qp, f).cpu().numpy().view(np.uint16),
+                                          ro[f].astype(np.float16).view(np.uint16), err_msg=f"{n} reset {f}")
+        np.testing.assert_array_equal(s.obs.cpu().numpy(), ro["obs"], err_msg=f"{n} reset obs")
+    for t, act in enumerate(_actions(11, B, 4)):
+        acts = mix.split_actions(torch.from_numpy(act).cuda())
+        sos = [o.step(_state_np32(s), a.cpu().numpy(), flags=FLAGS, episode_length=L, nthreads=NT)
+               for o, s, a in zip(oes, ms, acts)]
+        ms = mix.step_(ms, [a.contiguous() for a in acts])
+        for n, s, so in zip(names, ms, sos):
+            _assert_fp16_step(s, so, f"mixed fp16 {n} step {t}")
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_tag"])
+def test_wall_stress_256_thread_blocks(name):
+    """test_gpu_parity.test_step_parity_against_walls at B = 8 192 (256-thread blocks, four
+    waves sharing the block's LDS wall rows): ants teleported onto the walls."""
+    B, T = 8192, 4
+    env = _envs().create(name, batch_size=B, episode_length=1000)
+    s = env.reset(torch.from_numpy(_keys(B, 5)).cuda())
+    walls = _walls(name)
+    ext = np.array([[abs(c[0]) + max(h), abs(c[1]) + max(h)] for c, _, h in walls]).max(0)
+    lo = np.array([-ext[0], min(c[1] - max(h) for c, _, h in walls)])
+    hi = np.array([ext[0], max(c[1] + max(h) for c, _, h in walls)])
+    rng = np.random.default_rng(9)
+    cand = rng.uniform(lo, hi, (16 * B, 2))
+    near = cand[_near_wall(cand, walls, 1.0)]
+    assert len(near) >= 3 * B // 4
+    xy = np.concatenate([near[: 3 * B // 4], cand[: B - 3 * B // 4]]).astype(np.float32)[rng.permutation(B)]
+    off = torch.from_numpy(xy - s.qp.pos[:, 0, :2].cpu().numpy()).cuda()
+    s.qp.pos[:, :9, :2] += off[:, None, :]
+    o = orc.OracleEnv(name)
+    for t, act in enumerate(_actions(13, B, T)):
+        so = o.step(_state_np(s), act, flags=FLAGS, episode_length=1000, nthreads=NT)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} wall B={B} step {t}")

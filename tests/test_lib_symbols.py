@@ -30,7 +30,8 @@ def test_lib_exports_every_declared_symbol():
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(re.findall(r" T (pob_\w+)", out))
     assert set(_declared()) <= exported
-    assert lib.pob_abi_version() == 2
+    from po_brax_amd import _lib
+    assert lib.pob_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_python_binding_covers_header():

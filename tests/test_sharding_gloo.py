@@ -84,3 +84,84 @@ def test_shard_range_covers():
             rs = [shard_range(total, world, r) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == total
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+# ---------------------------------------------------------------- sharded gym autoreset
+BG, TG, LG = 49, 9, 4  # ragged shards (25 + 24), episodes of 4 steps -> several gym resets
+
+
+def _gym_rank(rank, world, port, name, q):
+    """One rank of a sharded AutoresetVmapGymWrapper loop, with the PRODUCT's host logic
+    (po_brax_amd.sharding: Shard rows of the global gym-key split, the any-done all-reduce,
+    the ragged obs all-gather) and the CPU oracle as the per-env compute (the GPU box runs
+    the same logic over RCCL with the HIP kernels, pob_reset_where_done_shard)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "po-brax_amd"), os.path.join(root, "oracle")]
+    import orc
+    import pob_np as P
+    from po_brax_amd.sharding import Shard, all_reduce_any_done, gather_obs_ragged
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = Shard.current(BG)
+    assert (sh.world, sh.rank) == (world, rank)
+    num, first, count = sh.gym_key_rows()
+    gkey = P.prngkey(3)
+    ks = P.split(gkey, num)
+    e = orc.OracleEnv(name)
+    s = e.reset(ks[first:first + count])
+    gkey = ks[0].copy()
+    akey = P.prngkey(8)
+    any_steps = 0
+    for t in range(TG):
+        akey, k = P.split(akey)
+        act = P.uniform(k, (BG, 8), -1, 1)[sh.lo:sh.hi]
+        s = e.step(s, act, flags=orc.F_EPISODE, episode_length=LG)
+        flag = torch.tensor([1 if (s["done"] != 0).any() else 0, 0, 0, 0], dtype=torch.uint32)
+        all_reduce_any_done(flag)
+        if int(flag[0]):  # wrappers.py:247-261 on this rank's rows of the global split
+            any_steps += 1
+            ks = P.split(gkey, num)
+            gkey = ks[0].copy()
+            d = s["done"] != 0
+            if d.any():
+                fresh = e.reset(ks[first:first + count][d])
+                for f in ("pos", "rot", "vel", "ang", "obs"):
+                    s[f][d] = fresh[f]
+                s["steps"][d] = 0.0
+    obs = gather_obs_ragged(torch.from_numpy(s["obs"]), BG)
+    if rank == 0:
+        q.put((obs.numpy(), gkey, any_steps))
+    dist.destroy_process_group()
+
+
+def _gym_single(name):
+    import orc
+    import pob_np as P
+    e = orc.OracleEnv(name)
+    ks = P.split(P.prngkey(3), BG + 1)
+    s, gkey = e.reset(ks[1:]), ks[0].copy()
+    akey = P.prngkey(8)
+    for t in range(TG):
+        akey, k = P.split(akey)
+        s = e.step(s, P.uniform(k, (BG, 8), -1, 1), flags=orc.F_EPISODE, episode_length=LG)
+        e.gym_autoreset(s, gkey)
+    return s["obs"], gkey
+
+
+def test_sharded_gym_autoreset_equals_single_world2():
+    ctx = mp.get_context("spawn")
+    for name in ("ant_tag", "ant_heavenhell"):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_gym_rank, args=(r, 2, port, name, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        obs, gkey, any_steps = q.get(timeout=120)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert any_steps >= 2  # the global key advanced on several steps
+        want_obs, want_key = _gym_single(name)
+        np.testing.assert_array_equal(obs, want_obs)
+        np.testing.assert_array_equal(gkey, want_key)
