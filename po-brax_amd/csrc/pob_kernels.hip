@@ -72,7 +72,14 @@ template <> struct Q<float> {
 };
 template <> struct Q<__half> {
   static POB_D float ld(const float *p, size_t i) { return __half2float(reinterpret_cast<const __half *>(p)[i]); }
-  static POB_D void st(float *p, size_t i, float v) { reinterpret_cast<__half *>(p)[i] = __float2half_rn(v); }
+  // The float32 value is pinned in a VGPR first: otherwise the backend may fuse the
+  // producing FMA into the conversion (v_fma_mixlo_f16: ONE rounding, straight to binary16),
+  // which differs from the spec's float32 result rounded to binary16 exactly when that
+  // float32 value is a binary16 tie (measured: 11 of 393 K reset rot elements at B = 10 923)
+  static POB_D void st(float *p, size_t i, float v) {
+    asm volatile("" : "+v"(v));
+    reinterpret_cast<__half *>(p)[i] = __float2half_rn(v);
+  }
 };
 template <typename QT> POB_D v3 ld3(const float *p, size_t i) {
   return V(Q<QT>::ld(p, i), Q<QT>::ld(p, i + 1), Q<QT>::ld(p, i + 2));

@@ -336,7 +336,8 @@ class PoBraxEnv(Env):
             info["first_qp"] = QP(b["first_pos"], b["first_rot"], b["first_vel"], b["first_ang"])
             info["first_obs"] = b["first_obs"]
         # the public tensors handed out, so _bufs_of can tell them from caller replacements
-        aux["pub"] = {"done": done, **{f"m{self.slot_names.index(n)}": t for n, t in metrics.items()}}
+        aux["pub"] = {"done": done, **{f"m{self.slot_names.index(n)}": t for n, t in metrics.items()
+                                       if n in self.slot_names}}
         if "truncation" in info:
             aux["pub"]["truncation"] = info["truncation"]
         st = State(QP(b["pos"], b["rot"], b["vel"], b["ang"]), b["obs"], b["reward"], done,
