@@ -81,6 +81,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-obs", action="store_true",
                     help="RCCL all-gather of the obs batch inside every timed step (N>1)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every step from Python instead of replaying the K steps from a "
+                         "hipGraph (po_brax_amd.rollout); the gym and --gather-obs paths are always eager")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,8 +167,16 @@ def main() -> int:
             gather()
     torch.cuda.synchronize()
 
-    # timed region: K steps; events bracket the step's kernels (and, with --gather-obs, the
-    # all-gather that follows them) on torch's current stream, which the kernels use
+    use_graph = not args.no_graph and gym is None and not do_gather and pre
+    roll = None
+    if use_graph:  # capture the K timed steps (capture does not run them)
+        from po_brax_amd.rollout import GraphRollout
+        roll = GraphRollout(env, state, acts[args.warmup:args.warmup + args.steps])
+
+    # timed region: K steps.  Eager: events bracket each step's kernels (and, with
+    # --gather-obs, the all-gather after them) on torch's current stream, which the kernels
+    # use.  Graph: one replay of the K captured steps; the per-kernel time then comes from
+    # an eager pass of K more steps after the timed region.
     ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_c = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if do_gather else None
@@ -173,17 +184,26 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev_a[k].record()
-        one_step(args.warmup + k)
-        ev_b[k].record()
-        if do_gather:
-            gather()
-            ev_c[k].record()
+    if roll is not None:
+        roll.replay()
+    else:
+        for k in range(args.steps):
+            ev_a[k].record()
+            one_step(args.warmup + k)
+            ev_b[k].record()
+            if do_gather:
+                gather()
+                ev_c[k].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    if roll is not None:  # untimed: per-step kernel durations for the roofline
+        for k in range(args.steps):
+            ev_a[k].record()
+            one_step(args.warmup + k)
+            ev_b[k].record()
+        torch.cuda.synchronize()
     per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
     kern_ms = sum(per) / len(per)
     gather_ms = (sum(ev_b[k].elapsed_time(ev_c[k]) for k in range(args.steps)) / args.steps) if do_gather else None
@@ -269,7 +289,8 @@ def main() -> int:
                                + (", RCCL obs all-gather per step" if do_gather else ""),
                    "env": args.env, "global_batch": total, "batch_per_gpu": B,
                    "episode_length": args.episode_length, "qp_storage": args.qp_dtype, "parallelism": par,
-                   "path": "gym" if gym is not None else "brax"},
+                   "path": "gym" if gym is not None else "brax",
+                   "launch": "hipGraph replay of the K steps" if roll is not None else "eager per step"},
         "gpu_event_ms_per_step": round(kern_ms_max + (float(elapsed[2]) if do_gather else 0.0), 4),
         "roofline": roofline, "cpu_baseline": cpu, "obs_finite": finite,
     }
