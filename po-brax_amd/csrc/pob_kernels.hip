@@ -942,15 +942,43 @@ POB_D void fk(csys_t &S, const float (&qpos)[POB_NJ], const float (&qvel)[POB_NJ
 enum { RESET_FULL = 0, RESET_GYM = 1, RESET_OWN = 2 };
 
 // jax.random.choice(key, grid, (K,), replace=False) = first K of a stable argsort of
-// random_bits(split(key)[1], (n,)) (one shuffle round for n <= ~1600).  Per-lane
-// insertion into a sorted list kept in LDS (lane-minor, conflict-free).
+// random_bits(split(key)[1], (n,)) (one shuffle round for n <= ~1600): choice_topk_quad.
+
+// Env.reset with FOUR lanes per env (the step kernel's split, pob_quad.h): lane k of the
+// env's quad owns the torso (replica) and leg k.  A masked reset (gym / randomized
+// autoreset) typically has one done env per wave, so its cost is one env's latency: the
+// quad splits the forward kinematics (two joints per lane instead of eight), the contact
+// detection and solve (three bodies per lane) and the obs (two joints per lane).
+// Op order per value = oracle/pob_oracle.c (reset + sys.info + _get_obs).
+struct QReset {
+  QBody bd;
+  v3 cv[QNB], ca[QNB];    // sys.info(qp).contact of the local bodies (the reset obs' cfrc)
+  float jang[QNJ], jvel[QNJ];
+  float ax, ay;           // HH / TAG: ant xy offset (also shifts the Ground row)
+  float tx, ty;           // TAG target xy
+  int hh_first;           // HH: goal order of choice(rng3, hhp[:2], 2)
+  uint32_t rng0, rng1;    // new info['rng']
+};
+
+// minimum over the env's lane quad (exact and order-free; all four lanes active)
+POB_D float quad_min(float x) {
+  const float a = fminf(quad_bcast<0>(x), quad_bcast<1>(x));
+  const float b = fminf(quad_bcast<2>(x), quad_bcast<3>(x));
+  return fminf(a, b);
+}
+
+// choice_topk on an env's lane quad: lane k inserts the keys of grid indices i = k (mod 4)
+// into its own sorted list (its LDS column, stable: equal keys keep index order), then lane
+// 0 merges the four lists by (key, index) -- the first K of the stable argsort of all n
+// keys, as choice_topk -- into out[o * OS] (o = 0..K-1).
 template <int BS>
-POB_D void choice_topk(uint32_t k0, uint32_t k1, int n, int K, uint32_t *lds_key, int *lds_idx) {
+POB_D void choice_topk_quad(uint32_t k0, uint32_t k1, int n, int K, int k, uint32_t *lds_key, int *lds_idx, int *out,
+                            int OS) {
   const int t = threadIdx.x;
   uint32_t s0, s1;
   tf_split(k0, k1, 2u, 1u, s0, s1);
   int cnt = 0;
-  for (int i = 0; i < n; ++i) {
+  for (int i = k; i < n; i += 4) {
     const uint32_t key = tf_elem(s0, s1, (uint32_t)n, (uint32_t)i);
     if (cnt == K && key >= lds_key[(K - 1) * BS + t]) continue;
     int pos = cnt < K ? cnt : K - 1;
@@ -963,16 +991,39 @@ POB_D void choice_topk(uint32_t k0, uint32_t k1, int n, int K, uint32_t *lds_key
     lds_idx[pos * BS + t] = i;
     if (cnt < K) ++cnt;
   }
+  wave_lds_sync();
+  if (k == 0) {
+    int head[4], len[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      head[q] = 0;
+      const int nq = (n - q + 3) / 4;
+      len[q] = nq < K ? nq : K;
+    }
+    for (int m = 0; m < K; ++m) {
+      int best = -1;
+      uint32_t bk = 0u;
+      int bi = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (head[q] < len[q]) {
+          const uint32_t kq = lds_key[head[q] * BS + t + q];
+          const int iq = lds_idx[head[q] * BS + t + q];
+          if (best < 0 || kq < bk || (kq == bk && iq < bi)) { best = q; bk = kq; bi = iq; }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) head[q] += (q == best) ? 1 : 0;
+      out[m * OS] = bi;
+    }
+  }
+  wave_lds_sync();
 }
 
-// Env.reset for one lane.  Writes the qp rows (all N, QT storage) at r3/r4 and the obs
-// row (computed from the float32 state); returns the new info['rng'].
-template <int KIND, int BS, typename QT>
-POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *rot, float *vel, float *ang,
-                      const size_t r3, const size_t r4, float *o, uint32_t &rng0, uint32_t &rng1,
-                      uint32_t *lds_key, int *lds_idx) {
-  using QQ = Q<QT>;
-  const int N = n_bodies<KIND>(S);
+template <int KIND, int BS>
+POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const int k, uint32_t k0, uint32_t k1,
+                          QReset &R, uint32_t *lds_key, int *lds_idx) {
+  csys_t &S = *Sp;
   // random_split(rng, 5) (HH, TAG) | 4 (GA) | 3 (stock ant, brax envs/ant.py reset)
   const uint32_t ns = KIND == POB_GATHER ? 4u : (KIND == POB_ANT ? 3u : 5u);
   uint32_t r[5][2];
@@ -981,146 +1032,303 @@ POB_D void reset_lane(csys_t &S, uint32_t k0, uint32_t k1, float *pos, float *ro
     if (i < (int)ns) tf_split(k0, k1, ns, (uint32_t)i, r[i][0], r[i][1]);
     else { r[i][0] = 0u; r[i][1] = 0u; }
   }
-  float qpos[POB_NJ], qvel[POB_NJ];
+  // System.default_qp forward kinematics of this lane's leg (joints 2k, 2k + 1), the torso
+  // at the origin (oracle fk / kernel fk op order)
+  QBody &b = R.bd;
+  b.x[0] = V(0.0f, 0.0f, 0.0f);
+  b.q[0].w = 1.0f; b.q[0].x = 0.0f; b.q[0].y = 0.0f; b.q[0].z = 0.0f;
+  b.v[0] = V(0.0f, 0.0f, 0.0f); b.w[0] = V(0.0f, 0.0f, 0.0f);
 #pragma unroll
-  for (int j = 0; j < POB_NJ; ++j) {
-    qpos[j] = S.default_angle[j] + tf_uniform(r[1][0], r[1][1], 8u, (uint32_t)j, -0.1f, 0.1f);
-    qvel[j] = tf_uniform(r[2][0], r[2][1], 8u, (uint32_t)j, -0.1f, 0.1f);
+  for (int jl = 0; jl < QNJ; ++jl) {
+    const int j = 2 * k + jl, p = jparent(jl), c = jchild(jl);
+    const float qpos = S.default_angle[j] + tf_uniform(r[1][0], r[1][1], 8u, (uint32_t)j, -0.1f, 0.1f);
+    const float qvel = tf_uniform(r[2][0], r[2][1], 8u, (uint32_t)j, -0.1f, 0.1f);
+    float sn, co;
+    pob_sincosf(qpos * 0.5f, &sn, &co);
+    const v3 axis = QJV(LT, jl, QJ_AXIS);
+    q4 loc; loc.w = co; loc.x = axis.x * sn; loc.y = axis.y * sn; loc.z = axis.z * sn;
+    b.q[c] = qmul(b.q[p], loc);
+    const v3 anchor = vadd(b.x[p], qrot(QJV(LT, jl, QJ_OFFP), b.q[p]));
+    b.x[c] = vsub(anchor, qrot(QJV(LT, jl, QJ_OFFC), b.q[c]));
+    b.w[c] = vadd(b.w[p], vscl(qrot(axis, b.q[p]), qvel));
+    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
   }
-  Body bd;
-  fk(S, qpos, qvel, bd);
-  // frozen rows: default_qp values
-  const q4 qid = {1.0f, 0.0f, 0.0f, 0.0f};
-  for (int i = POB_NDYN; i < N; ++i) {
-    st3<QT>(pos, r3 + 3 * i, SV(S.frozen_pos[i]));
-    st4<QT>(rot, r4 + 4 * i, qid);
-    st3<QT>(vel, r3 + 3 * i, V(0.0f, 0.0f, 0.0f));
-    st3<QT>(ang, r3 + 3 * i, V(0.0f, 0.0f, 0.0f));
+  // lift: the lowest capsule point of the whole ant at z = 0
+  float zmin = vadd(b.x[0], qrot(qcap_end(S, LT, 0, 0), b.q[0])).z - q_cap_r(S, LT, 0);
+#pragma unroll
+  for (int l = 1; l < QNB; ++l) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float z = vadd(b.x[l], qrot(qcap_end(S, LT, l, q), b.q[l])).z - q_cap_r(S, LT, l);
+      zmin = z < zmin ? z : zmin;
+    }
   }
-  float tx = 0.0f, ty = 0.0f;  // TAG target (obs uses the float32 values)
+  zmin = quad_min(zmin);
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) b.x[l].z = b.x[l].z - zmin;
+  R.ax = 0.0f; R.ay = 0.0f; R.tx = 0.0f; R.ty = 0.0f; R.hh_first = 0;
   if (KIND == POB_HEAVENHELL) {
     // ant_heavenhell.py:87-103
-    const float ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, -0.5f, 0.5f);
-    const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, 0.5f, 1.5f);
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
-    QQ::st(pos, r3 + 27, S.frozen_pos[9][0] + ax);  // Ground is in ant_indices
-    QQ::st(pos, r3 + 28, S.frozen_pos[9][1] + ay);
+    R.ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, -0.5f, 0.5f);
+    R.ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, 0.5f, 1.5f);
     uint32_t s0, s1, y0, y1;  // choice(rng3, hhp[:2], 2, replace=False)
     tf_split(r[3][0], r[3][1], 2u, 1u, s0, s1);
     threefry2x32(s0, s1, 0u, 1u, y0, y1);
-    const int first = (y1 < y0) ? 1 : 0;
-    st3<QT>(pos, r3 + 33, V(S.hh_hhp[first][0], S.hh_hhp[first][1], 1.0f));
-    st3<QT>(pos, r3 + 36, V(S.hh_hhp[1 - first][0], S.hh_hhp[1 - first][1], 1.0f));
-    rng0 = r[0][0]; rng1 = r[0][1];
+    R.hh_first = (y1 < y0) ? 1 : 0;
+    R.rng0 = r[0][0]; R.rng1 = r[0][1];
   } else if (KIND == POB_GATHER) {
-    // ant_gather.py:109-123
-    choice_topk<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, lds_key, lds_idx);
-    for (int k = 0; k < S.n_obj; ++k) {
-      const int g = lds_idx[k * BS + threadIdx.x];
-      st3<QT>(pos, r3 + 3 * (11 + k), V(S.grid[3 * g], S.grid[3 * g + 1], k < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2]));
-    }
-    rng0 = k0; rng1 = k1;  // ant_gather.py:106 stores the input key
+    // ant_gather.py:109-123: the env's chosen grid indices go to lds_idx's env row block
+    choice_topk_quad<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, k, lds_key, lds_idx,
+                         lds_idx + POB_MAXOBJ * BS + (threadIdx.x >> 2), BS / 4);
+    R.rng0 = k0; R.rng1 = k1;  // ant_gather.py:106 stores the input key
   } else if (KIND == POB_ANT) {
-    rng0 = r[0][0]; rng1 = r[0][1];  // (not part of the stock ant's State)
+    R.rng0 = r[0][0]; R.rng1 = r[0][1];  // (not part of the stock ant's State)
   } else {
-    // ant_tag.py:63-105
+    // ant_tag.py:63-105 (all four lanes run the same rejection loop)
     const float lo0 = -S.tag_cage_xy[0], lo1 = -S.tag_cage_xy[1];
-    const float ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, lo0, S.tag_cage_xy[0]);
-    const float ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, lo1, S.tag_cage_xy[1]);
-#pragma unroll
-    for (int i = 0; i < POB_NDYN; ++i) { bd.x[i].x = bd.x[i].x + ax; bd.x[i].y = bd.x[i].y + ay; }
-    QQ::st(pos, r3 + 27, S.frozen_pos[9][0] + ax);
-    QQ::st(pos, r3 + 28, S.frozen_pos[9][1] + ay);
+    R.ax = tf_uniform(r[3][0], r[3][1], 2u, 0u, lo0, S.tag_cage_xy[0]);
+    R.ay = tf_uniform(r[3][0], r[3][1], 2u, 1u, lo1, S.tag_cage_xy[1]);
     uint32_t q0 = r[4][0], q1 = r[4][1];
-    tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
-    ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
-    for (int it = 0; it < 100000 && dist2d(tx, ty, ax, ay) <= S.tag_min_spawn_distance; ++it) {
+    float tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
+    float ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
+    for (int it = 0; it < 100000 && dist2d(tx, ty, R.ax, R.ay) <= S.tag_min_spawn_distance; ++it) {
       uint32_t n0, n1;
       tf_split(q0, q1, 2u, 1u, n0, n1);
       q0 = n0; q1 = n1;
       tx = tf_uniform(q0, q1, 2u, 0u, lo0, S.tag_cage_xy[0]);
       ty = tf_uniform(q0, q1, 2u, 1u, lo1, S.tag_cage_xy[1]);
     }
-    st3<QT>(pos, r3 + 30, V(tx, ty, 0.5f));
-    rng0 = r[0][0]; rng1 = r[0][1];
+    R.tx = tx; R.ty = ty;
+    R.rng0 = r[0][0]; R.rng1 = r[0][1];
   }
-  store_body<QT>(bd, pos, rot, vel, ang, r3, r4);
-  v3 cv[POB_NDYN], ca[POB_NDYN];
-  info_contact(&S, bd, cv, ca);
-  write_obs_common(S, N, bd, cv, ca, o, obs_shift(KIND));
-  const int base = 29 + 6 * N;
-  if (KIND == POB_HEAVENHELL) {
-    o[base] = 0.0f;  // priest_in_range = 0 at reset
-  } else if (KIND == POB_GATHER) {
-    float *rd = o + base;
-    ga_readings_begin(S, rd);
-    const float ori = ga_orientation(bd.q[0]);
-    for (int k = 0; k < S.n_obj; ++k) {
-      const int g = lds_idx[k * BS + threadIdx.x];
-      const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
-      ga_reading_one(S, k, ox, oy, dist2d(bd.x[0].x, bd.x[0].y, ox, oy), ori, rd);
+  if (KIND == POB_HEAVENHELL || KIND == POB_TAG) {
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { b.x[l].x = b.x[l].x + R.ax; b.x[l].y = b.x[l].y + R.ay; }
+  }
+  // sys.info(qp).contact: contact detection + velocity-level solve at the static qp
+  QContacts ct;
+  qdetect<KIND != POB_ANT>(Sp, LT, WT, b, ct);
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) { R.cv[l] = V(0.0f, 0.0f, 0.0f); R.ca[l] = V(0.0f, 0.0f, 0.0f); }
+  qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca);
+  // joint angle / velocity obs of this lane's joints (a3)
+#pragma unroll
+  for (int jl = 0; jl < QNJ; ++jl) {
+    const int p = jparent(jl), c = jchild(jl);
+    const v3 ap = qrot(QJV(LT, jl, QJ_AXIS), b.q[p]);
+    const v3 ref = QJV(LT, jl, QJ_REF);
+    const v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
+    R.jang[jl] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    R.jvel[jl] = vdot(vsub(b.w[c], b.w[p]), ap);
+  }
+}
+
+// Row writers: lane k writes its bodies' parts of one env row of each output array (float32
+// values; the storage conversion happens in the coalesced copy); the frozen rows are split
+// over the quad; lane 0 then writes the task rows (program order: after the frozen fill).
+enum { RROW_POS = 0, RROW_ROT = 1, RROW_VEL = 2, RROW_ANG = 3, RROW_OBS = 4 };
+template <int KIND, int BS>
+POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const int *lds_idx) {
+  const int N = n_bodies<KIND>(S);
+  const QBody &b = R.bd;
+  if (arr == RROW_POS) {
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      row[3 * g] = b.x[l].x; row[3 * g + 1] = b.x[l].y; row[3 * g + 2] = b.x[l].z;
     }
-  } else if (KIND == POB_TAG) {
-    const bool vis = dist2d(tx, ty, bd.x[0].x, bd.x[0].y) <= S.tag_visible_radius;
-    o[base] = vis ? tx : 0.0f; o[base + 1] = vis ? ty : 0.0f;
+    for (int i = POB_NDYN + k; i < N; i += 4) {
+      row[3 * i] = S.frozen_pos[i][0]; row[3 * i + 1] = S.frozen_pos[i][1]; row[3 * i + 2] = S.frozen_pos[i][2];
+    }
+    if (k == 0) {
+      if (KIND == POB_HEAVENHELL || KIND == POB_TAG) {  // Ground is in ant_indices
+        row[27] = S.frozen_pos[9][0] + R.ax; row[28] = S.frozen_pos[9][1] + R.ay;
+      }
+      if (KIND == POB_HEAVENHELL) {
+        row[33] = S.hh_hhp[R.hh_first][0]; row[34] = S.hh_hhp[R.hh_first][1]; row[35] = 1.0f;
+        row[36] = S.hh_hhp[1 - R.hh_first][0]; row[37] = S.hh_hhp[1 - R.hh_first][1]; row[38] = 1.0f;
+      } else if (KIND == POB_GATHER) {
+        for (int o = 0; o < S.n_obj; ++o) {
+          const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
+          float *d = row + 3 * (11 + o);
+          d[0] = S.grid[3 * g]; d[1] = S.grid[3 * g + 1]; d[2] = o < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
+        }
+      } else if (KIND == POB_TAG) {
+        row[30] = R.tx; row[31] = R.ty; row[32] = 0.5f;
+      }
+    }
+  } else if (arr == RROW_ROT) {
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      row[4 * g] = b.q[l].w; row[4 * g + 1] = b.q[l].x; row[4 * g + 2] = b.q[l].y; row[4 * g + 3] = b.q[l].z;
+    }
+    for (int i = POB_NDYN + k; i < N; i += 4) { row[4 * i] = 1.0f; row[4 * i + 1] = 0.0f; row[4 * i + 2] = 0.0f; row[4 * i + 3] = 0.0f; }
+  } else if (arr == RROW_VEL || arr == RROW_ANG) {
+    const v3 *v = arr == RROW_VEL ? b.v : b.w;
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      row[3 * g] = v[l].x; row[3 * g + 1] = v[l].y; row[3 * g + 2] = v[l].z;
+    }
+    for (int i = 3 * POB_NDYN + k; i < 3 * N; i += 4) row[i] = 0.0f;
+  } else {
+    const int sh = obs_shift(KIND);
+#pragma unroll
+    for (int jl = 0; jl < QNJ; ++jl) {
+      row[sh + 7 + 2 * k + jl] = R.jang[jl];
+      row[sh + 21 + 2 * k + jl] = R.jvel[jl];
+    }
+    float *oc = row + (29 + sh);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      const int g = qbody_global(l, k);
+      oc[3 * g] = clip1(R.cv[l].x); oc[1 + 3 * g] = clip1(R.cv[l].y); oc[2 + 3 * g] = clip1(R.cv[l].z);
+      oc[3 * N + 3 * g] = clip1(R.ca[l].x); oc[1 + 3 * N + 3 * g] = clip1(R.ca[l].y); oc[2 + 3 * N + 3 * g] = clip1(R.ca[l].z);
+    }
+    for (int q = 3 * POB_NDYN + k; q < 3 * N; q += 4) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+    if (k == 0) {
+      if (sh == 0) { row[0] = b.x[0].x; row[1] = b.x[0].y; }
+      row[sh + 2] = b.x[0].z;
+      row[sh + 3] = b.q[0].w; row[sh + 4] = b.q[0].x; row[sh + 5] = b.q[0].y; row[sh + 6] = b.q[0].z;
+      row[sh + 15] = b.v[0].x; row[sh + 16] = b.v[0].y; row[sh + 17] = b.v[0].z;
+      row[sh + 18] = b.w[0].x; row[sh + 19] = b.w[0].y; row[sh + 20] = b.w[0].z;
+      const int base = 29 + 6 * N;
+      if (KIND == POB_HEAVENHELL) {
+        row[base] = 0.0f;  // priest_in_range = 0 at reset
+      } else if (KIND == POB_GATHER) {
+        float *rd = row + base;
+        ga_readings_begin(S, rd);
+        const float ori = ga_orientation(b.q[0]);
+        for (int o = 0; o < S.n_obj; ++o) {
+          const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
+          const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
+          ga_reading_one(S, o, ox, oy, dist2d(b.x[0].x, b.x[0].y, ox, oy), ori, rd);
+        }
+      } else if (KIND == POB_TAG) {
+        const bool vis = dist2d(R.tx, R.ty, b.x[0].x, b.x[0].y) <= S.tag_visible_radius;
+        row[base] = vis ? R.tx : 0.0f; row[base + 1] = vis ? R.ty : 0.0f;
+      }
+    }
+  }
+}
+
+// Coalesced store of staged rows (row r of W elements at stg + r * WP) to
+// X[(b0 + r) * W ...] (and FX, when given) for the rows whose bit is set in `rows`.
+template <typename QT>
+POB_D void reset_store_rows(float *X, float *FX, const size_t b0, const int W, const int nrows, const int WP,
+                            const float *stg, const uint32_t rows, const int lane) {
+  int r = 0, e = lane;
+  while (e >= W) { e -= W; ++r; }
+  for (int i = lane; i < nrows * W; i += 64) {
+    if ((rows >> r) & 1u) {
+      const float v = stg[r * WP + e];
+      Q<QT>::st(X, b0 * W + i, v);
+      if (FX) Q<QT>::st(FX, b0 * W + i, v);
+    }
+    e += 64;
+    while (e >= W) { e -= W; ++r; }
   }
 }
 
 // gym mode: this batch is rows [first, first + B) of a global batch of `total` envs (index
 // sharding over ranks, sharding.py): keys = split(gym_key, total + 1)[1 + first + b], and
 // the gym key advances to split(gym_key, total + 1)[0] when *any_flag (the GLOBAL any-done,
-// all-reduced across ranks by the caller) is set
+// all-reduced across ranks by the caller) is set.
+// One wave per block = 16 envs x 4 lanes.  Every env's reset is computed in registers by
+// its quad, then each output array is staged row by row in LDS (16 rows of WP floats,
+// dynamic shared memory) and stored coalesced -- to the state and, in a full reset, to
+// first_qp / first_obs at the same time (no read-back).  Masked modes store only the rows
+// of done envs; a wave without one exits at once.
 template <int KIND, int BS, typename QT>
 __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, const int mode,
                                               const uint32_t *__restrict__ keys, const uint32_t *gym_in,
                                               uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s,
-                                              const int total, const int first) {
+                                              const int total, const int first, const int WP) {
+  static_assert(BS == 64, "k_reset stages one wave's rows per block");
   __shared__ uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
-  __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
-  csys_t &S = *(csys_t *)(size_t)sysp;
-  const int b = blockIdx.x * BS + threadIdx.x;
+  // per-lane sorted lists, then the merged choice per env (POB_MAXOBJ x 16 envs)
+  __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS + POB_MAXOBJ * (BS / 4) : 1];
+  __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
+  extern __shared__ float stg[];  // 16 rows of WP floats
+  csys_t *Sp = (csys_t *)(size_t)sysp;
+  csys_t &S = *Sp;
+  const int lane = (int)threadIdx.x;
+  const int k = lane & 3;
+  const int e0 = (int)blockIdx.x * (BS / 4);  // first env of this wave
+  const int b = e0 + (lane >> 2);
   if (mode == RESET_GYM) {
     const bool any = *any_flag != 0u;
-    if (b == 0 && gym_out) {
+    if (b == 0 && k == 0 && gym_out) {
       uint32_t g0 = gym_in[0], g1 = gym_in[1];
       if (any) tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, 0u, g0, g1);
       gym_out[0] = g0; gym_out[1] = g1;
     }
-    if (!any) return;
+    if (!any) return;  // block-uniform
   }
-  if (b >= B) return;
-  uint32_t k0, k1;
-  if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
-  else {
-    if (s.done[b] == 0.0f) return;
-    if (mode == RESET_GYM)
-      tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
-    else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
+  bool active = b < B;
+  uint32_t k0 = 0u, k1 = 0u;
+  if (active) {
+    if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
+    else {
+      active = s.done[b] != 0.0f;
+      if (mode == RESET_GYM)
+        tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
+      else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
+    }
   }
+  const uint64_t lanes = __ballot(active && k == 0);
+  if (lanes == 0ull) return;  // block-uniform (a masked reset with no done env in this wave)
+  uint32_t rows = 0u;  // bit e: env e0 + e is reset
+#pragma unroll
+  for (int e = 0; e < 16; ++e) rows |= (uint32_t)((lanes >> (4 * e)) & 1ull) << e;
+  stage_leg_table(Sp, legtab);
+  const float *LT = legtab + k * POB_LEG_FLOATS;
+  const float *WT = legtab + 4 * POB_LEG_FLOATS;
+  QReset R;
+  if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx);
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
-  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
-  uint32_t rng0, rng1;
-  reset_lane<KIND, BS, QT>(S, k0, k1, s.pos, s.rot, s.vel, s.ang, r3, r4, s.obs + (size_t)b * D, rng0, rng1,
-                           lds_key, lds_idx);
+  const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
+  const bool full = mode == RESET_FULL && s.first_pos;
+  float *myrow = stg + (lane >> 2) * WP;
+#pragma unroll 1
+  for (int arr = 0; arr < 5; ++arr) {
+    const int W = arr == RROW_OBS ? D : (arr == RROW_ROT ? 4 * N : 3 * N);
+    float *X = arr == RROW_POS ? s.pos : (arr == RROW_ROT ? s.rot : (arr == RROW_VEL ? s.vel : (arr == RROW_ANG ? s.ang : s.obs)));
+    float *FX = !full ? nullptr
+                      : (arr == RROW_POS ? s.first_pos
+                                         : (arr == RROW_ROT ? s.first_rot
+                                                            : (arr == RROW_VEL ? s.first_vel
+                                                                               : (arr == RROW_ANG ? s.first_ang : s.first_obs))));
+    if (active) qreset_row<KIND, BS>(S, R, k, arr, myrow, lds_idx);
+    wave_lds_sync();
+    if (arr == RROW_OBS) reset_store_rows<float>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
+    else reset_store_rows<QT>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
+    wave_lds_sync();
+  }
+  if (!active || k != 0) return;
   if (mode == RESET_FULL) {
-    s.rng[2 * b] = rng0; s.rng[2 * b + 1] = rng1;
+    s.rng[2 * b] = R.rng0; s.rng[2 * b + 1] = R.rng1;
     s.reward[b] = 0.0f; s.done[b] = 0.0f;
     if (s.steps) s.steps[b] = 0.0f;
     if (s.truncation) s.truncation[b] = 0.0f;
     if (s.m0) s.m0[b] = 0.0f;
     if (s.m1) s.m1[b] = 0.0f;
     if (s.m2) s.m2[b] = 0.0f;
-    if (s.first_pos) {
-      cpq<QT>(s.first_pos, s.pos, r3, 3 * N);
-      cpq<QT>(s.first_vel, s.vel, r3, 3 * N);
-      cpq<QT>(s.first_ang, s.ang, r3, 3 * N);
-      cpq<QT>(s.first_rot, s.rot, r4, 4 * N);
-      for (int k = 0; k < D; ++k) s.first_obs[(size_t)b * D + k] = s.obs[(size_t)b * D + k];
-    }
   } else if (mode == RESET_GYM) {
     if (s.steps) s.steps[b] = 0.0f;
   }
+}
+
+// LDS row pitch of k_reset's staging area: the widest row (obs or rot), odd so that the
+// envs' rows start in distinct banks
+static int reset_pitch(const pob_sys &S) {
+  const int w = S.D > 4 * S.N ? S.D : 4 * S.N;
+  return w | 1;
 }
 
 __global__ void k_any_done(const float *done, int B, uint32_t *flag) {
@@ -1208,15 +1416,17 @@ static inline dim3 grid_for(int n, int bs) { return dim3((unsigned)((n + bs - 1)
 
 // host-side launch helpers (kind / storage dispatch)
 template <typename QT>
-static void launch_reset(int kind, dim3 g, hipStream_t st, const void *sp, int B, int mode, const uint32_t *keys,
-                         const uint32_t *gin, uint32_t *gout, const uint32_t *flag, const StatePtrs &p,
-                         int total = 0, int first = 0) {
+static void launch_reset(const pob_sys &S, dim3 g, hipStream_t st, const void *sp, int B, int mode,
+                         const uint32_t *keys, const uint32_t *gin, uint32_t *gout, const uint32_t *flag,
+                         const StatePtrs &p, int total = 0, int first = 0) {
   if (total <= 0) total = B;
-  switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
-    case POB_TAG: hipLaunchKernelGGL((k_reset<POB_TAG, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
-    default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), 0, st, sp, B, mode, keys, gin, gout, flag, p, total, first); break;
+  const int WP = reset_pitch(S);
+  const size_t shm = sizeof(float) * 16 * (size_t)WP;  // 16 envs per block
+  switch (S.kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_reset<POB_HEAVENHELL, 64, QT>), g, dim3(64), shm, st, sp, B, mode, keys, gin, gout, flag, p, total, first, WP); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_reset<POB_GATHER, 64, QT>), g, dim3(64), shm, st, sp, B, mode, keys, gin, gout, flag, p, total, first, WP); break;
+    case POB_TAG: hipLaunchKernelGGL((k_reset<POB_TAG, 64, QT>), g, dim3(64), shm, st, sp, B, mode, keys, gin, gout, flag, p, total, first, WP); break;
+    default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), shm, st, sp, B, mode, keys, gin, gout, flag, p, total, first, WP); break;
   }
 }
 template <typename QT>
@@ -1313,9 +1523,9 @@ int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, voi
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs p = to_ptrs(*out);
   if (e->sys.qp_f16)
-    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
+    launch_reset<__half>(e->sys, grid_for(B, 16), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
   else
-    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
+    launch_reset<float>(e->sys, grid_for(B, 16), st, e->d_sys, B, RESET_FULL, keys, nullptr, nullptr, nullptr, p);
   return hip_check(hipGetLastError(), "k_reset launch");
 }
 
@@ -1411,10 +1621,10 @@ int pob_reset_where_done_shard(pob_env *e, int B, int total, int first, int mode
   }
   const int kmode = mode == POB_RESET_GYM ? RESET_GYM : RESET_OWN;
   if (e->sys.qp_f16)
-    launch_reset<__half>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
+    launch_reset<__half>(e->sys, grid_for(B, 16), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
                          first);
   else
-    launch_reset<float>(e->sys.kind, grid_for(B, 64), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
+    launch_reset<float>(e->sys, grid_for(B, 16), st, e->d_sys, B, kmode, nullptr, gym_in, gym_out, flag, p, total,
                         first);
   return hip_check(hipGetLastError(), "k_reset(where done) launch");
 }
