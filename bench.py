@@ -81,6 +81,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-obs", action="store_true",
                     help="RCCL all-gather of the obs batch inside every timed step (N>1)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N>1 ('nccl' = RCCL; 'gloo' lets several ranks share "
+                         "one GPU for a functional rehearsal, not a measurement)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
                          "hipGraph (po_brax_amd.rollout); the gym and --gather-obs paths are always eager")
@@ -91,11 +94,12 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        kw = dict(device_id=dev) if args.dist_backend == "nccl" else {}
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
     if args.gym and args.env == "mixed":
         ap.error("--gym runs one env kind")
 
@@ -207,7 +211,8 @@ def main() -> int:
     per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
     kern_ms = sum(per) / len(per)
     gather_ms = (sum(ev_b[k].elapsed_time(ev_c[k]) for k in range(args.steps)) / args.steps) if do_gather else None
-    elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64,
+                           device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     wall, kern_ms_max = float(elapsed[0]), float(elapsed[1])
