@@ -187,9 +187,12 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     if roll is not None:
+        g0.record()
         roll.replay()
+        g1.record()
     else:
         for k in range(args.steps):
             ev_a[k].record()
@@ -209,7 +212,11 @@ def main() -> int:
             ev_b[k].record()
         torch.cuda.synchronize()
     per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
-    kern_ms = sum(per) / len(per)
+    eager_ms = sum(per) / len(per)
+    # the dominant kernel's time per launch: from the graph replay (back-to-back launches, no
+    # host gaps) when there is one -- an eager step's event pair also holds the host's launch
+    # time whenever the kernel is shorter than it (small batches)
+    kern_ms = g0.elapsed_time(g1) / args.steps if roll is not None else eager_ms
     gather_ms = (sum(ev_b[k].elapsed_time(ev_c[k]) for k in range(args.steps)) / args.steps) if do_gather else None
     elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64,
                            device=dev if args.dist_backend == "nccl" else "cpu")
@@ -248,6 +255,9 @@ def main() -> int:
         "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
         "kernel": kname + (" + gym any-done + k_reset(where done)" if gym is not None else ""),
         "kernel_ms": round(kern_ms, 4), "units_per_launch": B,
+        "kernel_ms_source": "hipGraph replay of the K timed steps / K" if roll is not None
+                            else "HIP events around each eager step",
+        "eager_event_ms": round(eager_ms, 4),
         "flops_per_env_step": round(f_ref, 1),
         "flops_basis": "instrumented CPU restatement (oracle/pob_oracle.c, ORC_COUNT_FLOPS), executed branches, "
                        "every capsule x wall x end pair evaluated as in the reference (brax evaluates all pairs)",

@@ -1,18 +1,28 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, then bench lines for the BASELINE.json configs.
-# Every GPU step has its own time limit; the chain stops at the first failure.
+# One GPU-box pass: parity tests, then bench lines for the BASELINE.json configs (and the
+# gym path), all into gpurun_out/$TAG/.  Every GPU step has its own time limit; the chain
+# stops at the first failure.   TAG=r2h bash scripts/gpu_check.sh [--no-tests]
 set -o pipefail
-mkdir -p gpurun_out
+TAG=${TAG:-check}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -s > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || exit 1
-cat gpurun_out/bench_default.json
-timeout -k 10 200 python bench.py --env mixed --batch 32768 --qp-dtype f16 --no-cpu-baseline > gpurun_out/bench_mixed_f16.json || exit 1
-timeout -k 10 200 python bench.py --env mixed --batch 32768 --no-cpu-baseline > gpurun_out/bench_mixed_f32.json || exit 1
-timeout -k 10 200 python bench.py --env ant_heavenhell --batch 65536 --qp-dtype f16 --no-cpu-baseline > gpurun_out/bench_hh_f16.json || exit 1
-timeout -k 10 200 python bench.py --env ant_heavenhell --batch 4096 --no-cpu-baseline > gpurun_out/bench_hh_4096.json || exit 1
-timeout -k 10 200 python bench.py --env ant_gather --batch 16384 --no-cpu-baseline > gpurun_out/bench_ga_16384.json || exit 1
-timeout -k 10 200 python bench.py --env ant_tag --batch 65536 --no-cpu-baseline > gpurun_out/bench_tag_65536.json || exit 1
-timeout -k 10 200 python bench.py --env ant --batch 65536 --no-cpu-baseline > gpurun_out/bench_ant_65536.json || exit 1
-for f in gpurun_out/bench_*.json; do python -c "import json,sys; d=json.load(open('$f')); print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'])"; done
+if [ "${1:-}" != "--no-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { grep -E "^E |FAILED" $OUT/pytest_gpu.log | head -30; exit 1; }
+  tail -2 $OUT/pytest_gpu.log
+fi
+timeout -k 10 300 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || exit 1
+run() {  # name, bench args...
+  local name=$1; shift
+  timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err || exit 1
+}
+run hh_4096 --batch 4096 &&
+run ga_16384 --env ant_gather --batch 16384 &&
+run tag_65536 --env ant_tag --batch 65536 &&
+run mixed_f16_32768 --env mixed --qp-dtype f16 --batch 32768 &&
+run mixed_f32_32768 --env mixed --batch 32768 &&
+run hh_f16 --qp-dtype f16 &&
+run ant_65536 --env ant --batch 65536 &&
+run gym_hh --gym &&
+run hh_steady --steps 1000 --warmup 50 || exit 1
+for f in $OUT/bench_*.json; do python -c "import json,sys; d=json.load(open('$f')); r=d['roofline']; print('$f', d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'])"; done
