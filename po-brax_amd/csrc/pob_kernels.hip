@@ -23,6 +23,7 @@
 
 #include "../../include/pob.h"
 #include "pob_quad.h"
+#include "pob_octet.h"
 #include "pob_physics.h"
 
 namespace pob {
@@ -905,6 +906,257 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_mixed(const Mi
                                 (bx - blk0) * 256 + (int)threadIdx.x, lds, legtab);
 }
 
+// ------------------------------------------------------------------ step, lane octets
+// The same fused step with EIGHT lanes per env (pob_octet.h) for small batches: one wave =
+// 8 envs, one wave per block.  Lane m of an env: A_m (m < 4: hip joint m, torso + Aux) or
+// B_(7-m) (m >= 4: knee joint, Aux + lower leg).  Lane A_0 runs the per-env POMDP tail.
+#define POB_OSTAGE_FLOATS (OL_FLOATS * 64)
+template <int KIND, typename QT>
+__global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, const StatePtrs in,
+                                                 const float *__restrict__ act, const StatePtrs out,
+                                                 const uint32_t flags, const int L) {
+  static_assert(KIND != POB_MIXED, "the eight-lane kernel runs one env kind per launch");
+  __shared__ float stg[POB_OSTAGE_FLOATS];
+  __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS];
+  csys_t *Sp = (csys_t *)(size_t)sysp;
+  {
+    const __attribute__((address_space(4))) float *src = &Sp->oct[0][0];
+    for (int i = (int)threadIdx.x; i < 8 * OT_FLOATS; i += 64) otab[i] = src[i];
+    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
+    for (int i = (int)threadIdx.x; i < POB_MAXW * POB_WALL_FLOATS; i += 64) otab[8 * OT_FLOATS + i] = wsrc[i];
+    __syncthreads();
+  }
+  csys_t &S = *Sp;
+  const int lane = (int)threadIdx.x;
+  const int m = lane & 7;
+  const bool isA = m < 4;
+  const int k = isA ? m : 7 - m;              // the leg
+  const int jown = isA ? 2 * k : 2 * k + 1;    // the lane's joint
+  const int g0 = isA ? 0 : 2 * k + 1, g1 = isA ? 2 * k + 1 : 2 * k + 2;  // its slots' bodies
+  const float *OT = otab + (isA ? k : 4 + k) * OT_FLOATS;
+  const float *WT = otab + 8 * OT_FLOATS;
+  const Lds Ls{stg, 64, lane};
+  const int b_first = (int)blockIdx.x * 8;
+  const int b = b_first + (lane >> 3);
+  const int nenv = B - b_first < 8 ? B - b_first : 8;
+  const int le = lane >> 3;
+  const bool act_lane = b < B;
+  const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+  constexpr int sh = obs_shift(KIND);
+  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  const bool lane0 = m == 0;  // A_0: the env's POMDP tail
+
+  // ---- state load: coalesced loads of the 8 envs' rows into LDS (pairs of arrays), then
+  // every lane picks its two bodies; per-lane loads when the qp pointers are not aligned
+  OBody bd;
+  constexpr int NMAX = KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : (KIND == POB_ANT ? 10 : POB_MAXB));
+  if ((flags & POB_F_STAGED) && 8 * N * 7 <= POB_OSTAGE_FLOATS) {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int c0 = 3, c1 = pr == 0 ? 4 : 3;
+      const int n0 = nenv * N * c0, n1 = nenv * N * c1;
+      stage_load<QT>(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, stg, lane);
+      stage_load<QT>(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, stg + n0, lane);
+      wave_lds_sync();
+      if (act_lane) {
+#pragma unroll
+        for (int sl = 0; sl < ONB; ++sl) {
+          const int g = sl == 0 ? g0 : g1;
+          const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
+          if (pr == 0) {
+            bd.x[sl] = V(s0[0], s0[1], s0[2]);
+            bd.q[sl].w = s1[0]; bd.q[sl].x = s1[1]; bd.q[sl].y = s1[2]; bd.q[sl].z = s1[3];
+          } else {
+            bd.v[sl] = V(s0[0], s0[1], s0[2]);
+            bd.w[sl] = V(s1[0], s1[1], s1[2]);
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  } else if (act_lane) {
+#pragma unroll
+    for (int sl = 0; sl < ONB; ++sl) {
+      const int g = sl == 0 ? g0 : g1;
+      bd.x[sl] = ld3<QT>(in.pos, r3 + 3 * g);
+      bd.q[sl] = ld4<QT>(in.rot, r4 + 4 * g);
+      bd.v[sl] = ld3<QT>(in.vel, r3 + 3 * g);
+      bd.w[sl] = ld3<QT>(in.ang, r3 + 3 * g);
+    }
+  }
+  (void)NMAX;
+
+  // ---- physics (10 substeps in registers + the lane's LDS slots)
+  float jang = 0.0f, jvel = 0.0f;
+  v3 cvl[ONB], cal[ONB];
+  TaskOut t;
+  if (act_lane) {
+    const float xb = bd.x[0].x;
+    const float a = act[(size_t)b * POB_NJ + jown];
+#pragma unroll
+    for (int sl = 0; sl < ONB; ++sl) { Ls.set3(OL_CV(sl), V(0.0f, 0.0f, 0.0f)); Ls.set3(OL_CA(sl), V(0.0f, 0.0f, 0.0f)); }
+    const int iters = Sp->substeps / 2;
+#pragma nounroll
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, Ls, (it & 1) != 0);
+    {  // joint angle / velocity obs of the lane's joint (a3)
+      const v3 ap = qrot(OTV(OT, OT_AXIS), bd.q[0]);
+      const v3 ref = OTV(OT, OT_REF);
+      const v3 fp = qrot(ref, bd.q[0]), fc = qrot(ref, bd.q[1]);
+      jang = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      jvel = vdot(vsub(bd.w[1], bd.w[0]), ap);
+    }
+#pragma unroll
+    for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = Ls.get3(OL_CV(sl)); cal[sl] = Ls.get3(OL_CA(sl)); }
+    if (lane0) {
+      float steps = in.steps ? in.steps[b] : 0.0f;
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
+      t.steps = steps;
+      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+      t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
+      if (KIND == POB_ANT) {
+        // full action row; contact rows 0..8 = torso, then Aux k (lane A_k slot 1) and lower
+        // leg k (lane B_k slot 1) for k = 0..3
+        t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
+        float sc = ant_contact_add(0.0f, cvl[0]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sc = ant_contact_add(sc, Ls.get3_lane(OL_CV(1), lane + q));
+          sc = ant_contact_add(sc, Ls.get3_lane(OL_CV(1), lane + 7 - q));
+        }
+        t.contact = 0.0005f * sc;
+      }
+    }
+  }
+  wave_lds_sync();  // every LDS read of the physics slots is done: the region is staging now
+
+  // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
+  float done = 0.0f;
+  t.ga_done_quad = false;
+  const bool ga_quad = KIND == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
+  GaQuad gq;
+  if (ga_quad && act_lane && isA) ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
+  const int P = POB_OSTAGE_FLOATS / D < 8 ? POB_OSTAGE_FLOATS / D : 8;
+  for (int p0 = 0; p0 < nenv; p0 += P) {
+    const int pn = nenv - p0 < P ? nenv - p0 : P;
+    if (act_lane && le >= p0 && le < p0 + pn) {
+      float *o = stg + (le - p0) * D;
+      o[sh + 7 + jown] = jang;
+      o[sh + 21 + jown] = jvel;
+      // cfrc rows: A_0 the torso, A_k Aux k (slot 1), B_k lower leg k (slot 1); the frozen
+      // bodies' zero rows split over the eight lanes
+      float *oc = o + (29 + sh);
+      if (lane0) {
+        oc[0] = clip1(cvl[0].x); oc[1] = clip1(cvl[0].y); oc[2] = clip1(cvl[0].z);
+        oc[3 * N] = clip1(cal[0].x); oc[1 + 3 * N] = clip1(cal[0].y); oc[2 + 3 * N] = clip1(cal[0].z);
+      }
+      oc[3 * g1] = clip1(cvl[1].x); oc[1 + 3 * g1] = clip1(cvl[1].y); oc[2 + 3 * g1] = clip1(cvl[1].z);
+      oc[3 * N + 3 * g1] = clip1(cal[1].x); oc[1 + 3 * N + 3 * g1] = clip1(cal[1].y);
+      oc[2 + 3 * N + 3 * g1] = clip1(cal[1].z);
+      for (int q = 3 * POB_NDYN + m; q < 3 * N; q += 8) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+      if (lane0) {
+        if (sh == 0) { o[0] = bd.x[0].x; o[1] = bd.x[0].y; }
+        o[sh + 2] = bd.x[0].z;
+        o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
+        o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
+        o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
+        if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
+          for (int i = POB_NDYN; i < N; ++i) {
+            if (!(ga_quad && i >= 11)) cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+            cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+            cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+            cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
+          }
+        }
+      }
+      if (ga_quad && isA) ga_quad_scatter(S, gq, k, o + 29 + 6 * N);
+      if (lane0) {
+        task_step<KIND, QT>(S, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
+        done = t.done;
+      }
+      {  // the env's done to all eight lanes: A quad from A_0, B quad via A_0 -> B_0 (lane 7)
+        const float d1 = quad_bcast<0>(done);
+        const float d2 = quad_bcast<3>(oct_swap(d1));
+        done = isA ? d1 : d2;
+      }
+      // AutoResetWrapper: the row of a reset env is first_obs (written last)
+      if (lane0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+        wave_lds_sync();
+        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+      }
+    }
+    wave_lds_sync();
+    float *dst = out.obs + (size_t)(b_first + p0) * D;
+    const int n = pn * D;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      const int n4 = n >> 2;
+      for (int i = lane; i < n4; i += 64) reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(stg)[i];
+      for (int i = 4 * n4 + lane; i < n; i += 64) dst[i] = stg[i];
+    } else {
+      for (int i = lane; i < n; i += 64) dst[i] = stg[i];
+    }
+    wave_lds_sync();
+  }
+
+  // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
+  const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#pragma unroll
+  for (int arr = 0; arr < 4; ++arr) {
+    const int c = arr == 1 ? 4 : 3;
+    if (act_lane) {
+#pragma unroll
+      for (int sl = 0; sl < ONB; ++sl) {
+        if (sl == 0 && !lane0) continue;  // slot 0: the torso (A_0) or an Aux replica
+        const int g = sl == 0 ? g0 : g1;
+        float *o = stg + (le * POB_NDYN + g) * c;
+        if (reset_rows) {
+          const float *F = arr == 0 ? in.first_pos : (arr == 1 ? in.first_rot : (arr == 2 ? in.first_vel : in.first_ang));
+          const size_t src = (arr == 1 ? r4 : r3) + (size_t)g * c;
+          for (int q = 0; q < c; ++q) o[q] = Q<QT>::ld(F, src + q);
+        } else if (arr == 0) { o[0] = bd.x[sl].x; o[1] = bd.x[sl].y; o[2] = bd.x[sl].z; }
+        else if (arr == 1) { o[0] = bd.q[sl].w; o[1] = bd.q[sl].x; o[2] = bd.q[sl].y; o[3] = bd.q[sl].z; }
+        else if (arr == 2) { o[0] = bd.v[sl].x; o[1] = bd.v[sl].y; o[2] = bd.v[sl].z; }
+        else { o[0] = bd.w[sl].x; o[1] = bd.w[sl].y; o[2] = bd.w[sl].z; }
+      }
+    }
+    wave_lds_sync();
+    if (arr == 1) stage_store_dyn<QT, 4>(out.rot, (size_t)b_first * N * 4, N, nenv, stg, lane);
+    else stage_store_dyn<QT, 3>(arr == 0 ? out.pos : (arr == 2 ? out.vel : out.ang), (size_t)b_first * N * 3, N, nenv,
+                                stg, lane);
+    wave_lds_sync();
+  }
+
+  // ---- per-env tail (A_0): frozen rows, first_*, scalar outputs
+  if (act_lane && lane0) {
+    if (reset_rows) {
+      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
+    }
+    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
+      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
+      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
+      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
+      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
+    }
+    out.reward[b] = t.reward;
+    out.done[b] = t.done;
+    if (out.steps) out.steps[b] = t.steps;
+    if (out.truncation) out.truncation[b] = t.trunc;
+    if (out.m0) out.m0[b] = t.m0;
+    if (out.m1) out.m1[b] = t.m1;
+    if (out.m2) out.m2[b] = t.m2;
+    out.rng[2 * b] = t.rng0;
+    out.rng[2 * b + 1] = t.rng1;
+  }
+  if (out.any_done) {
+    const unsigned long long mk = __ballot(act_lane && lane0 && done != 0.0f);
+    if (mk != 0ull && lane == 0) atomicOr(out.any_done, 1u);
+  }
+}
+
 // ----------------------------------------------------------------------------- reset
 // System.default_qp forward kinematics (a4): child.rot = parent.rot * axis_angle(axis, q),
 // child.pos = anchor - R(child) off_c with anchor = parent.pos + R(parent) off_p; then the
@@ -1429,6 +1681,23 @@ static void launch_reset(const pob_sys &S, dim3 g, hipStream_t st, const void *s
     default: hipLaunchKernelGGL((k_reset<POB_ANT, 64, QT>), g, dim3(64), shm, st, sp, B, mode, keys, gin, gout, flag, p, total, first, WP); break;
   }
 }
+// eight lanes per env up to this batch (the POB_OCTET_MAX_B environment variable, read at
+// every launch, overrides it; 0 disables the eight-lane kernel)
+static int octet_max_batch() {
+  const char *e = getenv("POB_OCTET_MAX_B");
+  return e ? atoi(e) : 16384;
+}
+template <typename QT>
+static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
+                            const StatePtrs &po, uint32_t flags, int L) {
+  const dim3 g((unsigned)((B + 7) / 8)), b(64);
+  switch (kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_oct<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_oct<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_oct<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_oct<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+  }
+}
 template <typename QT>
 static void launch_step_quad(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                              const float *act, const StatePtrs &po, uint32_t flags, int L) {
@@ -1560,7 +1829,10 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  const bool oct = e->sys.oct_ok && B <= octet_max_batch();
+  if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else launch_step_quad<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");
 }

@@ -1,0 +1,410 @@
+// pob_octet.h -- the PBD Ant step with EIGHT lanes per environment (gfx950), for batches
+// too small to fill the chip with the four-lane kernel (pob_quad.h).
+//
+// Why: below ~16 K envs the four-lane kernel runs at most one wave per SIMD and its time
+// is one wave's dependency chain (a lone wave issues one VALU instruction
+// per ~7 cycles; no ILP left to harvest).  Eight lanes per env halve the joint work and
+// cut the bodies per lane from three to two, so the chain is shorter, and twice as many
+// waves share the SIMDs.
+//
+// Split: every lane owns ONE joint and its two bodies -- slot 0 = the joint's parent,
+// slot 1 = its child:
+//   A_k (hip, joint 2k):     slot 0 = torso (replica in the 4 A lanes), slot 1 = Aux k+1
+//   B_k (knee, joint 2k+1):  slot 0 = Aux k+1 (replica of A_k's),      slot 1 = lower leg k
+// Lane m of the env's 8 (m = lane & 7) is A_m for m < 4 and B_(7-m) for m >= 4, so the A
+// lanes form one DPP quad (the torso's sums over the four hips are quad broadcasts, as in
+// the four-lane kernel) and A_k <-> B_k is one row_half_mirror DPP move (lane m <-> 7 - m).
+// Every lane runs the SAME instruction stream (no role branches): role-dependent values
+// come from a per-role table row in LDS and from selects.  The aux body's terms are summed
+// in both of its lanes in the oracle's order (hip joint first, then knee joint), from the
+// lane's own term and its partner's, so the two replicas stay bit-identical.
+// The joint projection is the oracle's generic form (rotation matrices, full vectors).
+#pragma once
+#include "pob_quad.h"
+
+#define ONB 2  // bodies per lane
+
+struct OBody {
+  v3 x[ONB];
+  q4 q[ONB];
+  v3 v[ONB];
+  v3 w[ONB];
+};
+
+// per-role table row (8 rows per block: row k = A_k, row 4 + k = B_k), staged in LDS
+#define OT_J 0              // joint: off_p(3) off_c(3) axis(3) ref(3) lim_lo lim_hi jdamp strength
+#define OT_OFFP 0
+#define OT_OFFC 3
+#define OT_AXIS 6
+#define OT_REF 9
+#define OT_LO 12
+#define OT_HI 13
+#define OT_DAMP 14
+#define OT_STRENGTH 15
+#define OT_B(s) (16 + 8 * (s))  // slot s body: inv_mass, cap_r, capsule end e0 (3); ends are +-e0
+#define OT_G 32                 // ground contact: end (3), radius, slot (0.0f / 1.0f)
+#define OT_FLOATS POB_OCT_FLOATS
+#define OT_TAB_FLOATS (8 * OT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
+
+#define OTV(T, f) V((T)[(f)], (T)[(f) + 1], (T)[(f) + 2])
+
+// lane m of an env's octet <-> 7 - m (A_k <-> B_k)
+POB_D float oct_swap(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xf, 0xf, true));  // row_half_mirror
+}
+POB_D v3 oct_swap3(v3 a) { return V(oct_swap(a.x), oct_swap(a.y), oct_swap(a.z)); }
+POB_D v3 vsel(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+
+// Per-lane LDS scratch (lane-minor): substep-start pose of the 2 slots (14 floats) and their
+// Info.contact accumulators (12 floats).
+#define OL_PX(s) (7 * (s))
+#define OL_PQ(s) (7 * (s) + 3)
+#define OL_CV(s) (14 + 6 * (s))
+#define OL_CA(s) (14 + 6 * (s) + 3)
+#define OL_FLOATS 26
+
+struct OContacts {
+  float gpen;          // ground contact of the lane's ground body (A: torso, B: lower leg)
+  v3 gpe;              // its sphere centre (x + rotate(end, q))
+  float pen[ONB];      // deepest wall contact of slot s
+  v3 n[ONB];
+  bool sel[ONB];
+  v3 pe[ONB];
+};
+
+// slot s's capsule end points x +- rotate(e0, q) (torso: e0 = 0, both = x)
+POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
+  const v3 rv = qrot_xy(OTV(OT, OT_B(s) + 2), b.q[s]);
+  p0 = vadd(b.x[s], rv);
+  p1 = vsub(b.x[s], rv);
+}
+
+// Contact detection of a collide substep on one lane: the ground contact of its ground
+// body and, per slot, the deepest wall contact over the walls near the lane's two body
+// centres (qdetect's exact per-lane broadphase and d2 pre-cull, wall rows in LDS).
+template <bool WALLS>
+POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslot1, const OBody &b, OContacts &ct) {
+  {
+    const v3 xg = gslot1 ? b.x[1] : b.x[0];
+    const q4 qg = gslot1 ? b.q[1] : b.q[0];
+    ct.gpe = vadd(xg, qrot_xy(OTV(OT, OT_G), qg));
+    ct.gpen = OT[OT_G + 3] - ct.gpe.z;
+  }
+  uint32_t lane_mask = 0u;
+  if (WALLS) {
+    const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
+    const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
+    csys_t &S = *launder(Sp);
+    const int nw = S.n_walls;
+    for (int w = 0; w < nw; ++w) {
+      const bool near = mnx <= S.wall_hi[w][0] && mxx >= S.wall_lo[w][0] && mny <= S.wall_hi[w][1] &&
+                        mxy >= S.wall_lo[w][1];
+      lane_mask |= near ? 1u << w : 0u;
+    }
+  }
+  const bool any_near = WALLS && __any(lane_mask != 0u);
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    POB_FENCE();
+    csys_t &S = *launder(Sp);
+    float best = 0.0f;
+    v3 bn = V(0.0f, 0.0f, 0.0f);
+    bool bsel = false;
+    v3 bpe = bn;
+    if (any_near) {
+      v3 pe[2];
+      ocap_points(OT, b, s, pe[0], pe[1]);
+      const float r = OT[OT_B(s) + 1];
+      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
+      uint32_t m = lane_mask;
+      while (__any(m != 0u)) {
+        const bool on = m != 0u;
+        const int w = on ? __builtin_ctz(m) : 0;
+        m &= m - 1u;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
+      }
+    }
+    ct.pen[s] = best;
+    ct.n[s] = bn;
+    ct.sel[s] = bsel;
+    ct.pe[s] = bpe;
+  }
+}
+
+// position-level ground contact (n = +z; qcontact_position's ground branch) on body (x, q)
+POB_D void oground_position(csys_t &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
+                            const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
+  const v3 cp = V(pe.x, pe.y, pe.z - rad);
+  const v3 rr = vsub(cp, x);
+  const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
+  const float lam = POB_DIV(pen, w);
+  DX.z = FMA(lam, im, DX.z);  // P = (0, 0, lam)
+  DA = V(DA.x + rr.y * lam, DA.y + -(rr.x * lam), DA.z);  // rr x P
+  const v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
+  const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
+  const float lt = pob_sqrt(FMA(dpy, dpy, dpx * dpx));
+  if (lt > 0.0f) {
+    const float inv = pob_rcp(lt);
+    const float tx = dpx * inv, ty = dpy * inv;
+    const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
+    const float wt = im + vdot(ctn, ctn);
+    const float lamt = POB_DIV(lt, wt);
+    if (lamt < S.friction * lam) {
+      const float px_ = tx * -lamt, py_ = ty * -lamt;
+      DX.x = FMA(px_, im, DX.x);
+      DX.y = FMA(py_, im, DX.y);
+      DA = vadd(DA, V(-(rr.z * py_), rr.z * px_, FMA(rr.x, py_, -(rr.y * px_))));  // rr x Pt
+    }
+  }
+}
+
+// position-level wall contact (qcontact_position's general branch)
+POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
+                          const v3 x, const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
+  v3 cp = vfma(n, -rad, pe);
+  v3 rr = vsub(cp, x);
+  v3 cn = vcross(rr, n);
+  float w = im + vdot(cn, cn);
+  float lam = POB_DIV(pen, w);
+  v3 P = vscl(n, lam);
+  DX = vfma(P, im, DX);
+  DA = vadd(DA, vcross(rr, P));
+  v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
+  v3 dp = vsub(cp, cprev);
+  v3 dpt = vfma(n, -vdot(dp, n), dp);
+  float lt = pob_sqrt(vdot(dpt, dpt));
+  if (lt > 0.0f) {
+    v3 t = vdivs(dpt, lt);
+    v3 ctn = vcross(rr, t);
+    float wt = im + vdot(ctn, ctn);
+    float lamt = POB_DIV(lt, wt);
+    if (lamt < S.friction * lam) {
+      v3 Pt = vscl(t, -lamt);
+      DX = vfma(Pt, im, DX);
+      DA = vadd(DA, vcross(rr, Pt));
+    }
+  }
+}
+
+// contact processing order of one body = the oracle's: ground contact first, then wall
+POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const Lds &L,
+                             const OContacts &ct, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    POB_FENCE();
+    csys_t &S = *launder(Sp);
+    const float im = OT[OT_B(s)];
+    const q4 pq = L.get4(OL_PQ(s));
+    const v3 px = L.get3(OL_PX(s));
+    const bool g = (s == 1) == gslot1;  // this slot holds the lane's ground body
+    if (g && ct.gpen > 0.0f) oground_position(S, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+    if (ct.pen[s] > 0.0f)
+      owall_position(S, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+  }
+}
+
+// velocity-level contact (qcontact_velocity's body of one contact); e = the body-frame end
+POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
+                            const float im, const v3 x, const q4 q, const v3 v, const v3 w, v3 &dV, v3 &dW) {
+  v3 pe = vadd(x, qrot_xy(e, q));
+  v3 cp = vfma(n, -rad, pe);
+  v3 rr = vsub(cp, x);
+  v3 vr = vadd(v, vcross(w, rr));
+  v3 dv = V(0.0f, 0.0f, 0.0f);
+  if (ground) {
+    const float vn = vr.z;
+    const float lt = pob_sqrt(FMA(vr.y, vr.y, vr.x * vr.x));
+    if (lt > 0.0f) {
+      const float fr = fminf(S.friction * pen * S.inv_h, lt);
+      const float k = -POB_DIV(fr, lt);
+      dv = V(vr.x * k, vr.y * k, 0.0f);
+    }
+    if (vn < 0.0f) dv.z = -vn;
+  } else {
+    float vn = vdot(vr, n);
+    v3 vt = vfma(n, -vn, vr);
+    float lt = pob_sqrt(vdot(vt, vt));
+    if (lt > 0.0f) {
+      float fr = fminf(S.friction * pen * S.inv_h, lt);
+      dv = vscl(vt, -POB_DIV(fr, lt));
+    }
+    if (vn < 0.0f) dv = vfma(n, -vn, dv);
+  }
+  float D = pob_sqrt(vdot(dv, dv));
+  if (D > 0.0f) {
+    v3 dh = vdivs(dv, D);
+    v3 cd = vcross(rr, dh);
+    float wgt = im + vdot(cd, cd);
+    v3 P = vdivs(dv, wgt);
+    dV = vfma(P, im, dV);
+    dW = vadd(dW, vcross(rr, P));
+  }
+}
+
+POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const OContacts &ct,
+                             v3 (&dV)[ONB], v3 (&dW)[ONB]) {
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    POB_FENCE();
+    csys_t &S = *launder(Sp);
+    const float im = OT[OT_B(s)];
+    const bool g = (s == 1) == gslot1;
+    if (g && ct.gpen > 0.0f)
+      ocontact_vel_one(S, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
+                       b.w[s], dV[s], dW[s]);
+    if (ct.pen[s] > 0.0f) {
+      const v3 e0 = OTV(OT, OT_B(s) + 2);
+      const v3 e = ct.sel[s] ? V(-e0.x, -e0.y, -e0.z) : e0;
+      ocontact_vel_one(S, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
+                       dW[s]);
+    }
+  }
+}
+
+// the lane's joint, oracle joints_position form: point-to-point impulse P and its angular
+// parts xp / xc, hinge alignment + angle limit s
+struct OJoint {
+  v3 P, xp, xc, s;
+};
+POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &J) {
+  csys_t &S = *launder(Sp);
+  const float imp = OT[OT_B(0)], imc = OT[OT_B(1)];
+  const m3 Rp = qmat(b.q[0]), Rc = qmat(b.q[1]);
+  const v3 rp = mrot(Rp, OTV(OT, OT_OFFP)), rc = mrot(Rc, OTV(OT, OT_OFFC));
+  const v3 axis = OTV(OT, OT_AXIS), ref = OTV(OT, OT_REF);
+  const v3 ap = mrot(Rp, axis), ac = mrot(Rc, axis);
+  const v3 fp = mrot(Rp, ref), fc = mrot(Rc, ref);
+  v3 d = vsub(vadd(b.x[1], rc), vadd(b.x[0], rp));
+  const float L2 = vdot(d, d);
+  J.P = V(0.0f, 0.0f, 0.0f); J.xp = J.P; J.xc = J.P;
+  if (L2 > 0.0f) {
+    const v3 ep = vcross(rp, d), ec = vcross(rc, d);
+    const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
+    const float k = POB_DIV(L2 * S.s_pos, den);
+    J.P = vscl(d, k); J.xp = vscl(ep, k); J.xc = vscl(ec, k);
+  }
+  const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+  const float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+  float dl = 0.0f;
+  if (psi < OT[OT_LO]) dl = psi - OT[OT_LO];
+  else if (psi > OT[OT_HI]) dl = psi - OT[OT_HI];
+  const v3 Pl = vscl(ap, dl * S.half_s_ang);
+  J.s = vadd(Pa, Pl);
+}
+
+// One XPBD substep on an env octet (isA: this lane is A_k; see the header comment).
+template <bool WALLS>
+POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool isA, OBody &b, const float act,
+                        const Lds &L, const bool COLLIDE) {
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) { L.set3(OL_PX(s), b.x[s]); L.set4(OL_PQ(s), b.q[s]); }
+  // 1. acceleration level: the lane's joint torque tt (actuator + damping)
+  {
+    v3 tt;
+    {
+      const v3 a = qrot(OTV(OT, OT_AXIS), b.q[0]);
+      const v3 t = vscl(a, act * OT[OT_STRENGTH]);
+      const v3 d = vscl(vsub(b.w[0], b.w[1]), OT[OT_DAMP]);
+      tt = vadd(t, d);
+    }
+    const v3 tpart = oct_swap3(tt);  // the partner's joint torque
+    v3 dw[ONB];
+    {
+      // A slot 0 (torso): (((0 - t0) - t2) - t4) - t6 over the A quad
+      const v3 t0 = quad_bcast3<0>(tt), t2 = quad_bcast3<1>(tt), t4 = quad_bcast3<2>(tt), t6 = quad_bcast3<3>(tt);
+      const v3 torso = vsub(vsub(vsub(vsub(V(0.0f, 0.0f, 0.0f), t0), t2), t4), t6);
+      // aux (A slot 1, B slot 0): (0 + t_hip) - t_knee; B slot 1 (leg): 0 + t_knee
+      const v3 thip = isA ? tt : tpart, tknee = isA ? tpart : tt;
+      const v3 aux = vsub(vadd(V(0.0f, 0.0f, 0.0f), thip), tknee);
+      dw[0] = isA ? torso : aux;
+      dw[1] = isA ? aux : vadd(V(0.0f, 0.0f, 0.0f), tt);
+    }
+    csys_t &S = *launder(Sp);
+#pragma unroll
+    for (int s = 0; s < ONB; ++s) {
+      const v3 v = b.v[s], w = b.w[s];
+      b.v[s] = V(FMA(S.lin_damp, v.x, 0.0f * S.h), FMA(S.lin_damp, v.y, 0.0f * S.h), FMA(S.lin_damp, v.z, S.gz * S.h));
+      b.w[s] = V(FMA(S.ang_damp, w.x, dw[s].x * S.h), FMA(S.ang_damp, w.y, dw[s].y * S.h),
+                 FMA(S.ang_damp, w.z, dw[s].z * S.h));
+    }
+    // 2. kinetic
+#pragma unroll
+    for (int s = 0; s < ONB; ++s) {
+      b.x[s] = vfma(b.v[s], S.h, b.x[s]);
+      q4 dq = qmul_vq(b.w[s], b.q[s]);
+      q4 q = b.q[s];
+      q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
+      q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
+      b.q[s] = qnormalize(q);
+    }
+  }
+  // 3. position projection
+  OContacts ct;
+  const bool gslot1 = !isA;
+  {
+    v3 DX[ONB], DA[ONB];
+    POB_FENCE();
+    OJoint J;
+    ojoint_position(Sp, OT, b, J);
+    POB_FENCE();
+    {
+      const float imp = OT[OT_B(0)], imc = OT[OT_B(1)];
+      // the aux term this lane contributes: A = hip child term, B = knee parent term
+      const v3 tp = vadd(J.xp, J.s), tc = vadd(J.xc, J.s);
+      const v3 Pp = oct_swap3(J.P);
+      const v3 Tp = oct_swap3(isA ? tc : tp);
+      const v3 Phip = isA ? J.P : Pp, Pknee = isA ? Pp : J.P;
+      const v3 Thip = isA ? tc : Tp, Tknee = isA ? Tp : tp;
+      // aux (inverse mass im_aux: A's child = B's parent): hip child term, then knee parent term
+      const float imaux = isA ? imc : imp;
+      const v3 dx_aux = vfma(Pknee, imaux, vfma(Phip, -imaux, V(0.0f, 0.0f, 0.0f)));
+      const v3 da_aux = vadd(vsub(V(0.0f, 0.0f, 0.0f), Thip), Tknee);
+      // torso (A slot 0): the four hips' parent terms in joint order (A quad)
+      const float imp0 = launder(Sp)->inv_mass[0];
+      v3 dxt = V(0.0f, 0.0f, 0.0f), dat = dxt;
+      dxt = vfma(quad_bcast3<0>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<0>(tp));
+      dxt = vfma(quad_bcast3<1>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<1>(tp));
+      dxt = vfma(quad_bcast3<2>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<2>(tp));
+      dxt = vfma(quad_bcast3<3>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<3>(tp));
+      // leg (B slot 1): knee child term
+      const v3 dx_leg = vfma(J.P, -imc, V(0.0f, 0.0f, 0.0f));
+      const v3 da_leg = vsub(V(0.0f, 0.0f, 0.0f), tc);
+      DX[0] = isA ? dxt : dx_aux; DA[0] = isA ? dat : da_aux;
+      DX[1] = isA ? dx_aux : dx_leg; DA[1] = isA ? da_aux : da_leg;
+    }
+    if (COLLIDE) {
+      odetect<WALLS>(Sp, OT, WT, gslot1, b, ct);
+      ocontact_position(Sp, OT, gslot1, b, L, ct, DX, DA);
+    }
+#pragma unroll
+    for (int s = 0; s < ONB; ++s) {
+      b.x[s] = vadd(b.x[s], DX[s]);
+      qadd_half(b.q[s], qmul_vq(DA[s], b.q[s]), 1.0f);
+    }
+  }
+  // 4. velocity projection
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    csys_t &S = *launder(Sp);
+    b.q[s] = qnormalize(b.q[s]);
+    b.v[s] = vscl(vsub(b.x[s], L.get3(OL_PX(s))), S.inv_h);
+    q4 dq = qmul(b.q[s], qinv(L.get4(OL_PQ(s))));
+    const float k2 = 2.0f * S.inv_h;
+    const float kw = dq.w >= 0.0f ? k2 : -k2;
+    b.w[s] = V(dq.x * kw, dq.y * kw, dq.z * kw);
+  }
+  // 5. velocity-level contacts
+  if (COLLIDE) {
+    v3 dV[ONB], dW[ONB];
+#pragma unroll
+    for (int s = 0; s < ONB; ++s) { dV[s] = V(0.0f, 0.0f, 0.0f); dW[s] = V(0.0f, 0.0f, 0.0f); }
+    ocontact_velocity(Sp, OT, gslot1, b, ct, dV, dW);
+#pragma unroll
+    for (int s = 0; s < ONB; ++s) {
+      b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);
+      L.set3(OL_CV(s), vadd(L.get3(OL_CV(s)), dV[s]));
+      L.set3(OL_CA(s), vadd(L.get3(OL_CA(s)), dW[s]));
+    }
+  }
+}

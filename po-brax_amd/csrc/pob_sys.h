@@ -29,6 +29,8 @@
 // rows = 1 KiB, which keeps the quad kernel's LDS at 40 KiB per block (4 blocks per CU).
 #define POB_WALL_FLOATS 6
 #define POB_TAB_FLOATS (4 * POB_LEG_FLOATS + POB_MAXW * POB_WALL_FLOATS)
+// per-role rows of the eight-lanes-per-env kernel (pob_octet.h: OT_* offsets)
+#define POB_OCT_FLOATS 40
 
 struct pob_sys {
   int kind, N, D, n_obj;
@@ -62,6 +64,8 @@ struct pob_sys {
   float tag_cage_xy[2], tag_dying_cost;
   float leg[4][POB_LEG_FLOATS];  // gathered copies of the per-leg rows above
   float wall_row[POB_MAXW][POB_WALL_FLOATS];  // the walls again, one row each (follows leg)
+  float oct[8][POB_OCT_FLOATS];  // eight-lane kernel: rows A_0..A_3 (hips), B_0..B_3 (knees)
+  int oct_ok;         // the Ant pattern the eight-lane kernel assumes holds (torso sphere)
   float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
   int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)
   int torso_point;    // body 0's capsule end and ground end are the body origin (the Ant torso

@@ -287,6 +287,31 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
   for (int q = 0; q < 2; ++q)
     for (int c = 0; c < 3; ++c) s.torso_point &= s.cap_end[0][q][c] == 0.0f;
   for (int c = 0; c < 3; ++c) s.torso_point &= s.ground_end[0][c] == 0.0f;
+  // eight-lane kernel rows (pob_octet.h): role A_k = joint 2k (torso, Aux k+1), B_k = joint
+  // 2k+1 (Aux k+1, lower leg k); per slot the body's inverse mass, radius and capsule end e0
+  // (ends +-e0; the torso sphere: 0); the lane's ground contact (A: torso, B: lower leg)
+  for (int r = 0; r < 8; ++r) {
+    const int k = r & 3;
+    const bool A = r < 4;
+    const int j = A ? 2 * k : 2 * k + 1;
+    const int body[2] = {A ? 0 : 2 * k + 1, A ? 2 * k + 1 : 2 * k + 2};
+    float *O = s.oct[r];
+    for (int i = 0; i < POB_OCT_FLOATS; ++i) O[i] = 0.0f;
+    for (int c = 0; c < 3; ++c) {
+      O[c] = s.off_p[j][c]; O[3 + c] = s.off_c[j][c]; O[6 + c] = s.axis[j][c]; O[9 + c] = s.ref[j][c];
+    }
+    O[12] = s.lim_lo[j]; O[13] = s.lim_hi[j]; O[14] = s.jdamp[j]; O[15] = s.strength[j];
+    for (int sl = 0; sl < 2; ++sl) {
+      float *Bd = O + 16 + 8 * sl;
+      Bd[0] = s.inv_mass[body[sl]]; Bd[1] = s.cap_r[body[sl]];
+      for (int c = 0; c < 3; ++c) Bd[2 + c] = s.cap_end[body[sl]][0][c];
+    }
+    const int g = A ? 0 : k + 1;
+    for (int c = 0; c < 3; ++c) O[32 + c] = s.ground_end[g][c];
+    O[35] = s.ground_r[g];
+    O[36] = A ? 0.0f : 1.0f;
+  }
+  s.oct_ok = s.torso_point;
   return nullptr;
 }
 

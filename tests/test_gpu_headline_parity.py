@@ -1,9 +1,11 @@
 """GPU parity at the BASELINE.json batch sizes, on the launch paths the bench takes.
 
-``launch_step_quad`` (po-brax_amd/csrc/pob_kernels.hip) launches one-wave (64-thread)
-blocks for B <= 4096 and 256-thread blocks above that; the mixed launch is always
-256-thread blocks.  The small-batch parity tests (test_gpu_parity.py, B <= 512) all take
-the one-wave path, so this file checks, against the CPU oracle (OpenMP over envs):
+``pob_step`` runs the eight-lanes-per-env kernel (``k_step_oct``) for B <= 16 384 and the
+four-lane kernel (``k_step_quad``) above -- with one-wave (64-thread) blocks when the
+eight-lane kernel is disabled (``POB_OCTET_MAX_B=0``) and B <= 4 096, 256-thread blocks
+otherwise; the mixed launch is always the four-lane kernel in 256-thread blocks.  The
+small-batch parity tests (test_gpu_parity.py, B <= 512) take the eight-lane path, so this
+file checks, against the CPU oracle (OpenMP over envs):
 
 * the headline config: AntHeavenHell B = 65 536 (config 1 of the bench),
 * AntTag B = 65 536 (config 4's total batch on one GPU), AntGather B = 16 384 (config 3),
@@ -58,31 +60,50 @@ def _per_step(name, B, T=4, L=3, seed=0):
 
 
 @pytest.mark.parametrize("name,B", [("ant_heavenhell", 65536), ("ant_tag", 65536), ("ant_gather", 16384),
-                                    ("ant_heavenhell", 4096), ("ant_heavenhell", 4097), ("ant_gather", 4097),
-                                    ("ant_tag", 4097), ("ant", 4097)])
+                                    ("ant_heavenhell", 16385), ("ant_heavenhell", 4096), ("ant_heavenhell", 4097),
+                                    ("ant_gather", 4097), ("ant_tag", 4097), ("ant", 4097)])
 def test_per_step_parity_bench_sizes(name, B):
     _per_step(name, B)
 
 
-def test_block_switch_prefix_identical():
-    """The first 4 096 envs of a B = 4 097 run (256-thread blocks) equal a B = 4 096 run
-    (one-wave blocks) bit for bit, fp32 and fp16 storage, for every kind."""
+@pytest.mark.parametrize("B", [64, 4097])
+def test_per_step_parity_four_lane_small(monkeypatch, B):
+    """The four-lane kernel at small batches (eight-lane kernel disabled): one-wave blocks
+    (B = 64) and 256-thread blocks with a one-env tail wave (B = 4 097)."""
+    monkeypatch.setenv("POB_OCTET_MAX_B", "0")
+    for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
+        _per_step(name, B, seed=B)
+
+
+def _prefix_identical(Ba, Bb, env_a=None, env_b=None):
     envs = _envs()
     for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
         for qp_dtype in (torch.float32, torch.float16):
-            keys = torch.from_numpy(_keys(4097, 3)).cuda()
-            ea = envs.create(name, batch_size=4096, episode_length=5, qp_dtype=qp_dtype)
-            eb = envs.create(name, batch_size=4097, episode_length=5, qp_dtype=qp_dtype)
-            sa, sb = ea.reset(keys[:4096].contiguous()), eb.reset(keys)
-            for act in _actions(7, 4097, 8):
+            keys = torch.from_numpy(_keys(Bb, 3)).cuda()
+            ea = envs.create(name, batch_size=Ba, episode_length=5, qp_dtype=qp_dtype)
+            eb = envs.create(name, batch_size=Bb, episode_length=5, qp_dtype=qp_dtype)
+            sa, sb = ea.reset(keys[:Ba].contiguous()), eb.reset(keys)
+            for act in _actions(7, Bb, 8):
                 a = torch.from_numpy(act).cuda()
-                sa = ea.step_(sa, a[:4096].contiguous())
+                sa = ea.step_(sa, a[:Ba].contiguous())
                 sb = eb.step_(sb, a)
             for f in ("pos", "rot", "vel", "ang"):
-                assert torch.equal(getattr(sa.qp, f), getattr(sb.qp, f)[:4096]), (name, qp_dtype, f)
-            assert torch.equal(sa.obs, sb.obs[:4096]), (name, qp_dtype)
-            assert torch.equal(sa.reward, sb.reward[:4096]), (name, qp_dtype)
-            assert torch.equal(sa.aux["done"], sb.aux["done"][:4096]), (name, qp_dtype)
+                assert torch.equal(getattr(sa.qp, f), getattr(sb.qp, f)[:Ba]), (name, qp_dtype, f)
+            assert torch.equal(sa.obs, sb.obs[:Ba]), (name, qp_dtype)
+            assert torch.equal(sa.reward, sb.reward[:Ba]), (name, qp_dtype)
+            assert torch.equal(sa.aux["done"], sb.aux["done"][:Ba]), (name, qp_dtype)
+
+
+def test_octet_quad_switch_prefix_identical():
+    """The first 16 384 envs of a B = 16 385 run (four-lane kernel) equal a B = 16 384 run
+    (eight-lane kernel) bit for bit, fp32 and fp16 storage, for every kind."""
+    _prefix_identical(16384, 16385)
+
+
+def test_quad_block_switch_prefix_identical(monkeypatch):
+    """Four-lane kernel only: B = 4 097 (256-thread blocks) vs B = 4 096 (one-wave blocks)."""
+    monkeypatch.setenv("POB_OCTET_MAX_B", "0")
+    _prefix_identical(4096, 4097)
 
 
 def test_mixed_fp16_config5_parity():
