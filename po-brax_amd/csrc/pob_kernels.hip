@@ -933,7 +933,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   const int k = isA ? m : 7 - m;              // the leg
   const int jown = isA ? 2 * k : 2 * k + 1;    // the lane's joint
   const int g0 = isA ? 0 : 2 * k + 1, g1 = isA ? 2 * k + 1 : 2 * k + 2;  // its slots' bodies
-  const float *OT = otab + (isA ? k : 4 + k) * OT_FLOATS;
+  float OT[OT_FLOATS];  // the lane's role row, in registers (constant indices only)
+#pragma unroll
+  for (int i = 0; i < OT_FLOATS; ++i) OT[i] = otab[(isA ? k : 4 + k) * OT_FLOATS + i];
   const float *WT = otab + 8 * OT_FLOATS;
   const Lds Ls{stg, 64, lane};
   const int b_first = (int)blockIdx.x * 8;
@@ -994,10 +996,10 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     const float xb = bd.x[0].x;
     const float a = act[(size_t)b * POB_NJ + jown];
 #pragma unroll
-    for (int sl = 0; sl < ONB; ++sl) { Ls.set3(OL_CV(sl), V(0.0f, 0.0f, 0.0f)); Ls.set3(OL_CA(sl), V(0.0f, 0.0f, 0.0f)); }
+    for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = V(0.0f, 0.0f, 0.0f); cal[sl] = V(0.0f, 0.0f, 0.0f); }
     const int iters = Sp->substeps / 2;
 #pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, Ls, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, (it & 1) != 0);
     {  // joint angle / velocity obs of the lane's joint (a3)
       const v3 ap = qrot(OTV(OT, OT_AXIS), bd.q[0]);
       const v3 ref = OTV(OT, OT_REF);
@@ -1005,8 +1007,10 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       jang = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
       jvel = vdot(vsub(bd.w[1], bd.w[0]), ap);
     }
+    // the lower legs' / auxes' contact velocity sums for the stock ant's contact cost
 #pragma unroll
-    for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = Ls.get3(OL_CV(sl)); cal[sl] = Ls.get3(OL_CA(sl)); }
+    for (int sl = 0; sl < ONB; ++sl) Ls.set3(3 * sl, cvl[sl]);
+    wave_lds_sync();
     if (lane0) {
       float steps = in.steps ? in.steps[b] : 0.0f;
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
@@ -1021,8 +1025,8 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
         float sc = ant_contact_add(0.0f, cvl[0]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          sc = ant_contact_add(sc, Ls.get3_lane(OL_CV(1), lane + q));
-          sc = ant_contact_add(sc, Ls.get3_lane(OL_CV(1), lane + 7 - q));
+          sc = ant_contact_add(sc, Ls.get3_lane(3, lane + q));
+          sc = ant_contact_add(sc, Ls.get3_lane(3, lane + 7 - q));
         }
         t.contact = 0.0005f * sc;
       }

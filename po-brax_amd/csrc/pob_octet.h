@@ -47,6 +47,10 @@ struct OBody {
 #define OT_TAB_FLOATS (8 * OT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
 
 #define OTV(T, f) V((T)[(f)], (T)[(f) + 1], (T)[(f) + 2])
+// The eight-lane kernel runs at most a few waves per SIMD, so the system table's scalars
+// may stay in SGPRs for the whole substep loop (no per-stage re-load, pob_physics.h
+// launder), and the lane's role row lives in VGPRs (k_step_oct copies it out of LDS).
+#define OLAUNDER(p) (p)
 
 // lane m of an env's octet <-> 7 - m (A_k <-> B_k)
 POB_D float oct_swap(float x) {
@@ -55,12 +59,8 @@ POB_D float oct_swap(float x) {
 POB_D v3 oct_swap3(v3 a) { return V(oct_swap(a.x), oct_swap(a.y), oct_swap(a.z)); }
 POB_D v3 vsel(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 
-// Per-lane LDS scratch (lane-minor): substep-start pose of the 2 slots (14 floats) and their
-// Info.contact accumulators (12 floats).
-#define OL_PX(s) (7 * (s))
-#define OL_PQ(s) (7 * (s) + 3)
-#define OL_CV(s) (14 + 6 * (s))
-#define OL_CA(s) (14 + 6 * (s) + 3)
+// per-lane LDS staging area of the eight-lane kernel (floats per lane): the state load, the
+// obs rows and the qp stores go through it
 #define OL_FLOATS 26
 
 struct OContacts {
@@ -94,7 +94,7 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
   if (WALLS) {
     const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
     const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
     const int nw = S.n_walls;
     for (int w = 0; w < nw; ++w) {
       const bool near = mnx <= S.wall_hi[w][0] && mxx >= S.wall_lo[w][0] && mny <= S.wall_hi[w][1] &&
@@ -106,7 +106,7 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
@@ -188,15 +188,15 @@ POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, c
 }
 
 // contact processing order of one body = the oracle's: ground contact first, then wall
-POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const Lds &L,
-                             const OContacts &ct, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
+POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const v3 (&pxs)[ONB],
+                             const q4 (&pqs)[ONB], const OContacts &ct, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
     const float im = OT[OT_B(s)];
-    const q4 pq = L.get4(OL_PQ(s));
-    const v3 px = L.get3(OL_PX(s));
+    const q4 pq = pqs[s];
+    const v3 px = pxs[s];
     const bool g = (s == 1) == gslot1;  // this slot holds the lane's ground body
     if (g && ct.gpen > 0.0f) oground_position(S, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
     if (ct.pen[s] > 0.0f)
@@ -247,7 +247,7 @@ POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, con
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
     const float im = OT[OT_B(s)];
     const bool g = (s == 1) == gslot1;
     if (g && ct.gpen > 0.0f)
@@ -268,10 +268,12 @@ struct OJoint {
   v3 P, xp, xc, s;
 };
 POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &J) {
-  csys_t &S = *launder(Sp);
+  csys_t &S = *OLAUNDER(Sp);
   const float imp = OT[OT_B(0)], imc = OT[OT_B(1)];
   const m3 Rp = qmat(b.q[0]), Rc = qmat(b.q[1]);
-  const v3 rp = mrot(Rp, OTV(OT, OT_OFFP)), rc = mrot(Rc, OTV(OT, OT_OFFC));
+  // (offsets lie in the body xy-plane for every Ant joint, checked by pob_system.cpp: the
+  // products with their zero z drop out, results equal up to the sign of a zero)
+  const v3 rp = mrot_xy(Rp, OTV(OT, OT_OFFP)), rc = mrot_xy(Rc, OTV(OT, OT_OFFC));
   const v3 axis = OTV(OT, OT_AXIS), ref = OTV(OT, OT_REF);
   const v3 ap = mrot(Rp, axis), ac = mrot(Rc, axis);
   const v3 fp = mrot(Rp, ref), fc = mrot(Rc, ref);
@@ -294,11 +296,16 @@ POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &
 }
 
 // One XPBD substep on an env octet (isA: this lane is A_k; see the header comment).
+// (the substep-start poses px / pq and the Info.contact accumulators cv / ca stay in
+// registers: at one or two waves per SIMD there are registers to spare, and an LDS round
+// trip would sit on the lone wave's dependency chain)
 template <bool WALLS>
 POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool isA, OBody &b, const float act,
-                        const Lds &L, const bool COLLIDE) {
+                        v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE) {
+  v3 px[ONB];
+  q4 pq[ONB];
 #pragma unroll
-  for (int s = 0; s < ONB; ++s) { L.set3(OL_PX(s), b.x[s]); L.set4(OL_PQ(s), b.q[s]); }
+  for (int s = 0; s < ONB; ++s) { px[s] = b.x[s]; pq[s] = b.q[s]; }
   // 1. acceleration level: the lane's joint torque tt (actuator + damping)
   {
     v3 tt;
@@ -320,7 +327,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       dw[0] = isA ? torso : aux;
       dw[1] = isA ? aux : vadd(V(0.0f, 0.0f, 0.0f), tt);
     }
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       const v3 v = b.v[s], w = b.w[s];
@@ -361,7 +368,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       const v3 dx_aux = vfma(Pknee, imaux, vfma(Phip, -imaux, V(0.0f, 0.0f, 0.0f)));
       const v3 da_aux = vadd(vsub(V(0.0f, 0.0f, 0.0f), Thip), Tknee);
       // torso (A slot 0): the four hips' parent terms in joint order (A quad)
-      const float imp0 = launder(Sp)->inv_mass[0];
+      const float imp0 = OLAUNDER(Sp)->inv_mass[0];
       v3 dxt = V(0.0f, 0.0f, 0.0f), dat = dxt;
       dxt = vfma(quad_bcast3<0>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<0>(tp));
       dxt = vfma(quad_bcast3<1>(J.P), imp0, dxt); dat = vadd(dat, quad_bcast3<1>(tp));
@@ -375,7 +382,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
     }
     if (COLLIDE) {
       odetect<WALLS>(Sp, OT, WT, gslot1, b, ct);
-      ocontact_position(Sp, OT, gslot1, b, L, ct, DX, DA);
+      ocontact_position(Sp, OT, gslot1, b, px, pq, ct, DX, DA);
     }
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
@@ -386,10 +393,10 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
   // 4. velocity projection
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
-    csys_t &S = *launder(Sp);
+    csys_t &S = *OLAUNDER(Sp);
     b.q[s] = qnormalize(b.q[s]);
-    b.v[s] = vscl(vsub(b.x[s], L.get3(OL_PX(s))), S.inv_h);
-    q4 dq = qmul(b.q[s], qinv(L.get4(OL_PQ(s))));
+    b.v[s] = vscl(vsub(b.x[s], px[s]), S.inv_h);
+    q4 dq = qmul(b.q[s], qinv(pq[s]));
     const float k2 = 2.0f * S.inv_h;
     const float kw = dq.w >= 0.0f ? k2 : -k2;
     b.w[s] = V(dq.x * kw, dq.y * kw, dq.z * kw);
@@ -403,8 +410,8 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);
-      L.set3(OL_CV(s), vadd(L.get3(OL_CV(s)), dV[s]));
-      L.set3(OL_CA(s), vadd(L.get3(OL_CA(s)), dW[s]));
+      cv[s] = vadd(cv[s], dV[s]);
+      ca[s] = vadd(ca[s], dW[s]);
     }
   }
 }
