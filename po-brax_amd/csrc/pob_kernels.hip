@@ -998,8 +998,14 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 #pragma unroll
     for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = V(0.0f, 0.0f, 0.0f); cal[sl] = V(0.0f, 0.0f, 0.0f); }
     const int iters = Sp->substeps / 2;
+#if defined(POB_EXP_NO_COLLIDE)
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+#elif defined(POB_EXP_NO_PHYSICS)
+    for (int it = 0; it < 0 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+#else
 #pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, (it & 1) != 0);
+#endif
     {  // joint angle / velocity obs of the lane's joint (a3)
       const v3 ap = qrot(OTV(OT, OT_AXIS), bd.q[0]);
       const v3 ref = OTV(OT, OT_REF);

@@ -95,7 +95,11 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
     const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
     const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
     csys_t &S = *OLAUNDER(Sp);
+#ifdef POB_EXP_NO_WALLS
+    const int nw = 0;  // timing experiment only
+#else
     const int nw = S.n_walls;
+#endif
     for (int w = 0; w < nw; ++w) {
       const bool near = mnx <= S.wall_hi[w][0] && mxx >= S.wall_lo[w][0] && mny <= S.wall_hi[w][1] &&
                         mxy >= S.wall_lo[w][1];

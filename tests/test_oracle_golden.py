@@ -6,8 +6,11 @@
   notebook cell ant_tag.ipynb:470-477;
 * construction tables: wall boxes of draw_t_maze / draw_arena (envs/utils.py:6-119), the
   AntGather object grid (ant_gather.py:85-91);
-* reset invariants of the three envs (ant_*.py reset / sample_init_qp).
-Physics beyond frame 0 is parity-unpinned against brax.
+* reset invariants of the three envs (ant_*.py reset / sample_init_qp);
+* legacy-spring physics: frames 1..20 of the same trajectory (the cell's 20 jitted steps) by
+  the float64 restatement oracle/legacy_np.py, which also pins brax default_qp's joint-velocity
+  semantics and the torque actuators' limit gate.
+The PBD physics step itself stays parity-unpinned against brax (no artefact records it).
 """
 import json
 import os
@@ -78,6 +81,52 @@ def test_notebook_frame0_c_oracle_fk_f32():
     pos[:9, :2] += ant_xy
     np.testing.assert_allclose(pos[:9], np.array(TRAJ["pos"][0])[:9], atol=3e-6, rtol=0)
     np.testing.assert_allclose(rot[:9], np.array(TRAJ["rot"][0])[:9], atol=3e-6, rtol=0)
+
+
+def _traj_frames():
+    return np.array(TRAJ["pos"])[:, :9], np.array(TRAJ["rot"])[:, :9]
+
+
+def _qerr(q, ref):
+    s = np.sign(np.sum(q * ref, -1))[:, None]  # q and -q are the same rotation
+    return np.abs(q * s - ref).max()
+
+
+def test_legacy_matches_notebook_frames():
+    """notebooks/ant_tag.ipynb:470-477 frames 1..20 (legacy-spring brax, jitted float32) by the
+    float64 restatement: <= 1e-6 m at frame 1, <= 2e-5 over all 20 frames (float32 drift)."""
+    import legacy_np as LG
+    pos, rot = _traj_frames()
+    out = LG.notebook_rollout(pos[0], rot[0], 20)
+    for t, (x, q) in enumerate(out, start=1):
+        tol = 2e-6 if t == 1 else 2e-5
+        assert np.abs(x - pos[t]).max() <= tol, (t, np.abs(x - pos[t]).max())
+        assert _qerr(q, rot[t]) <= tol, (t, _qerr(q, rot[t]))
+
+
+def test_legacy_pins_have_teeth():
+    """Negative controls: the alternatives the fixture rejects (each off by >= 0.5 mm)."""
+    import legacy_np as LG
+    pos, rot = _traj_frames()
+    key = P.np_prngkey(0)
+    acts = []
+    rng = key
+    for _ in range(2):
+        rng, r1 = P.np_split(rng, 2)
+        acts.append(P.f32(P.np_uniform(r1, (8,), -1, 1)))
+    qvel = P.np_uniform(P.np_split(key, 5)[2], (8,), -0.1, 0.1)
+    ant = LG.LegacyAnt()
+    # (a) default_qp velocities accumulated down the tree with the bodies' linear velocities
+    _, _, v_acc, w_acc = P.default_qp(P.default_angle(), qvel)
+    assert np.abs(ant.step(pos[0], rot[0], v_acc, w_acc, acts[0])[0] - pos[1]).max() > 5e-4
+    # the pinned form
+    v0, w0 = LG.joint_velocities(rot[0], qvel)
+    x, q, v, w, _, _ = ant.step(pos[0], rot[0], v0, w0, acts[0])
+    assert np.abs(x - pos[1]).max() <= 2e-6
+    assert np.abs(ant.step(x, q, v, w, acts[1])[0] - pos[2]).max() <= 2e-6
+    # (b) torque actuators not gated at the joint limits: frame 2 off by mm
+    ungated = LG.LegacyAnt(gate_actuators=False)
+    assert np.abs(ungated.step(x, q, v, w, acts[1])[0] - pos[2]).max() > 5e-4
 
 
 def test_notebook_config_matches_restated_ant():
