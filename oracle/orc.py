@@ -71,6 +71,7 @@ class Params(C.Structure):
         ("tag_target_step", C.c_float), ("tag_min_spawn_distance", C.c_float),
         ("tag_cage_xy", C.c_float * 2), ("tag_dying_cost", C.c_float),
         ("action_repeat", C.c_int), ("solver_scale_pos", C.c_float), ("solver_scale_ang", C.c_float),
+        ("legacy_spring", C.c_int),
     ]
 
 

@@ -215,8 +215,9 @@ def default_qp(qpos, qvel=None):
         rot[c] = quat_mul(rot[p], local)
         anchor = pos[p] + rotate(f32(offp), rot[p])
         pos[c] = anchor - rotate(f32(offc), rot[c])
-        ang[c] = ang[p] + rotate(axis, rot[p]) * qvel[j]
-        vel[c] = vel[p] + np.cross(ang[p], anchor - pos[p]) + np.cross(ang[c], pos[c] - anchor)
+        # brax default_qp [ext]: own joint's axis * qvel rotated by the parent, no linear
+        # velocity (pinned by the notebook trajectory: oracle/legacy_np.py)
+        ang[c] = rotate(axis, rot[p]) * qvel[j]
     zmin = np.inf
     for i in range(9):
         ends, r = capsule_ends(i)

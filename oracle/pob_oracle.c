@@ -317,7 +317,11 @@ struct orc_env {
   /* joints (ant tree; parent(j) = j odd ? j : 0, child(j) = j+1) */
   v3 off_p[NJ], off_c[NJ], axis[NJ], ref[NJ];
   float lim_lo[NJ], lim_hi[NJ], jdamp[NJ], strength[NJ];
+  float tan_lo[NJ], tan_hi[NJ]; /* actuator gate (actuator_inside) */
   float default_angle[NJ];
+  /* legacy spring dynamics (brax <= 0.0.12 config: notebooks/ant_tag.ipynb:449) */
+  int legacy;
+  float k_spring, c_spring, k_limit, erp;
   /* colliders: one capsule per ant body */
   v3 cap_end[NDYN][2]; int cap_nend[NDYN]; float cap_r[NDYN];
   int n_ground; int ground_body[NDYN]; v3 ground_end[NDYN]; float ground_r[NDYN];
@@ -348,6 +352,7 @@ void orc_default_params(orc_params *p) {
   p->tag_dying_cost = -1.0f;
   p->action_repeat = 1;
   p->solver_scale_pos = 0.6f; p->solver_scale_ang = 0.2f;
+  p->legacy_spring = 0;
 }
 
 /* double-precision config maths (System construction time) */
@@ -421,6 +426,11 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
   e->friction = 1.0f;
   e->s_pos = p.solver_scale_pos;
   e->half_s_ang = 0.5f * p.solver_scale_ang;
+  /* legacy: stiffness 18000, springDamping 80, limit strength = stiffness (limitStrength
+   * unset), baumgarteErp 0.1 scaled by substeps / dt (brax Collider [ext]) */
+  e->legacy = p.legacy_spring != 0;
+  e->k_spring = 18000.0f; e->c_spring = 80.0f; e->k_limit = 18000.0f;
+  e->erp = (float)(f32d(0.1) * sub / dt);
   for (int i = 0; i < NDYN; ++i) { e->mass[i] = (float)ANT_MASS[i]; e->inv_mass[i] = 1.0f / e->mass[i]; }
   for (int j = 0; j < NJ; ++j) {
     const double *J = ANT_JOINT[j];
@@ -437,6 +447,8 @@ orc_env *orc_env_create(int kind, const orc_params *pin) {
     e->ref[j] = V((float)r[0], (float)r[1], (float)r[2]);
     e->lim_lo[j] = (float)(J[9] * M_PI / 180.0);
     e->lim_hi[j] = (float)(J[10] * M_PI / 180.0);
+    e->tan_lo[j] = (float)tan((double)e->lim_lo[j]);
+    e->tan_hi[j] = (float)tan((double)e->lim_hi[j]);
     e->default_angle[j] = (float)((J[9] + J[10]) * M_PI / 360.0);
     e->jdamp[j] = 20.0f; e->strength[j] = 350.0f;
   }
@@ -530,8 +542,11 @@ void orc_default_qp(const orc_env *e, const float *qpos, const float *qvel, floa
     b.q[c] = qmul(b.q[p], loc);
     v3 anchor = vadd(b.x[p], qrot(e->off_p[j], b.q[p]));
     b.x[c] = vsub(anchor, qrot(e->off_c[j], b.q[c]));
-    b.w[c] = vadd(b.w[p], vscl(qrot(e->axis[j], b.q[p]), qvel[j]));
-    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
+    /* joint velocity: the child's angular velocity is its own joint's axis (parent frame) * qvel,
+     * rotated to the world; no accumulation down the tree, zero linear velocity (brax
+     * System.default_qp [ext]; pinned by the notebook trajectory, tests/test_oracle_golden.py) */
+    b.w[c] = vscl(qrot(e->axis[j], b.q[p]), qvel[j]);
+    b.v[c] = V(0, 0, 0);
   }
   float zmin = 3.0e38f;
   for (int i = 0; i < NDYN; ++i)
@@ -812,6 +827,23 @@ static void joints_position(const orc_env *e, const body_t *b, v3 *DX, v3 *DA) {
   }
 }
 
+/* Torque actuator gate: brax applies NO actuator torque while the joint angle is outside its
+ * limits (pinned in legacy mode by the notebook trajectory, oracle/legacy_np.py; the Torque
+ * actuator [ext] is shared by both dynamics modes).  Here at the substep-start pose: the
+ * angle's direction (gx, gy) = (ref . u, (ref x u) . axis), u = the child's reference
+ * direction in the parent frame through M = R(q_p^-1 q_c); psi = atan2(gy, gx) lies in
+ * [lo, hi] (both within (-pi/2, pi/2), checked at env creation) iff gx > 0 and
+ * tan(lo) gx <= gy <= tan(hi) gx -- the same decision as the angle test up to rounding at the
+ * limit itself, without the arctangent. */
+static int actuator_inside(const orc_env *e, int j, q4 qp, q4 qc) {
+  const q4 r = qmul(qinv(qp), qc);
+  const m3 M = qmat(r);
+  const v3 u = mrot(&M, e->ref[j]);
+  const float gx = vdot(e->ref[j], u), gy = vdot(vcross(e->ref[j], u), e->axis[j]);
+  FL(2);
+  return gx > 0.0f && gy >= e->tan_lo[j] * gx && gy <= e->tan_hi[j] * gx;
+}
+
 static void pbd_substep(const orc_env *e, body_t *b, const float *act, int collide, v3 *cvel, v3 *cang) {
   body_t prev = *b;
   /* 1. acceleration level: torque actuators + joint angular damping, gravity */
@@ -821,7 +853,8 @@ static void pbd_substep(const orc_env *e, body_t *b, const float *act, int colli
     int p = jparent(j), c = jchild(j);
     v3 a = qrot(e->axis[j], b->q[p]);
     FL(1);
-    v3 t = vscl(a, act[j] * e->strength[j]);
+    const float aj = actuator_inside(e, j, b->q[p], b->q[c]) ? act[j] : 0.0f;
+    v3 t = vscl(a, aj * e->strength[j]);
     v3 d = vscl(vsub(b->w[p], b->w[c]), e->jdamp[j]);
     v3 tt = vadd(t, d);
     dw[p] = vsub(dw[p], tt);
@@ -898,9 +931,111 @@ static void store_body(const body_t *b, float *pos, float *rot, float *vel, floa
   }
 }
 
-/* brax System.step: substeps/2 iterations of (plain substep, collide substep) */
+/* ------------------------------------------------------- the legacy spring step */
+/* One-way contact impulses of brax <= 0.0.12 (OneWayCollider [ext]; ground contacts pinned by
+ * the notebook trajectory): Baumgarte-stabilised inelastic normal impulse and Coulomb drag
+ * capped by friction * normal impulse, applied when penetrating, approaching and the impulse
+ * is positive (the drag also needs a tangential speed above 0.01).  Velocity deltas per
+ * body, summed in contact order (ground contacts, then each capsule's deepest wall contact). */
+static void legacy_contacts(const orc_env *e, const body_t *b, v3 *dV, v3 *dW) {
+  contacts_t ct; detect(e, b, &ct);
+  for (int k = 0; k < ct.count; ++k) {
+    const float pen = ct.pen[k];
+    if (!(pen > 0.0f)) continue;
+    const int i = ct.body[k]; const v3 n = ct.n[k];
+    const v3 pe = cpoint(ct.e[k], b->q[i], b->x[i]);
+    const v3 rel = vsub(vfma(n, -ct.r[k], pe), b->x[i]);
+    const v3 cv = vadd(b->v[i], vcross(b->w[i], rel));
+    const float nv = vdot(n, cv);
+    const float ang = vdot(n, vcross(vcross(rel, n), rel));
+    FL(6);
+    const float rden = 1.0f / (e->inv_mass[i] + ang);
+    const float imp = (e->erp * pen - nv) * rden;
+    if (!(nv < 0.0f && imp > 0.0f)) continue;
+    const v3 vd = vfma(n, -nv, cv);
+    const float nd = sqrtf(vdot(vd, vd));
+    v3 P = vscl(n, imp);
+    if (nd > 0.01f) {
+      FL(6);
+      const float impd = fminf(nd * rden, e->friction * imp);
+      P = vfma(vd, -(impd * (1.0f / (1e-6f + nd))), P);
+    }
+    dV[i] = vfma(P, e->inv_mass[i], dV[i]);
+    dW[i] = vadd(dW[i], vcross(rel, P));
+  }
+}
+
+/* revolute spring joints + torque actuators of brax <= 0.0.12 as accelerations [ext]: anchor
+ * spring k (p_p - p_c) + c (v_p - v_c), axis alignment k ap x ac, limit spring -k ap dang,
+ * damping -20 (w_p - w_c); actuator ap * act * 350, gated off outside the limits.  Body terms
+ * summed in joint order. */
+static void legacy_joints(const orc_env *e, const body_t *b, const float *act, v3 *dv, v3 *dw) {
+  for (int j = 0; j < NJ; ++j) {
+    const int p = jparent(j), c = jchild(j);
+    const v3 rp = qrot(e->off_p[j], b->q[p]), rc = qrot(e->off_c[j], b->q[c]);
+    const v3 dpos = vsub(vadd(b->x[p], rp), vadd(b->x[c], rc));
+    const v3 dvel = vsub(vadd(b->v[p], vcross(b->w[p], rp)), vadd(b->v[c], vcross(b->w[c], rc)));
+    const v3 imp = vfma(dpos, e->k_spring, vscl(dvel, e->c_spring));
+    const v3 ap = qrot(e->axis[j], b->q[p]), ac = qrot(e->axis[j], b->q[c]);
+    const v3 fp = qrot(e->ref[j], b->q[p]), fc = qrot(e->ref[j], b->q[c]);
+    const float psi = orc_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+    float dang = 0.0f;
+    if (psi < e->lim_lo[j]) { FL(1); dang = e->lim_lo[j] - psi; }
+    else if (psi > e->lim_hi[j]) { FL(1); dang = e->lim_hi[j] - psi; }
+    FL(2);
+    v3 tq = vscl(vcross(ap, ac), e->k_spring);
+    tq = vfma(ap, -(e->k_limit * dang), tq);
+    tq = vfma(vsub(b->w[p], b->w[c]), -e->jdamp[j], tq);
+    const v3 ta = vscl(ap, (dang != 0.0f ? 0.0f : act[j]) * e->strength[j]);
+    const v3 tw = vsub(tq, ta);  /* parent: + tw, child: - tw */
+    dv[p] = vfma(imp, -e->inv_mass[p], dv[p]);
+    dv[c] = vfma(imp, e->inv_mass[c], dv[c]);
+    dw[p] = vadd(dw[p], vadd(vcross(rp, vscl(imp, -1.0f)), tw));
+    dw[c] = vadd(dw[c], vsub(vcross(rc, imp), tw));
+  }
+}
+
+static void legacy_substep(const orc_env *e, body_t *b, const float *act, v3 *cvel, v3 *cang) {
+  /* kinetic */
+  for (int i = 0; i < NDYN; ++i) {
+    b->x[i] = vfma(b->v[i], e->h, b->x[i]);
+    q4 dq = qmul_vq(b->w[i], b->q[i]);
+    FL(8);
+    q4 q = b->q[i];
+    q.w = fmaf(e->half_h, dq.w, q.w); q.x = fmaf(e->half_h, dq.x, q.x);
+    q.y = fmaf(e->half_h, dq.y, q.y); q.z = fmaf(e->half_h, dq.z, q.z);
+    b->q[i] = qnormalize(q);
+  }
+  /* joints + actuators -> potential update (gravity, damping) */
+  v3 dv[NDYN], dw[NDYN];
+  for (int i = 0; i < NDYN; ++i) { dv[i] = V(0, 0, 0); dw[i] = V(0, 0, 0); }
+  legacy_joints(e, b, act, dv, dw);
+  for (int i = 0; i < NDYN; ++i) {
+    FL(24);
+    const v3 v = b->v[i], w = b->w[i];
+    b->v[i] = V(fmaf(e->lin_damp, v.x, (dv[i].x + e->g[0]) * e->h), fmaf(e->lin_damp, v.y, (dv[i].y + e->g[1]) * e->h),
+                fmaf(e->lin_damp, v.z, (dv[i].z + e->g[2]) * e->h));
+    b->w[i] = V(fmaf(e->ang_damp, w.x, dw[i].x * e->h), fmaf(e->ang_damp, w.y, dw[i].y * e->h),
+                fmaf(e->ang_damp, w.z, dw[i].z * e->h));
+  }
+  /* collisions: velocity impulses */
+  v3 dV[NDYN], dW[NDYN];
+  for (int i = 0; i < NDYN; ++i) { dV[i] = V(0, 0, 0); dW[i] = V(0, 0, 0); }
+  legacy_contacts(e, b, dV, dW);
+  for (int i = 0; i < NDYN; ++i) {
+    b->v[i] = vadd(b->v[i], dV[i]); b->w[i] = vadd(b->w[i], dW[i]);
+    cvel[i] = vadd(cvel[i], dV[i]); cang[i] = vadd(cang[i], dW[i]);
+  }
+}
+
+/* brax System.step: PBD = substeps/2 iterations of (plain substep, collide substep); legacy
+ * spring = substeps of (kinetic, joints + actuators, collisions) */
 static void physics_step(const orc_env *e, body_t *b, const float *act, v3 *cvel, v3 *cang) {
   for (int i = 0; i < NDYN; ++i) { cvel[i] = V(0, 0, 0); cang[i] = V(0, 0, 0); }
+  if (e->legacy) {
+    for (int it = 0; it < e->substeps; ++it) legacy_substep(e, b, act, cvel, cang);
+    return;
+  }
   for (int it = 0; it < e->substeps / 2; ++it) {
     pbd_substep(e, b, act, 0, cvel, cang);
     pbd_substep(e, b, act, 1, cvel, cang);
@@ -909,8 +1044,9 @@ static void physics_step(const orc_env *e, body_t *b, const float *act, v3 *cvel
 
 /* sys.info(qp).contact (a2): contact passes evaluated at a static state */
 static void info_contact(const orc_env *e, const body_t *b, v3 *cvel, v3 *cang) {
-  contacts_t ct; detect(e, b, &ct);
   for (int i = 0; i < NDYN; ++i) { cvel[i] = V(0, 0, 0); cang[i] = V(0, 0, 0); }
+  if (e->legacy) { legacy_contacts(e, b, cvel, cang); return; }  /* the colliders' impulses */
+  contacts_t ct; detect(e, b, &ct);
   contact_velocity(e, b, &ct, cvel, cang);
 }
 void orc_contact_info(const orc_env *e, const float *pos, const float *rot, const float *vel,

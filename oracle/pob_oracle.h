@@ -42,6 +42,9 @@ typedef struct orc_params {
   /* physics */
   int action_repeat;
   float solver_scale_pos, solver_scale_ang;
+  /* dynamics: 0 = PBD (brax 0.0.13-0.0.16 "pbd"), 1 = legacy spring (brax <= 0.0.12, the
+   * physics of the notebook trajectory notebooks/ant_tag.ipynb:449) */
+  int legacy_spring;
 } orc_params;
 
 typedef struct orc_state {

@@ -659,7 +659,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     for (int jl = 0; jl < QNJ; ++jl) {
       const int p = jparent(jl), c = jchild(jl);
       v3 ap = qrot(QJV(LT, jl, QJ_AXIS), bd.q[p]);
-      const v3 ref = QJV(LT, jl, QJ_REF);
+      const v3 ref = jl == 0 ? V(-1.0f, 0.0f, 0.0f) : V(0.0f, 0.0f, 1.0f);  // the Ant's (pob_system.cpp)
       v3 fp = qrot(ref, bd.q[p]), fc = qrot(ref, bd.q[c]);
       jang[jl] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
       jvel[jl] = vdot(vsub(bd.w[c], bd.w[p]), ap);
@@ -1185,8 +1185,8 @@ POB_D void fk(csys_t &S, const float (&qpos)[POB_NJ], const float (&qvel)[POB_NJ
     b.q[c] = qmul(b.q[p], loc);
     v3 anchor = vadd(b.x[p], qrot(SV(S.off_p[j]), b.q[p]));
     b.x[c] = vsub(anchor, qrot(SV(S.off_c[j]), b.q[c]));
-    b.w[c] = vadd(b.w[p], vscl(qrot(axis, b.q[p]), qvel[j]));
-    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
+    b.w[c] = vscl(qrot(axis, b.q[p]), qvel[j]);  // default_qp: own joint only, no linear velocity
+    b.v[c] = V(0.0f, 0.0f, 0.0f);
   }
   float zmin = 3.0e38f;
 #pragma unroll
@@ -1312,8 +1312,10 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
     b.q[c] = qmul(b.q[p], loc);
     const v3 anchor = vadd(b.x[p], qrot(QJV(LT, jl, QJ_OFFP), b.q[p]));
     b.x[c] = vsub(anchor, qrot(QJV(LT, jl, QJ_OFFC), b.q[c]));
-    b.w[c] = vadd(b.w[p], vscl(qrot(axis, b.q[p]), qvel));
-    b.v[c] = vadd(vadd(b.v[p], vcross(b.w[p], vsub(anchor, b.x[p]))), vcross(b.w[c], vsub(b.x[c], anchor)));
+    // default_qp's joint velocity: the child's own joint only (axis * qvel rotated by the
+    // parent), no linear velocity (oracle orc_default_qp)
+    b.w[c] = vscl(qrot(axis, b.q[p]), qvel);
+    b.v[c] = V(0.0f, 0.0f, 0.0f);
   }
   // lift: the lowest capsule point of the whole ant at z = 0
   float zmin = vadd(b.x[0], qrot(qcap_end(S, LT, 0, 0), b.q[0])).z - q_cap_r(S, LT, 0);
@@ -1378,7 +1380,7 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
   for (int jl = 0; jl < QNJ; ++jl) {
     const int p = jparent(jl), c = jchild(jl);
     const v3 ap = qrot(QJV(LT, jl, QJ_AXIS), b.q[p]);
-    const v3 ref = QJV(LT, jl, QJ_REF);
+    const v3 ref = jl == 0 ? V(-1.0f, 0.0f, 0.0f) : V(0.0f, 0.0f, 1.0f);  // the Ant's (pob_system.cpp)
     const v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
     R.jang[jl] = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
     R.jvel[jl] = vdot(vsub(b.w[c], b.w[p]), ap);

@@ -146,6 +146,28 @@ POB_D q4 qmul_vq(v3 a, q4 q) {
   return r;
 }
 POB_D q4 qinv(q4 q) { q4 r; r.w = q.w; r.x = -q.x; r.y = -q.y; r.z = -q.z; return r; }
+// Torque actuator gate (oracle actuator_inside): no actuator torque while the joint angle is
+// outside its limits.  The angle's direction from the relative rotation M = R(q_p^-1 q_c) (the
+// qmat formula): hip (reference -x, axis +z) gx = M00, gy = M10; knee (reference +z, axis in
+// the xy-plane) gx = M22, gy = M02 ay - M12 ax -- the oracle's generic (ref . M ref,
+// (ref x M ref) . axis) with the products of the frames' exact zeros and ones folded.  Inside
+// [lo, hi] (both in (-pi/2, pi/2)) iff gx > 0 and tan(lo) gx <= gy <= tan(hi) gx.
+POB_D bool actuator_inside(q4 qp, q4 qc, bool hip, v3 axis, float tlo, float thi) {
+  const q4 r = qmul(qinv(qp), qc);
+  const float c = FMA(r.w, r.w, -FMA(r.z, r.z, FMA(r.y, r.y, r.x * r.x)));
+  const float s2 = 2.0f * r.w, x2 = 2.0f * r.x;
+  float gx, gy;
+  if (hip) {
+    gx = FMA(x2, r.x, c);
+    gy = FMA(x2, r.y, s2 * r.z);
+  } else {
+    const float y2 = 2.0f * r.y, z2 = 2.0f * r.z;
+    const float m02 = FMA(x2, r.z, s2 * r.y), m12 = FMA(y2, r.z, -(s2 * r.x));
+    gx = FMA(z2, r.z, c);
+    gy = FMA(m02, axis.y, -m12 * axis.x);
+  }
+  return gx > 0.0f && gy >= tlo * gx && gy <= thi * gx;
+}
 // a * s + b, fused per component
 POB_D v3 vfma(v3 a, float s, v3 b) { return V(FMA(a.x, s, b.x), FMA(a.y, s, b.y), FMA(a.z, s, b.z)); }
 // x + rotate(v, q) with the translation folded into the rotation's fused chain

@@ -43,6 +43,8 @@ struct OBody {
 #define OT_STRENGTH 15
 #define OT_B(s) (16 + 8 * (s))  // slot s body: inv_mass, cap_r, capsule end e0 (3); ends are +-e0
 #define OT_G 32                 // ground contact: end (3), radius, slot (0.0f / 1.0f)
+#define OT_TLO 37               // tan(lim_lo), tan(lim_hi): the actuator gate
+#define OT_THI 38
 #define OT_FLOATS POB_OCT_FLOATS
 #define OT_TAB_FLOATS (8 * OT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
 
@@ -315,7 +317,8 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
     v3 tt;
     {
       const v3 a = qrot(OTV(OT, OT_AXIS), b.q[0]);
-      const v3 t = vscl(a, act * OT[OT_STRENGTH]);
+      const bool in = actuator_inside(b.q[0], b.q[1], isA, OTV(OT, OT_AXIS), OT[OT_TLO], OT[OT_THI]);
+      const v3 t = vscl(a, (in ? act : 0.0f) * OT[OT_STRENGTH]);
       const v3 d = vscl(vsub(b.w[0], b.w[1]), OT[OT_DAMP]);
       tt = vadd(t, d);
     }

@@ -62,7 +62,8 @@ template <int J> POB_D v3 quad_bcast3(v3 a) { return V(quad_bcast_b<J>(a.x), qua
 #define QJ_OFFP 0
 #define QJ_OFFC 3
 #define QJ_AXIS 6
-#define QJ_REF 9
+#define QJ_TLO 9   // tan(lim_lo), tan(lim_hi): the actuator gate
+#define QJ_THI 10
 #define QJ_LO 12
 #define QJ_HI 13
 #define QJ_DAMP 14
@@ -448,8 +449,10 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
       const int p = jparent(jl), c = jchild(jl);
-      const v3 a = jl == 0 ? qrot_ez(b.q[p]) : qrot_xy(QJV(LT, jl, QJ_AXIS), b.q[p]);
-      v3 t = vscl(a, act[jl] * QJS(LT, jl, QJ_STRENGTH));
+      const v3 axis = QJV(LT, jl, QJ_AXIS);
+      const v3 a = jl == 0 ? qrot_ez(b.q[p]) : qrot_xy(axis, b.q[p]);
+      const bool in = actuator_inside(b.q[p], b.q[c], jl == 0, axis, QJS(LT, jl, QJ_TLO), QJS(LT, jl, QJ_THI));
+      v3 t = vscl(a, (in ? act[jl] : 0.0f) * QJS(LT, jl, QJ_STRENGTH));
       v3 d = vscl(vsub(b.w[p], b.w[c]), QJS(LT, jl, QJ_DAMP));
       tt[jl] = vadd(t, d);
     }

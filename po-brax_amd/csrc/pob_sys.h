@@ -20,7 +20,7 @@
 
 // per-leg table of the four-lanes-per-env kernel (pob_quad.h), leg k = joints 2k, 2k+1,
 // bodies 2k+1, 2k+2, ground collider k+1; staged in LDS once per block
-#define POB_LEG_JOINT(jl) (16 * (jl))   // off_p(3) off_c(3) axis(3) ref(3) lim_lo lim_hi jdamp strength
+#define POB_LEG_JOINT(jl) (16 * (jl))   // off_p(3) off_c(3) axis(3) tan_lo tan_hi 0 lim_lo lim_hi jdamp strength
 #define POB_LEG_BODY(l) (32 + 8 * ((l) - 1))  // inv_mass cap_r cap_end[2][3]   (l = 1, 2)
 #define POB_LEG_GROUND 48               // ground_end(3) ground_r
 #define POB_LEG_FLOATS 52
@@ -43,6 +43,7 @@ struct pob_sys {
   // limits (rad), angular damping, actuator strength, default angle
   float off_p[POB_NJ][3], off_c[POB_NJ][3], axis[POB_NJ][3], ref[POB_NJ][3];
   float lim_lo[POB_NJ], lim_hi[POB_NJ], jdamp[POB_NJ], strength[POB_NJ], default_angle[POB_NJ];
+  float tan_lo[POB_NJ], tan_hi[POB_NJ];  // torque actuator gate (pob_math.h actuator_inside)
   // one capsule per dynamic body: segment end points (body frame) and radius; body 0's
   // segment is degenerate (a sphere: one end point)
   float cap_end[POB_NDYN][2][3], cap_r[POB_NDYN];

@@ -141,6 +141,10 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     for (int c = 0; c < 3; ++c) { s.axis[j][c] = (float)a[c]; s.ref[j][c] = (float)r[c]; }
     s.lim_lo[j] = (float)(J[9] * M_PI / 180.0);
     s.lim_hi[j] = (float)(J[10] * M_PI / 180.0);
+    s.tan_lo[j] = (float)tan((double)s.lim_lo[j]);  // oracle orc_env_create: the same host libm
+    s.tan_hi[j] = (float)tan((double)s.lim_hi[j]);
+    if (!(s.lim_lo[j] > (float)(-M_PI / 2) && s.lim_hi[j] < (float)(M_PI / 2) && s.lim_lo[j] <= s.lim_hi[j]))
+      return "joint limits outside (-90, 90) degrees (the actuator gate assumes them)";
     s.default_angle[j] = (float)((J[9] + J[10]) * M_PI / 360.0);
     s.jdamp[j] = 20.0f; s.strength[j] = 350.0f;
   }
@@ -223,8 +227,9 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
       const int j = 2 * k + jl;
       float *J = L + POB_LEG_JOINT(jl);
       for (int c = 0; c < 3; ++c) {
-        J[c] = s.off_p[j][c]; J[3 + c] = s.off_c[j][c]; J[6 + c] = s.axis[j][c]; J[9 + c] = s.ref[j][c];
+        J[c] = s.off_p[j][c]; J[3 + c] = s.off_c[j][c]; J[6 + c] = s.axis[j][c];
       }
+      J[9] = s.tan_lo[j]; J[10] = s.tan_hi[j]; J[11] = 0.0f;  // (the kernels use the Ant's fixed references)
       J[12] = s.lim_lo[j]; J[13] = s.lim_hi[j]; J[14] = s.jdamp[j]; J[15] = s.strength[j];
     }
     for (int l = 1; l <= 2; ++l) {
@@ -310,6 +315,7 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     for (int c = 0; c < 3; ++c) O[32 + c] = s.ground_end[g][c];
     O[35] = s.ground_r[g];
     O[36] = A ? 0.0f : 1.0f;
+    O[37] = s.tan_lo[j]; O[38] = s.tan_hi[j];
   }
   s.oct_ok = s.torso_point;
   return nullptr;

@@ -116,17 +116,67 @@ def test_legacy_pins_have_teeth():
         acts.append(P.f32(P.np_uniform(r1, (8,), -1, 1)))
     qvel = P.np_uniform(P.np_split(key, 5)[2], (8,), -0.1, 0.1)
     ant = LG.LegacyAnt()
-    # (a) default_qp velocities accumulated down the tree with the bodies' linear velocities
-    _, _, v_acc, w_acc = P.default_qp(P.default_angle(), qvel)
+    # (a) joint velocities accumulated down the tree, with the bodies' linear velocities
+    v_acc, w_acc = np.zeros((9, 3)), np.zeros((9, 3))
+    for j in range(8):
+        p, c = LG.PAR[j], LG.CHI[j]
+        w_acc[c] = w_acc[p] + P.rotate(LG.AXIS[j], rot[0][p]) * qvel[j]
+        anchor = pos[0][p] + P.rotate(LG.OFFP[j], rot[0][p])
+        v_acc[c] = v_acc[p] + np.cross(w_acc[p], anchor - pos[0][p]) + np.cross(w_acc[c], pos[0][c] - anchor)
     assert np.abs(ant.step(pos[0], rot[0], v_acc, w_acc, acts[0])[0] - pos[1]).max() > 5e-4
-    # the pinned form
+    # the pinned form (= pob_np.default_qp's velocities)
     v0, w0 = LG.joint_velocities(rot[0], qvel)
+    _, _, v_np, w_np = P.default_qp(LG.joint_angles(rot[0]), qvel)
+    np.testing.assert_allclose(w_np, w0, atol=1e-12)
+    assert not v_np.any()
     x, q, v, w, _, _ = ant.step(pos[0], rot[0], v0, w0, acts[0])
     assert np.abs(x - pos[1]).max() <= 2e-6
     assert np.abs(ant.step(x, q, v, w, acts[1])[0] - pos[2]).max() <= 2e-6
     # (b) torque actuators not gated at the joint limits: frame 2 off by mm
     ungated = LG.LegacyAnt(gate_actuators=False)
     assert np.abs(ungated.step(x, q, v, w, acts[1])[0] - pos[2]).max() > 5e-4
+
+
+def notebook_legacy_state(env, pos0, rot0):
+    """TAG state (B = 1) at the notebook's frame 0: the 9 ant rows from the recorded frame,
+    joint velocities from the reset key's split(rng, 5)[2] (oracle/legacy_np.py)."""
+    import legacy_np as LG
+    s = env.empty(1)
+    s["rot"][0, :, 0] = 1.0
+    s["pos"][0, :9] = pos0
+    s["rot"][0, :9] = rot0
+    qvel = P.np_uniform(P.np_split(P.np_prngkey(0), 5)[2], (8,), -0.1, 0.1)
+    _, w = LG.joint_velocities(np.asarray(rot0, float), qvel)
+    s["ang"][0, :9] = w
+    s["pos"][0, 10] = (3.0, 3.0, 0.5)   # the target, out of the way (it never collides)
+    s["pos"][0, 11] = (0.0, 0.0, 0.5)   # the arena body
+    return s
+
+
+def notebook_actions(T):
+    rng = P.np_prngkey(0)
+    out = []
+    for _ in range(T):
+        rng, r1 = P.np_split(rng, 2)
+        out.append(P.np_uniform(r1, (8,), -1, 1).astype(np.float32))
+    return out
+
+
+def test_c_oracle_legacy_matches_notebook_frames():
+    """The float32 C restatement in legacy-spring mode (orc legacy_spring=1) reproduces the
+    notebook's 20 frames.  AntTag with cage 5.5 puts the box walls' inner faces at +-6.5 like
+    the notebook's capsule walls (no wall contact either way)."""
+    pos, rot = _traj_frames()
+    e = orc.OracleEnv("ant_tag", legacy_spring=1, tag_cage_xy=(5.5, 5.5))
+    s = notebook_legacy_state(e, pos[0].astype(np.float32), rot[0].astype(np.float32))
+    worst = 0.0
+    for t, a in enumerate(notebook_actions(20), start=1):
+        s = e.step(s, a[None], flags=0)
+        dx = np.abs(s["pos"][0, :9] - pos[t]).max()
+        dq = _qerr(s["rot"][0, :9].astype(np.float64), rot[t])
+        worst = max(worst, dx, dq)
+        assert dx <= 2e-5 and dq <= 2e-5, (t, dx, dq)
+    assert worst > 0.0
 
 
 def test_notebook_config_matches_restated_ant():
