@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 3
+#define POB_ABI_VERSION 4
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -95,6 +95,8 @@ typedef struct pob_params {
   int action_repeat;                  /* ActionRepeatWrapper wrappers.py:16-24 */
   float solver_scale_pos, solver_scale_ang; /* PBD joint solver scales */
   int qp_storage;                     /* pob_qp_storage (engine extension; default F32) */
+  int legacy_spring;                  /* 1: brax <= 0.0.12 spring dynamics (brax Ant(legacy_spring=True),
+                                         the physics of notebooks/ant_tag.ipynb:449); 0: PBD */
 } pob_params;
 
 /* Env state: device pointers, batch-major.  Optional members may be NULL.  With

@@ -525,7 +525,7 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
 #define POB_TS_WAVES 65536
 __device__ unsigned long long pob_ts_buf[POB_TS_WAVES * 8];  // timing experiment only
 #endif
-template <int KIND, typename QT>
+template <int KIND, typename QT, bool LEG = false>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
                           const float *legtab) {
@@ -634,6 +634,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
+    if (LEG) {
+      // legacy spring dynamics: every substep kinetic + springs + contact impulses
+#pragma nounroll
+      for (int it = 0; it < Sp->substeps; ++it) qlegacy_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls);
+    } else {
 #pragma nounroll
 #if defined(POB_EXP_NO_COLLIDE)
     for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
@@ -654,6 +659,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0);
     }
 #endif
+    }
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {
@@ -849,6 +855,19 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
                            (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
+}
+
+// The same fused step with the legacy spring dynamics (pob_params.legacy_spring; pob_quad.h
+// qlegacy_substep) -- a kernel of its own so the PBD kernels keep their register allocation.
+template <int KIND, typename QT>
+__global__ __launch_bounds__(256) void k_step_legacy(const void *sysp, const int B, const StatePtrs in,
+                                                     const float *__restrict__ act, const StatePtrs out,
+                                                     const uint32_t flags, const int L) {
+  __shared__ float lds[QL_FLOATS * 256];
+  __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
+  stage_leg_table((csys_t *)(size_t)sysp, legtab);
+  step_quad_body<KIND, QT, true>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                 (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
 }
 
 // Mixed launch: segment k owns blocks [blk0_k, blk0_{k+1}); the segment index is
@@ -1374,7 +1393,8 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
   qdetect<KIND != POB_ANT>(Sp, LT, WT, b, ct);
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { R.cv[l] = V(0.0f, 0.0f, 0.0f); R.ca[l] = V(0.0f, 0.0f, 0.0f); }
-  qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca);
+  if (S.legacy) qlegacy_contacts(Sp, LT, b, ct, R.cv, R.ca);  // legacy sys.info: the colliders' impulses
+  else qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca);
   // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
   for (int jl = 0; jl < QNJ; ++jl) {
@@ -1711,13 +1731,22 @@ static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, con
   }
 }
 template <typename QT>
-static void launch_step_quad(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+static void launch_step_quad(int kind, bool legacy, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                              const float *act, const StatePtrs &po, uint32_t flags, int L) {
   // Batches of at most one wave per CU launch one-wave blocks, so each wave gets a CU (its
   // scalar unit, LDS and instruction cache) to itself instead of four waves sharing 1/4 of
   // the CUs; larger batches use 256-thread blocks (the kernel is block-size agnostic)
   const int bs = 4 * B <= 64 * 256 ? 64 : 256;
   const dim3 g = grid_for(4 * B, bs), b(bs);
+  if (legacy) {
+    switch (kind) {
+      case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_legacy<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+      case POB_GATHER: hipLaunchKernelGGL((k_step_legacy<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+      case POB_TAG: hipLaunchKernelGGL((k_step_legacy<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+      default: hipLaunchKernelGGL((k_step_legacy<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    }
+    return;
+  }
   switch (kind) {
     case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
     case POB_GATHER: hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
@@ -1841,11 +1870,11 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const bool oct = e->sys.oct_ok && B <= octet_max_batch();
+  const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();  // legacy: lane quads only
   if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
-  else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
-  else launch_step_quad<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);
+  else launch_step_quad<float>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");
 }
 
@@ -1863,6 +1892,7 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
     const pob_env *e = envs[k];
     if (int rc = check_step(e, B[k], &in[k], act[k], &out[k], flags, episode_length)) return rc;
     if (e->sys.qp_f16 != envs[0]->sys.qp_f16) return fail(POB_EINVAL, "mixed step: envs must share qp_storage");
+    if (e->sys.legacy) return fail(POB_EINVAL, "mixed step: legacy-spring envs step through pob_step");
     if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
     stage = stage && can_stage(e, &in[k]);
     MixSeg &s = A.s[k];

@@ -547,3 +547,135 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     }
   }
 }
+
+// ------------------------------------------------------------- legacy spring dynamics
+// brax <= 0.0.12 spring/impulse step (oracle legacy_substep; pinned by the 20 frames of
+// notebooks/ant_tag.ipynb:449) on the same lane quads: kinetic, then spring joints + torque
+// actuators as accelerations, then one-way contact impulses.  Every expression follows the
+// oracle's generic form (no frame specialisation: this mode is the parity reference for the
+// notebook, not the throughput path).
+
+// one-way contact impulses of the detected contacts into dV / dW (oracle legacy_contacts;
+// per body: ground contact first, then wall)
+POB_D void qlegacy_contacts(csys_t *Sp, const float *LT, const QBody &b, const QContacts &ct, v3 (&dV)[QNB],
+                            v3 (&dW)[QNB]) {
+#pragma unroll
+  for (int c = 0; c < 2 + QNB; ++c) {
+    const int l = qcontact_body(c);
+    const float pen = ct.pen[c];
+    if (pen > 0.0f) {
+      csys_t &S = *launder(Sp);
+      v3 e, n;
+      float rad;
+      qcontact_geom(S, LT, ct, c, e, n, rad);
+      const float im = q_inv_mass(S, LT, l);
+      const v3 rel = vsub(vfma(n, -rad, ct.pe[c]), b.x[l]);  // pe = x + rotate(e, q) of the detection
+      const v3 cv = vadd(b.v[l], vcross(b.w[l], rel));
+      const float nv = vdot(n, cv);
+      const float ang = vdot(n, vcross(vcross(rel, n), rel));
+      const float rden = pob_rcp(im + ang);
+      const float imp = (S.erp * pen - nv) * rden;
+      if (nv < 0.0f && imp > 0.0f) {
+        const v3 vd = vfma(n, -nv, cv);
+        const float nd = pob_sqrt(vdot(vd, vd));
+        v3 P = vscl(n, imp);
+        if (nd > 0.01f) {
+          const float impd = fminf(nd * rden, S.friction * imp);
+          P = vfma(vd, -(impd * pob_rcp(1e-6f + nd)), P);
+        }
+        dV[l] = vfma(P, im, dV[l]);
+        dW[l] = vadd(dW[l], vcross(rel, P));
+      }
+    }
+  }
+}
+
+// spring joint jl of the lane (oracle legacy_joints): the anchor impulse imp and the angular
+// term tw (parent: + tw + rp x -imp, child: - tw + rc x imp)
+struct QSpring {
+  v3 imp, tp, tc;  // impulse; parent and child angular terms
+};
+POB_D QSpring qlegacy_joint(csys_t &S, const float *LT, const QBody &b, const int jl, const float act) {
+  const int p = jparent(jl), c = jchild(jl);
+  const v3 axis = QJV(LT, jl, QJ_AXIS);
+  const v3 ref = jl == 0 ? V(-1.0f, 0.0f, 0.0f) : V(0.0f, 0.0f, 1.0f);  // the Ant's (pob_system.cpp)
+  const v3 rp = qrot(QJV(LT, jl, QJ_OFFP), b.q[p]), rc = qrot(QJV(LT, jl, QJ_OFFC), b.q[c]);
+  const v3 dpos = vsub(vadd(b.x[p], rp), vadd(b.x[c], rc));
+  const v3 dvel = vsub(vadd(b.v[p], vcross(b.w[p], rp)), vadd(b.v[c], vcross(b.w[c], rc)));
+  QSpring J;
+  J.imp = vfma(dpos, S.k_spring, vscl(dvel, S.c_spring));
+  const v3 ap = qrot(axis, b.q[p]), ac = qrot(axis, b.q[c]);
+  const v3 fp = qrot(ref, b.q[p]), fc = qrot(ref, b.q[c]);
+  const float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+  const float lo = QJS(LT, jl, QJ_LO), hi = QJS(LT, jl, QJ_HI);
+  float dang = 0.0f;
+  if (psi < lo) dang = lo - psi;
+  else if (psi > hi) dang = hi - psi;
+  v3 tq = vscl(vcross(ap, ac), S.k_spring);
+  tq = vfma(ap, -(S.k_limit * dang), tq);
+  tq = vfma(vsub(b.w[p], b.w[c]), -QJS(LT, jl, QJ_DAMP), tq);
+  const v3 ta = vscl(ap, (dang != 0.0f ? 0.0f : act) * QJS(LT, jl, QJ_STRENGTH));
+  const v3 tw = vsub(tq, ta);
+  J.tp = vadd(vcross(rp, vscl(J.imp, -1.0f)), tw);
+  J.tc = vsub(vcross(rc, J.imp), tw);
+  return J;
+}
+
+template <bool WALLS>
+POB_D void qlegacy_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ],
+                           const Lds &L) {
+  // kinetic
+  {
+    csys_t &S = *launder(Sp);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      b.x[l] = vfma(b.v[l], S.h, b.x[l]);
+      q4 dq = qmul_vq(b.w[l], b.q[l]);
+      q4 q = b.q[l];
+      q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
+      q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
+      b.q[l] = qnormalize(q);
+    }
+  }
+  // joints + actuators (accelerations), summed per body in joint order
+  v3 dv[QNB], dw[QNB];
+  {
+    csys_t &S = *launder(Sp);
+    const QSpring hip = qlegacy_joint(S, LT, b, 0, act[0]);
+    const QSpring knee = qlegacy_joint(S, LT, b, 1, act[1]);
+    const float im0 = S.inv_mass[0], im1 = q_inv_mass(S, LT, 1), im2 = q_inv_mass(S, LT, 2);
+    // torso: parent of the hips (global joints 0, 2, 4, 6 = quad lanes 0..3)
+    v3 v0 = V(0.0f, 0.0f, 0.0f), w0 = v0;
+    v0 = vfma(quad_bcast3<0>(hip.imp), -im0, v0); w0 = vadd(w0, quad_bcast3<0>(hip.tp));
+    v0 = vfma(quad_bcast3<1>(hip.imp), -im0, v0); w0 = vadd(w0, quad_bcast3<1>(hip.tp));
+    v0 = vfma(quad_bcast3<2>(hip.imp), -im0, v0); w0 = vadd(w0, quad_bcast3<2>(hip.tp));
+    v0 = vfma(quad_bcast3<3>(hip.imp), -im0, v0); w0 = vadd(w0, quad_bcast3<3>(hip.tp));
+    dv[0] = v0; dw[0] = w0;
+    // aux: child of the hip, then parent of the knee; lower leg: child of the knee
+    dv[1] = vfma(knee.imp, -im1, vfma(hip.imp, im1, V(0.0f, 0.0f, 0.0f)));
+    dw[1] = vadd(vadd(V(0.0f, 0.0f, 0.0f), hip.tc), knee.tp);
+    dv[2] = vfma(knee.imp, im2, V(0.0f, 0.0f, 0.0f));
+    dw[2] = vadd(V(0.0f, 0.0f, 0.0f), knee.tc);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      const v3 v = b.v[l], w = b.w[l];
+      b.v[l] = V(FMA(S.lin_damp, v.x, (dv[l].x + 0.0f) * S.h), FMA(S.lin_damp, v.y, (dv[l].y + 0.0f) * S.h),
+                 FMA(S.lin_damp, v.z, (dv[l].z + S.gz) * S.h));
+      b.w[l] = V(FMA(S.ang_damp, w.x, dw[l].x * S.h), FMA(S.ang_damp, w.y, dw[l].y * S.h),
+                 FMA(S.ang_damp, w.z, dw[l].z * S.h));
+    }
+  }
+  // collisions: velocity impulses at the post-kinetic pose
+  QContacts ct;
+  qdetect<WALLS>(Sp, LT, WT, b, ct);
+  v3 dV[QNB], dW[QNB];
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
+  qlegacy_contacts(Sp, LT, b, ct, dV, dW);
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) {
+    b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
+    L.set3(QL_CV(l), vadd(L.get3(QL_CV(l)), dV[l]));
+    L.set3(QL_CA(l), vadd(L.get3(QL_CA(l)), dW[l]));
+  }
+}

@@ -56,6 +56,10 @@ struct pob_sys {
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
   float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
   float friction, s_pos, half_s_ang;
+  // legacy spring dynamics (pob_params.legacy_spring; brax <= 0.0.12): joint stiffness, spring
+  // damping, limit strength, Baumgarte rate (baumgarte_erp * substeps / dt)
+  int legacy;
+  float k_spring, c_spring, k_limit, erp;
   // default_qp rows of the frozen bodies (index >= 9)
   float frozen_pos[POB_MAXB][3];
   // env parameters (float32 as the reference's jnp scalars)

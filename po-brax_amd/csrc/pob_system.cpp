@@ -101,6 +101,7 @@ void default_params(pob_params &p) {
   p.tag_dying_cost = -1.0f;
   p.action_repeat = 1;
   p.solver_scale_pos = 0.6f; p.solver_scale_ang = 0.2f;
+  p.legacy_spring = 0;
 }
 
 // Returns an error message or nullptr.  grid (GA) is filled separately by the caller.
@@ -124,6 +125,12 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
   s.friction = 1.0f;
   s.s_pos = p.solver_scale_pos;
   s.half_s_ang = 0.5f * p.solver_scale_ang;
+  if (p.legacy_spring != 0 && p.legacy_spring != 1) return "legacy_spring must be 0 or 1";
+  // legacy spring config (notebooks/ant_tag.ipynb:449: stiffness 18000, springDamping 80, no
+  // limitStrength = stiffness, baumgarteErp 0.1); oracle orc_env_create
+  s.legacy = p.legacy_spring;
+  s.k_spring = 18000.0f; s.c_spring = 80.0f; s.k_limit = 18000.0f;
+  s.erp = (float)(f32d(0.1) * sub / dt);
   for (int i = 0; i < POB_NDYN; ++i) s.inv_mass[i] = 1.0f / (float)kMass[i];
   for (int j = 0; j < POB_NJ; ++j) {
     const double *J = kJoint[j];

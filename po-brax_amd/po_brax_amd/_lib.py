@@ -21,7 +21,7 @@ RESET_GYM, RESET_OWN = 0, 1
 KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 QP_F32, QP_F16 = 0, 1
 MIX_MAX = 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class pob_params(C.Structure):
@@ -36,7 +36,7 @@ class pob_params(C.Structure):
         ("tag_target_step", C.c_float), ("tag_min_spawn_distance", C.c_float),
         ("tag_cage_xy", C.c_float * 2), ("tag_dying_cost", C.c_float),
         ("action_repeat", C.c_int), ("solver_scale_pos", C.c_float), ("solver_scale_ang", C.c_float),
-        ("qp_storage", C.c_int),
+        ("qp_storage", C.c_int), ("legacy_spring", C.c_int),
     ]
 
 

@@ -58,7 +58,11 @@ class AntHeavenHellEnv(PoBraxEnv):
 
 
 def _common_params(params, p: dict) -> None:
-    """Engine-level knobs shared by the three envs (PBD joint solver scales)."""
+    """Engine-level knobs shared by the envs: PBD joint solver scales, and ``legacy_spring``
+    (as brax's ``Ant(legacy_spring=True)`` [ext]: the brax <= 0.0.12 spring dynamics the
+    notebook trajectory notebooks/ant_tag.ipynb:449 was made with)."""
+    if "legacy_spring" in p:
+        params.legacy_spring = 1 if p.pop("legacy_spring") else 0
     if "solver_scale_pos" in p:
         params.solver_scale_pos = float(p.pop("solver_scale_pos"))
     if "solver_scale_ang" in p:
