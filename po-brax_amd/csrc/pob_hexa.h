@@ -1,0 +1,249 @@
+// pob_hexa.h -- the PBD Ant step with SIXTEEN lanes per environment (gfx950), for batches
+// small enough that one wave per SIMD is all the chip gets (HH B = 4 096 is 512 waves of the
+// eight-lane kernel, half the SIMDs idle) and the step time is one wave's dependency chain.
+//
+// Split: every lane owns ONE body and one side of one joint (lane r = lane & 15 of the env):
+//   r = k       P_hip_k   torso (replica x4)   parent side of joint 2k
+//   r = 7 - k   C_hip_k   Aux k+1              child side of joint 2k
+//   r = 8 + k   P_knee_k  Aux k+1 (replica)    parent side of joint 2k+1
+//   r = 15 - k  C_knee_k  lower leg k          child side of joint 2k+1
+// so a joint's two sides are one row_half_mirror DPP apart (r <-> 7 - r within each half row),
+// an Aux body's two replicas one row_mirror apart (r <-> 15 - r), and the four torso replicas
+// form the row's first DPP quad (the torso sums over the hips are quad broadcasts in joint
+// order, as in the four- and eight-lane kernels).  Each lane integrates, projects and
+// collides its own body only; a joint's scalar work (point constraint, hinge, limit, the
+// actuator torque) runs on both of its lanes from the same exchanged operands, so both sides
+// hold the same bits.  Every value follows the oracle's op order (oracle/pob_oracle.c; the
+// generic joint projection of the eight-lane kernel), so the results are bit-identical to the
+// other kernels'.
+#pragma once
+#include "pob_octet.h"
+
+// per-role table row (16 rows, role r as above), staged in LDS, copied into registers
+#define HT_OFFP 0      // joint: off_p (3) off_c (3) axis (3) ref (3) lim_lo lim_hi jdamp strength
+#define HT_OFFC 3
+#define HT_AXIS 6
+#define HT_REF 9
+#define HT_LO 12
+#define HT_HI 13
+#define HT_DAMP 14
+#define HT_STRENGTH 15
+#define HT_IMP 16      // the joint's parent / child inverse masses
+#define HT_IMC 17
+#define HT_IM 18       // the lane's body: inverse mass, capsule radius, capsule end e0 (3)
+#define HT_R 19
+#define HT_E0 20
+#define HT_OFF 23      // the lane's joint offset (off_p on the parent side, off_c on the child side)
+#define HT_GE 26       // the body's ground contact: end (3), radius, 1.0 if it has one
+#define HT_GR 29
+#define HT_HASG 30
+#define HT_TLO 31      // tan(lim_lo), tan(lim_hi): the actuator gate
+#define HT_THI 32
+#define HT_ISP 33      // 1.0 on the parent side
+#define HT_ISHIP 34    // 1.0 for a hip joint
+#define HT_FLOATS POB_HEX_FLOATS
+#define HT_TAB_FLOATS (16 * HT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
+#define HTV(T, f) V((T)[(f)], (T)[(f) + 1], (T)[(f) + 2])
+
+// lane r <-> 7 - r (half row): a joint's two sides
+POB_D float hx_pair(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xf, 0xf, true));  // row_half_mirror
+}
+// lane r <-> 15 - r (row): an Aux body's two replicas
+POB_D float hx_mirror(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, true));  // row_mirror
+}
+POB_D v3 hx_pair3(v3 a) { return V(hx_pair(a.x), hx_pair(a.y), hx_pair(a.z)); }
+POB_D v3 hx_mirror3(v3 a) { return V(hx_mirror(a.x), hx_mirror(a.y), hx_mirror(a.z)); }
+POB_D q4 hx_pair4(q4 q) {
+  q4 r; r.w = hx_pair(q.w); r.x = hx_pair(q.x); r.y = hx_pair(q.y); r.z = hx_pair(q.z); return r;
+}
+POB_D v3 vsel3(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+POB_D q4 qsel(bool c, q4 a, q4 b) {
+  q4 r; r.w = c ? a.w : b.w; r.x = c ? a.x : b.x; r.y = c ? a.y : b.y; r.z = c ? a.z : b.z; return r;
+}
+
+struct HBody {
+  v3 x, v, w;
+  q4 q;
+};
+
+struct HContacts {
+  float gpen;  // ground contact (torso and lower legs; -1 otherwise)
+  v3 gpe;      // its sphere centre x + rotate(end, q)
+  float pen;   // deepest wall contact of the body's capsule
+  v3 n, pe;
+  bool sel;
+};
+
+// Contact detection of a collide substep on one lane: the body's ground contact and its
+// deepest wall contact over the walls whose grown box (pob_sys::wall_lo/hi) holds the body
+// centre -- exact: a culled pair has every capsule point farther than r from the wall box,
+// penetration < 0, and the strict ">" of the deepest-contact search keeps the oracle's
+// (wall, end) order.  (Per-body boxes would not shorten the walk: the wave iterates over the
+// most walls any of its lanes is near, a lower leg's.)
+template <bool WALLS>
+POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
+  ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
+  ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
+  uint32_t m = 0u;
+  if (WALLS) {
+#ifdef POB_EXP_NO_WALLS
+    const int nw = 0;  // timing experiment only
+#else
+    const int nw = S.n_walls;
+#endif
+    for (int w = 0; w < nw; ++w) {
+      const bool near = b.x.x <= S.wall_hi[w][0] && b.x.x >= S.wall_lo[w][0] && b.x.y <= S.wall_hi[w][1] &&
+                        b.x.y >= S.wall_lo[w][1];
+      m |= near ? 1u << w : 0u;
+    }
+  }
+  float best = 0.0f;
+  v3 bn = V(0.0f, 0.0f, 0.0f), bpe = bn;
+  bool bsel = false;
+  if (WALLS && __any(m != 0u)) {
+    const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
+    const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
+    const float r = HT[HT_R];
+    const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
+    while (__any(m != 0u)) {
+      const bool on = m != 0u;
+      const int w = on ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      qwall_end(S, WT + POB_WALL_FLOATS * w, pe0, r, T, on, false, best, bn, bsel, bpe);
+      qwall_end(S, WT + POB_WALL_FLOATS * w, pe1, r, T, on, true, best, bn, bsel, bpe);
+    }
+  }
+  ct.pen = best;
+  ct.n = bn;
+  ct.sel = bsel;
+  ct.pe = bpe;
+}
+
+// One XPBD substep on an env's sixteen lanes (see the header comment for the split).
+template <bool WALLS>
+POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, const float act, v3 &cv, v3 &ca,
+                        const bool COLLIDE) {
+  const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
+  const bool torso = isP && hip, leg = !isP && !hip;
+  const v3 px = b.x;
+  const q4 pq = b.q;
+  // 1. acceleration level: the joint's torque tt (actuator + damping) on both of its lanes
+  {
+    const q4 qo = hx_pair4(b.q);
+    const v3 wo = hx_pair3(b.w);
+    const q4 qpj = qsel(isP, b.q, qo), qcj = qsel(isP, qo, b.q);
+    const v3 wpj = vsel3(isP, b.w, wo), wcj = vsel3(isP, wo, b.w);
+    const v3 axis = HTV(HT, HT_AXIS);
+    const v3 a = qrot(axis, qpj);
+    const bool in = actuator_inside(qpj, qcj, hip, axis, HT[HT_TLO], HT[HT_THI]);
+    const v3 t = vscl(a, (in ? act : 0.0f) * HT[HT_STRENGTH]);
+    const v3 d = vscl(vsub(wpj, wcj), HT[HT_DAMP]);
+    const v3 tt = vadd(t, d);
+    const v3 tm = hx_mirror3(tt);  // the other Aux replica's joint torque
+    // torso: (((0 - t0) - t2) - t4) - t6 over the row's first quad; Aux: (0 + t_hip) - t_knee;
+    // lower leg: 0 + t_knee
+    const v3 t0 = quad_bcast3<0>(tt), t2 = quad_bcast3<1>(tt), t4 = quad_bcast3<2>(tt), t6 = quad_bcast3<3>(tt);
+    const v3 dwt = vsub(vsub(vsub(vsub(V(0.0f, 0.0f, 0.0f), t0), t2), t4), t6);
+    const v3 dwa = vsub(vadd(V(0.0f, 0.0f, 0.0f), hip ? tt : tm), hip ? tm : tt);
+    const v3 dwl = vadd(V(0.0f, 0.0f, 0.0f), tt);
+    const v3 dw = torso ? dwt : (leg ? dwl : dwa);
+    const v3 v = b.v, w = b.w;
+    b.v = V(FMA(S.lin_damp, v.x, 0.0f * S.h), FMA(S.lin_damp, v.y, 0.0f * S.h), FMA(S.lin_damp, v.z, S.gz * S.h));
+    b.w = V(FMA(S.ang_damp, w.x, dw.x * S.h), FMA(S.ang_damp, w.y, dw.y * S.h), FMA(S.ang_damp, w.z, dw.z * S.h));
+    // 2. kinetic
+    b.x = vfma(b.v, S.h, b.x);
+    const q4 dq = qmul_vq(b.w, b.q);
+    q4 q = b.q;
+    q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
+    q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
+    b.q = qnormalize(q);
+  }
+  // 3. position projection
+  HContacts ct;
+  {
+    v3 DX, DA;
+    {
+      // the joint (oracle joints_position, the eight-lane kernel's generic form): each lane
+      // rotates its own body's vectors, the partner's come over the pair DPP
+      const m3 R = qmat(b.q);
+      const v3 ro = mrot_xy(R, HTV(HT, HT_OFF));
+      const v3 ao = mrot(R, HTV(HT, HT_AXIS)), fo = mrot(R, HTV(HT, HT_REF));
+      const v3 xo = hx_pair3(b.x), rx = hx_pair3(ro), ax = hx_pair3(ao), fx = hx_pair3(fo);
+      const v3 xpj = vsel3(isP, b.x, xo), xcj = vsel3(isP, xo, b.x);
+      const v3 rp = vsel3(isP, ro, rx), rc = vsel3(isP, rx, ro);
+      const v3 ap = vsel3(isP, ao, ax), ac = vsel3(isP, ax, ao);
+      const v3 fp = vsel3(isP, fo, fx), fc = vsel3(isP, fx, fo);
+      const float imp = HT[HT_IMP], imc = HT[HT_IMC];
+      const v3 d = vsub(vadd(xcj, rc), vadd(xpj, rp));
+      const float L2 = vdot(d, d);
+      v3 P = V(0.0f, 0.0f, 0.0f), xp = P, xc = P;
+      if (L2 > 0.0f) {
+        const v3 ep = vcross(rp, d), ec = vcross(rc, d);
+        const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
+        const float k = POB_DIV(L2 * S.s_pos, den);
+        P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
+      }
+      const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
+      const float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      float dl = 0.0f;
+      if (psi < HT[HT_LO]) dl = psi - HT[HT_LO];
+      else if (psi > HT[HT_HI]) dl = psi - HT[HT_HI];
+      const v3 s = vadd(Pa, vscl(ap, dl * S.half_s_ang));
+      const v3 tp = vadd(xp, s), tc = vadd(xc, s);
+      // torso: the four hips' parent terms in joint order (the row's first quad)
+      const float imp0 = S.inv_mass[0];
+      v3 dxt = V(0.0f, 0.0f, 0.0f), dat = dxt;
+      dxt = vfma(quad_bcast3<0>(P), imp0, dxt); dat = vadd(dat, quad_bcast3<0>(tp));
+      dxt = vfma(quad_bcast3<1>(P), imp0, dxt); dat = vadd(dat, quad_bcast3<1>(tp));
+      dxt = vfma(quad_bcast3<2>(P), imp0, dxt); dat = vadd(dat, quad_bcast3<2>(tp));
+      dxt = vfma(quad_bcast3<3>(P), imp0, dxt); dat = vadd(dat, quad_bcast3<3>(tp));
+      // Aux: the hip's child term, then the knee's parent term (each replica sends its P
+      // and its own side's term over the row mirror)
+      const v3 Pm = hx_mirror3(P), Tm = hx_mirror3(isP ? tp : tc);
+      const float ima = HT[HT_IM];
+      const v3 Phip = hip ? P : Pm, Pknee = hip ? Pm : P;
+      const v3 Thip = hip ? tc : Tm, Tknee = hip ? Tm : tp;
+      const v3 dxa = vfma(Pknee, ima, vfma(Phip, -ima, V(0.0f, 0.0f, 0.0f)));
+      const v3 daa = vadd(vsub(V(0.0f, 0.0f, 0.0f), Thip), Tknee);
+      // lower leg: the knee's child term
+      const v3 dxl = vfma(P, -imc, V(0.0f, 0.0f, 0.0f));
+      const v3 dal = vsub(V(0.0f, 0.0f, 0.0f), tc);
+      DX = torso ? dxt : (leg ? dxl : dxa);
+      DA = torso ? dat : (leg ? dal : daa);
+    }
+    if (COLLIDE) {
+      hdetect<WALLS>(S, HT, WT, b, ct);
+      const float im = HT[HT_IM];
+      if (ct.gpen > 0.0f) oground_position(S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
+      if (ct.pen > 0.0f) owall_position(S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+    }
+    b.x = vadd(b.x, DX);
+    qadd_half(b.q, qmul_vq(DA, b.q), 1.0f);
+  }
+  // 4. velocity projection
+  b.q = qnormalize(b.q);
+  b.v = vscl(vsub(b.x, px), S.inv_h);
+  {
+    const q4 dq = qmul(b.q, qinv(pq));
+    const float k2 = 2.0f * S.inv_h;
+    const float kw = dq.w >= 0.0f ? k2 : -k2;
+    b.w = V(dq.x * kw, dq.y * kw, dq.z * kw);
+  }
+  // 5. velocity-level contacts (ground first, then wall: the oracle's per-body order)
+  if (COLLIDE) {
+    v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
+    const float im = HT[HT_IM];
+    if (ct.gpen > 0.0f)
+      ocontact_vel_one(S, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+    if (ct.pen > 0.0f) {
+      const v3 e0 = HTV(HT, HT_E0);
+      const v3 e = ct.sel ? V(-e0.x, -e0.y, -e0.z) : e0;
+      ocontact_vel_one(S, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
+    }
+    b.v = vadd(b.v, dV); b.w = vadd(b.w, dW);
+    cv = vadd(cv, dV);
+    ca = vadd(ca, dW);
+  }
+}

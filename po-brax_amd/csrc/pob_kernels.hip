@@ -24,6 +24,7 @@
 #include "../../include/pob.h"
 #include "pob_quad.h"
 #include "pob_octet.h"
+#include "pob_hexa.h"
 #include "pob_physics.h"
 
 namespace pob {
@@ -524,6 +525,27 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
 #ifdef POB_EXP_TIMING
 #define POB_TS_WAVES 65536
 __device__ unsigned long long pob_ts_buf[POB_TS_WAVES * 8];  // timing experiment only
+#define POB_TS_DECL() unsigned long long pob_ts[6]
+#define POB_TS(i) pob_ts[i] = __builtin_amdgcn_s_memtime()
+#define POB_TS_WRITE()                                                                   \
+  do {                                                                                   \
+    POB_TS(5);                                                                           \
+    if ((threadIdx.x & 63) == 0) {                                                       \
+      unsigned hwid, xcc;                                                                \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));                 \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                 \
+      const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);      \
+      if (w < POB_TS_WAVES) {                                                            \
+        unsigned long long *r = pob_ts_buf + w * 8;                                      \
+        r[0] = hwid; r[1] = xcc;                                                         \
+        for (int i = 0; i < 6; ++i) r[2 + i] = pob_ts[i];                                \
+      }                                                                                  \
+    }                                                                                    \
+  } while (0)
+#else
+#define POB_TS_DECL() ((void)0)
+#define POB_TS(i) ((void)0)
+#define POB_TS_WRITE() ((void)0)
 #endif
 template <int KIND, typename QT, bool LEG = false>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
@@ -531,12 +553,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
                           const float *legtab) {
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x & 63;
-#ifdef POB_EXP_TIMING
-  unsigned long long pob_ts[6];  // timing experiment only
-#define POB_TS(i) pob_ts[i] = __builtin_amdgcn_s_memtime()
-#else
-#define POB_TS(i) ((void)0)
-#endif
+  POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
   POB_TS(0);
   float *stg = lds + ((int)threadIdx.x >> 6) * POB_STAGE_FLOATS;  // this wave's region
   const Lds Ls{stg, 64, lane};
@@ -827,21 +844,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     const unsigned long long m = __ballot(act_lane && k == 0 && done != 0.0f);
     if (m != 0ull && lane == 0) atomicOr(out.any_done, 1u);
   }
-#ifdef POB_EXP_TIMING
-  POB_TS(5);
-  if ((threadIdx.x & 63) == 0) {
-    unsigned hwid, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w < POB_TS_WAVES) {
-      unsigned long long *r = pob_ts_buf + w * 8;
-      r[0] = hwid; r[1] = xcc;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) r[2 + i] = pob_ts[i];
-    }
-  }
-#endif
+  POB_TS_WRITE();
 }
 
 template <int KIND, typename QT>
@@ -935,6 +938,8 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
                                                  const float *__restrict__ act, const StatePtrs out,
                                                  const uint32_t flags, const int L) {
   static_assert(KIND != POB_MIXED, "the eight-lane kernel runs one env kind per launch");
+  POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
+  POB_TS(0);
   __shared__ float stg[POB_OSTAGE_FLOATS];
   __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
@@ -1006,6 +1011,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     }
   }
   (void)NMAX;
+  POB_TS(1);
 
   // ---- physics (10 substeps in registers + the lane's LDS slots)
   float jang = 0.0f, jvel = 0.0f;
@@ -1058,6 +1064,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     }
   }
   wave_lds_sync();  // every LDS read of the physics slots is done: the region is staging now
+  POB_TS(2);
 
   // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
   float done = 0.0f;
@@ -1127,6 +1134,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     wave_lds_sync();
   }
 
+  POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
 #pragma unroll
@@ -1155,6 +1163,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     wave_lds_sync();
   }
 
+  POB_TS(4);
   // ---- per-env tail (A_0): frozen rows, first_*, scalar outputs
   if (act_lane && lane0) {
     if (reset_rows) {
@@ -1184,7 +1193,258 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     const unsigned long long mk = __ballot(act_lane && lane0 && done != 0.0f);
     if (mk != 0ull && lane == 0) atomicOr(out.any_done, 1u);
   }
+  POB_TS_WRITE();
 }
+
+// ----------------------------------------------------------- step, sixteen lanes per env
+// The same fused step with SIXTEEN lanes per env (pob_hexa.h): one wave = 4 envs, one wave per
+// block; lane r of an env owns one body and one side of one joint (P_hip_r / C_hip_(7-r) /
+// P_knee_(r-8) / C_knee_(15-r)).  Lane 0 (P_hip_0, the torso) runs the per-env POMDP tail.
+#define POB_HSTAGE_FLOATS (OL_FLOATS * 64)
+template <int KIND, typename QT>
+__global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, const StatePtrs in,
+                                                 const float *__restrict__ act, const StatePtrs out,
+                                                 const uint32_t flags, const int L) {
+  static_assert(KIND != POB_MIXED, "the sixteen-lane kernel runs one env kind per launch");
+  POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
+  POB_TS(0);
+  __shared__ float stg[POB_HSTAGE_FLOATS];
+  __shared__ __attribute__((aligned(16))) float htab[HT_TAB_FLOATS];
+  csys_t *Sp = (csys_t *)(size_t)sysp;
+  {
+    const __attribute__((address_space(4))) float *src = &Sp->hex[0][0];
+    for (int i = (int)threadIdx.x; i < 16 * HT_FLOATS; i += 64) htab[i] = src[i];
+    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
+    for (int i = (int)threadIdx.x; i < POB_MAXW * POB_WALL_FLOATS; i += 64) htab[16 * HT_FLOATS + i] = wsrc[i];
+    __syncthreads();
+  }
+  csys_t &S = *Sp;
+  const int lane = (int)threadIdx.x;
+  const int r = lane & 15;
+  const bool hip = r < 8, isP = r < 4 || (r >= 8 && r < 12);
+  const int k = r < 4 ? r : (r < 8 ? 7 - r : (r < 12 ? r - 8 : 15 - r));  // the leg
+  const int jown = hip ? 2 * k : 2 * k + 1;                                 // the lane's joint
+  const int g = hip ? (isP ? 0 : 2 * k + 1) : (isP ? 2 * k + 1 : 2 * k + 2);  // its body
+  // the lane that writes the body's rows: the torso's lane 0, an Aux's child side, a lower leg
+  const bool canon = r == 0 || (hip && !isP) || (!hip && !isP);
+  float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
+#pragma unroll
+  for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
+  const float *WT = htab + 16 * HT_FLOATS;
+  const Lds Ls{stg, 64, lane};
+  const int b_first = (int)blockIdx.x * 4;
+  const int le = lane >> 4;
+  const int b = b_first + le;
+  const int nenv = B - b_first < 4 ? B - b_first : 4;
+  const bool act_lane = b < B;
+  const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
+  constexpr int sh = obs_shift(KIND);
+  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  const bool lane0 = r == 0;  // P_hip_0: the env's POMDP tail
+
+  // ---- state load: coalesced loads of the 4 envs' rows into LDS (pairs of arrays), then
+  // every lane picks its body; per-lane loads when the qp pointers are not aligned
+  HBody bd;
+  if ((flags & POB_F_STAGED) && 4 * N * 7 <= POB_HSTAGE_FLOATS) {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int c0 = 3, c1 = pr == 0 ? 4 : 3;
+      const int n0 = nenv * N * c0, n1 = nenv * N * c1;
+      stage_load<QT>(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, stg, lane);
+      stage_load<QT>(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, stg + n0, lane);
+      wave_lds_sync();
+      if (act_lane) {
+        const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
+        if (pr == 0) {
+          bd.x = V(s0[0], s0[1], s0[2]);
+          bd.q.w = s1[0]; bd.q.x = s1[1]; bd.q.y = s1[2]; bd.q.z = s1[3];
+        } else {
+          bd.v = V(s0[0], s0[1], s0[2]);
+          bd.w = V(s1[0], s1[1], s1[2]);
+        }
+      }
+      wave_lds_sync();
+    }
+  } else if (act_lane) {
+    bd.x = ld3<QT>(in.pos, r3 + 3 * g);
+    bd.q = ld4<QT>(in.rot, r4 + 4 * g);
+    bd.v = ld3<QT>(in.vel, r3 + 3 * g);
+    bd.w = ld3<QT>(in.ang, r3 + 3 * g);
+  }
+  POB_TS(1);
+
+  // ---- physics (10 substeps in registers)
+  float jang = 0.0f, jvel = 0.0f;
+  v3 cvl = V(0.0f, 0.0f, 0.0f), cal = cvl;
+  TaskOut t;
+  if (act_lane) {
+    const float xb = bd.x.x;
+    const float a = act[(size_t)b * POB_NJ + jown];
+    const int iters = Sp->substeps / 2;
+#if defined(POB_EXP_NO_COLLIDE)
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+#elif defined(POB_EXP_NO_PHYSICS)
+    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+#else
+#pragma nounroll
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+#endif
+    {  // joint angle / velocity obs of the lane's joint (a3), on both of its lanes
+      const q4 qo = hx_pair4(bd.q);
+      const v3 wo = hx_pair3(bd.w);
+      const q4 qp = qsel(isP, bd.q, qo), qc = qsel(isP, qo, bd.q);
+      const v3 wp = vsel3(isP, bd.w, wo), wc = vsel3(isP, wo, bd.w);
+      const v3 ap = qrot(HTV(HT, HT_AXIS), qp);
+      const v3 ref = HTV(HT, HT_REF);
+      const v3 fp = qrot(ref, qp), fc = qrot(ref, qc);
+      jang = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      jvel = vdot(vsub(wc, wp), ap);
+    }
+    // the bodies' contact velocity sums for the stock ant's contact cost
+    Ls.set3(0, cvl);
+    wave_lds_sync();
+    if (lane0) {
+      float steps = in.steps ? in.steps[b] : 0.0f;
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
+      t.steps = steps;
+      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+      t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
+      if (KIND == POB_ANT) {
+        // contact rows 0..8 = torso, then Aux k (lane 7 - k) and lower leg k (lane 15 - k)
+        t.ctrl = ant_ctrl_cost(act + (size_t)b * POB_NJ);
+        float sc = ant_contact_add(0.0f, cvl);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sc = ant_contact_add(sc, Ls.get3_lane(0, lane + 7 - q));
+          sc = ant_contact_add(sc, Ls.get3_lane(0, lane + 15 - q));
+        }
+        t.contact = 0.0005f * sc;
+      }
+    }
+  }
+  wave_lds_sync();  // every LDS read of the physics slots is done: the region is staging now
+  POB_TS(2);
+
+  // ---- obs rows: assembled in the wave's region (P envs per pass), stored coalesced
+  float done = 0.0f;
+  t.ga_done_quad = false;
+  const bool ga_quad = KIND == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
+  GaQuad gq;
+  if (ga_quad && act_lane && r < 4) ga_quad_objects<QT>(S, in, r3, bd.x, bd.q, r, out.pos, gq, t);
+  const int P = POB_HSTAGE_FLOATS / D < 4 ? POB_HSTAGE_FLOATS / D : 4;
+  for (int p0 = 0; p0 < nenv; p0 += P) {
+    const int pn = nenv - p0 < P ? nenv - p0 : P;
+    if (act_lane && le >= p0 && le < p0 + pn) {
+      float *o = stg + (le - p0) * D;
+      if (isP) {
+        o[sh + 7 + jown] = jang;
+        o[sh + 21 + jown] = jvel;
+      }
+      // cfrc rows from the body's writing lane; the frozen bodies' zero rows over the 16 lanes
+      float *oc = o + (29 + sh);
+      if (canon) {
+        oc[3 * g] = clip1(cvl.x); oc[1 + 3 * g] = clip1(cvl.y); oc[2 + 3 * g] = clip1(cvl.z);
+        oc[3 * N + 3 * g] = clip1(cal.x); oc[1 + 3 * N + 3 * g] = clip1(cal.y); oc[2 + 3 * N + 3 * g] = clip1(cal.z);
+      }
+      for (int q = 3 * POB_NDYN + r; q < 3 * N; q += 16) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+      if (lane0) {
+        if (sh == 0) { o[0] = bd.x.x; o[1] = bd.x.y; }
+        o[sh + 2] = bd.x.z;
+        o[sh + 3] = bd.q.w; o[sh + 4] = bd.q.x; o[sh + 5] = bd.q.y; o[sh + 6] = bd.q.z;
+        o[sh + 15] = bd.v.x; o[sh + 16] = bd.v.y; o[sh + 17] = bd.v.z;
+        o[sh + 18] = bd.w.x; o[sh + 19] = bd.w.y; o[sh + 20] = bd.w.z;
+        if (out.pos != in.pos) {  // functional mode: carry the frozen rows over
+          for (int i = POB_NDYN; i < N; ++i) {
+            if (!(ga_quad && i >= 11)) cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+            cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+            cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+            cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
+          }
+        }
+      }
+      if (ga_quad && r < 4) ga_quad_scatter(S, gq, r, o + 29 + 6 * N);
+      if (lane0) {
+        task_step<KIND, QT>(S, in, b, r3, N, bd.x, bd.q, out.pos, o, flags, L, t);
+        done = t.done;
+      }
+      done = __shfl(done, lane & ~15);  // the env's done to its sixteen lanes
+      // AutoResetWrapper: the row of a reset env is first_obs (written last)
+      if (lane0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+        wave_lds_sync();
+        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+      }
+    }
+    wave_lds_sync();
+    float *dst = out.obs + (size_t)(b_first + p0) * D;
+    const int n = pn * D;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      const int n4 = n >> 2;
+      for (int i = lane; i < n4; i += 64) reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(stg)[i];
+      for (int i = 4 * n4 + lane; i < n; i += 64) dst[i] = stg[i];
+    } else {
+      for (int i = lane; i < n; i += 64) dst[i] = stg[i];
+    }
+    wave_lds_sync();
+  }
+
+  POB_TS(3);
+  // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
+  const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#pragma unroll
+  for (int arr = 0; arr < 4; ++arr) {
+    const int c = arr == 1 ? 4 : 3;
+    if (act_lane && canon) {
+      float *o = stg + (le * POB_NDYN + g) * c;
+      if (reset_rows) {
+        const float *F = arr == 0 ? in.first_pos : (arr == 1 ? in.first_rot : (arr == 2 ? in.first_vel : in.first_ang));
+        const size_t src = (arr == 1 ? r4 : r3) + (size_t)g * c;
+        for (int q = 0; q < c; ++q) o[q] = Q<QT>::ld(F, src + q);
+      } else if (arr == 0) { o[0] = bd.x.x; o[1] = bd.x.y; o[2] = bd.x.z; }
+      else if (arr == 1) { o[0] = bd.q.w; o[1] = bd.q.x; o[2] = bd.q.y; o[3] = bd.q.z; }
+      else if (arr == 2) { o[0] = bd.v.x; o[1] = bd.v.y; o[2] = bd.v.z; }
+      else { o[0] = bd.w.x; o[1] = bd.w.y; o[2] = bd.w.z; }
+    }
+    wave_lds_sync();
+    if (arr == 1) stage_store_dyn<QT, 4>(out.rot, (size_t)b_first * N * 4, N, nenv, stg, lane);
+    else stage_store_dyn<QT, 3>(arr == 0 ? out.pos : (arr == 2 ? out.vel : out.ang), (size_t)b_first * N * 3, N, nenv,
+                                stg, lane);
+    wave_lds_sync();
+  }
+
+  POB_TS(4);
+  // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
+  if (act_lane && lane0) {
+    if (reset_rows) {
+      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
+      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
+    }
+    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
+      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
+      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
+      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
+      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
+    }
+    out.reward[b] = t.reward;
+    out.done[b] = t.done;
+    if (out.steps) out.steps[b] = t.steps;
+    if (out.truncation) out.truncation[b] = t.trunc;
+    if (out.m0) out.m0[b] = t.m0;
+    if (out.m1) out.m1[b] = t.m1;
+    if (out.m2) out.m2[b] = t.m2;
+    out.rng[2 * b] = t.rng0;
+    out.rng[2 * b + 1] = t.rng1;
+  }
+  if (out.any_done) {
+    const unsigned long long mk = __ballot(act_lane && lane0 && done != 0.0f);
+    if (mk != 0ull && lane == 0) atomicOr(out.any_done, 1u);
+  }
+  POB_TS_WRITE();
+}
+
 
 // ----------------------------------------------------------------------------- reset
 // System.default_qp forward kinematics (a4): child.rot = parent.rot * axis_angle(axis, q),
@@ -1719,6 +1979,22 @@ static int octet_max_batch() {
   const char *e = getenv("POB_OCTET_MAX_B");
   return e ? atoi(e) : 16384;
 }
+// sixteen lanes per env up to this batch (POB_HEXA_MAX_B overrides; 0 disables)
+static int hexa_max_batch() {
+  const char *e = getenv("POB_HEXA_MAX_B");
+  return e ? atoi(e) : 8192;
+}
+template <typename QT>
+static void launch_step_hex(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
+                            const StatePtrs &po, uint32_t flags, int L) {
+  const dim3 g((unsigned)((B + 3) / 4)), b(64);
+  switch (kind) {
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_hex<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_hex<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_hex<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_hex<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+  }
+}
 template <typename QT>
 static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
                             const StatePtrs &po, uint32_t flags, int L) {
@@ -1870,8 +2146,11 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();  // legacy: lane quads only
-  if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch();  // legacy: lane quads only
+  const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();
+  if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (hex) launch_step_hex<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);
   else launch_step_quad<float>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);

@@ -31,6 +31,8 @@
 #define POB_TAB_FLOATS (4 * POB_LEG_FLOATS + POB_MAXW * POB_WALL_FLOATS)
 // per-role rows of the eight-lanes-per-env kernel (pob_octet.h: OT_* offsets)
 #define POB_OCT_FLOATS 40
+// per-role rows of the sixteen-lanes-per-env kernel (pob_hexa.h: HT_* offsets)
+#define POB_HEX_FLOATS 36
 
 struct pob_sys {
   int kind, N, D, n_obj;
@@ -70,6 +72,7 @@ struct pob_sys {
   float leg[4][POB_LEG_FLOATS];  // gathered copies of the per-leg rows above
   float wall_row[POB_MAXW][POB_WALL_FLOATS];  // the walls again, one row each (follows leg)
   float oct[8][POB_OCT_FLOATS];  // eight-lane kernel: rows A_0..A_3 (hips), B_0..B_3 (knees)
+  float hex[16][POB_HEX_FLOATS];  // sixteen-lane kernel: role rows (pob_hexa.h)
   int oct_ok;         // the Ant pattern the eight-lane kernel assumes holds (torso sphere)
   float ctrl_dt;      // sys.config.dt (float32 proto field): stock ant forward reward
   int qp_f16;         // qp stored as binary16 (pob_params.qp_storage)

@@ -324,6 +324,31 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     O[36] = A ? 0.0f : 1.0f;
     O[37] = s.tan_lo[j]; O[38] = s.tan_hi[j];
   }
+  // sixteen-lane kernel rows (pob_hexa.h): role r = k (P_hip_k: torso), 7 - k (C_hip_k: Aux),
+  // 8 + k (P_knee_k: Aux), 15 - k (C_knee_k: lower leg); the joint's row plus the lane's body
+  for (int r = 0; r < 16; ++r) {
+    const bool hip = r < 8, isP = r < 4 || (r >= 8 && r < 12);
+    const int k = r < 4 ? r : (r < 8 ? 7 - r : (r < 12 ? r - 8 : 15 - r));
+    const int j = hip ? 2 * k : 2 * k + 1;
+    const int body = hip ? (isP ? 0 : 2 * k + 1) : (isP ? 2 * k + 1 : 2 * k + 2);
+    float *H = s.hex[r];
+    for (int i = 0; i < POB_HEX_FLOATS; ++i) H[i] = 0.0f;
+    for (int c = 0; c < 3; ++c) {
+      H[c] = s.off_p[j][c]; H[3 + c] = s.off_c[j][c]; H[6 + c] = s.axis[j][c]; H[9 + c] = s.ref[j][c];
+      H[20 + c] = s.cap_end[body][0][c];
+      H[23 + c] = isP ? s.off_p[j][c] : s.off_c[j][c];
+    }
+    H[12] = s.lim_lo[j]; H[13] = s.lim_hi[j]; H[14] = s.jdamp[j]; H[15] = s.strength[j];
+    H[16] = s.inv_mass[hip ? 0 : 2 * k + 1]; H[17] = s.inv_mass[hip ? 2 * k + 1 : 2 * k + 2];
+    H[18] = s.inv_mass[body]; H[19] = s.cap_r[body];
+    const int g = body == 0 ? 0 : (body == 2 * k + 2 ? k + 1 : -1);  // ground collider of the body
+    if (g >= 0) {
+      for (int c = 0; c < 3; ++c) H[26 + c] = s.ground_end[g][c];
+      H[29] = s.ground_r[g]; H[30] = 1.0f;
+    }
+    H[31] = s.tan_lo[j]; H[32] = s.tan_hi[j];
+    H[33] = isP ? 1.0f : 0.0f; H[34] = hip ? 1.0f : 0.0f;
+  }
   s.oct_ok = s.torso_point;
   return nullptr;
 }

@@ -1,11 +1,12 @@
 """GPU parity at the BASELINE.json batch sizes, on the launch paths the bench takes.
 
-``pob_step`` runs the eight-lanes-per-env kernel (``k_step_oct``) for B <= 16 384 and the
-four-lane kernel (``k_step_quad``) above -- with one-wave (64-thread) blocks when the
-eight-lane kernel is disabled (``POB_OCTET_MAX_B=0``) and B <= 4 096, 256-thread blocks
-otherwise; the mixed launch is always the four-lane kernel in 256-thread blocks.  The
-small-batch parity tests (test_gpu_parity.py, B <= 512) take the eight-lane path, so this
-file checks, against the CPU oracle (OpenMP over envs):
+``pob_step`` runs the sixteen-lanes-per-env kernel (``k_step_hex``) for B <= 8 192, the
+eight-lane kernel (``k_step_oct``) for B <= 16 384 and the four-lane kernel (``k_step_quad``)
+above -- with one-wave (64-thread) blocks when the smaller-batch kernels are disabled
+(``POB_HEXA_MAX_B=0``, ``POB_OCTET_MAX_B=0``) and B <= 4 096, 256-thread blocks otherwise; the
+mixed launch is always the four-lane kernel in 256-thread blocks.  The small-batch parity
+tests (test_gpu_parity.py, B <= 512) take the sixteen-lane path, so this file checks, against
+the CPU oracle (OpenMP over envs):
 
 * the headline config: AntHeavenHell B = 65 536 (config 1 of the bench),
 * AntTag B = 65 536 (config 4's total batch on one GPU), AntGather B = 16 384 (config 3),
@@ -68,11 +69,26 @@ def test_per_step_parity_bench_sizes(name, B):
 
 @pytest.mark.parametrize("B", [64, 4097])
 def test_per_step_parity_four_lane_small(monkeypatch, B):
-    """The four-lane kernel at small batches (eight-lane kernel disabled): one-wave blocks
-    (B = 64) and 256-thread blocks with a one-env tail wave (B = 4 097)."""
+    """The four-lane kernel at small batches (sixteen- and eight-lane kernels disabled):
+    one-wave blocks (B = 64) and 256-thread blocks with a one-env tail wave (B = 4 097)."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "0")
     monkeypatch.setenv("POB_OCTET_MAX_B", "0")
     for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
         _per_step(name, B, seed=B)
+
+
+@pytest.mark.parametrize("B", [61, 4097])
+def test_per_step_parity_eight_lane_small(monkeypatch, B):
+    """The eight-lane kernel at small batches (sixteen-lane kernel disabled), ragged tails."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "0")
+    for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
+        _per_step(name, B, seed=B + 1)
+
+
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 8192), ("ant_tag", 8192), ("ant_gather", 8191), ("ant", 8190)])
+def test_per_step_parity_sixteen_lane(name, B):
+    """The sixteen-lane kernel at its largest batches (config 4's per-GPU TAG batch)."""
+    _per_step(name, B, seed=5)
 
 
 def _prefix_identical(Ba, Bb, env_a=None, env_b=None):
@@ -100,8 +116,15 @@ def test_octet_quad_switch_prefix_identical():
     _prefix_identical(16384, 16385)
 
 
+def test_hexa_octet_switch_prefix_identical():
+    """The first 8 192 envs of a B = 8 193 run (eight-lane kernel) equal a B = 8 192 run
+    (sixteen-lane kernel) bit for bit, fp32 and fp16 storage, for every kind."""
+    _prefix_identical(8192, 8193)
+
+
 def test_quad_block_switch_prefix_identical(monkeypatch):
     """Four-lane kernel only: B = 4 097 (256-thread blocks) vs B = 4 096 (one-wave blocks)."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "0")
     monkeypatch.setenv("POB_OCTET_MAX_B", "0")
     _prefix_identical(4096, 4097)
 
