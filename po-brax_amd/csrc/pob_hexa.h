@@ -86,6 +86,10 @@ template <bool WALLS>
 POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
   ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
+  // (both wall loops are unrolled over POB_MAXW with wave-uniform guards, so the walls' boxes
+  // and rows are scalar-table constants the compiler keeps in SGPRs: a runtime wall loop
+  // re-loads them each iteration, one scalar-load round trip per wall -- with four envs per
+  // wave the union of the walls near any lane is as short as the longest per-lane walk)
   uint32_t m = 0u;
   if (WALLS) {
 #ifdef POB_EXP_NO_WALLS
@@ -93,10 +97,13 @@ POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, 
 #else
     const int nw = S.n_walls;
 #endif
-    for (int w = 0; w < nw; ++w) {
-      const bool near = b.x.x <= S.wall_hi[w][0] && b.x.x >= S.wall_lo[w][0] && b.x.y <= S.wall_hi[w][1] &&
-                        b.x.y >= S.wall_lo[w][1];
-      m |= near ? 1u << w : 0u;
+#pragma unroll
+    for (int w = 0; w < POB_MAXW; ++w) {
+      if (w < nw) {
+        const bool near = b.x.x <= S.wall_hi[w][0] && b.x.x >= S.wall_lo[w][0] && b.x.y <= S.wall_hi[w][1] &&
+                          b.x.y >= S.wall_lo[w][1];
+        m |= near ? 1u << w : 0u;
+      }
     }
   }
   float best = 0.0f;
@@ -107,14 +114,17 @@ POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, 
     const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
     const float r = HT[HT_R];
     const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
-    while (__any(m != 0u)) {
-      const bool on = m != 0u;
-      const int w = on ? __builtin_ctz(m) : 0;
-      m &= m - 1u;
-      qwall_end(S, WT + POB_WALL_FLOATS * w, pe0, r, T, on, false, best, bn, bsel, bpe);
-      qwall_end(S, WT + POB_WALL_FLOATS * w, pe1, r, T, on, true, best, bn, bsel, bpe);
+#pragma unroll
+    for (int w = 0; w < POB_MAXW; ++w) {
+      const bool on = ((m >> w) & 1u) != 0u;
+      if (__any(on)) {
+        const auto &R = S.wall_row[w];
+        qwall_end_v(S, R[0], R[1], R[2], R[3], R[4], R[5], pe0, r, T, on, false, best, bn, bsel, bpe);
+        qwall_end_v(S, R[0], R[1], R[2], R[3], R[4], R[5], pe1, r, T, on, true, best, bn, bsel, bpe);
+      }
     }
   }
+  (void)WT;
   ct.pen = best;
   ct.n = bn;
   ct.sel = bsel;

@@ -1245,26 +1245,23 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   // ---- state load: coalesced loads of the 4 envs' rows into LDS (pairs of arrays), then
   // every lane picks its body; per-lane loads when the qp pointers are not aligned
   HBody bd;
-  if ((flags & POB_F_STAGED) && 4 * N * 7 <= POB_HSTAGE_FLOATS) {
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const int c0 = 3, c1 = pr == 0 ? 4 : 3;
-      const int n0 = nenv * N * c0, n1 = nenv * N * c1;
-      stage_load<QT>(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, stg, lane);
-      stage_load<QT>(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, stg + n0, lane);
-      wave_lds_sync();
-      if (act_lane) {
-        const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
-        if (pr == 0) {
-          bd.x = V(s0[0], s0[1], s0[2]);
-          bd.q.w = s1[0]; bd.q.x = s1[1]; bd.q.y = s1[2]; bd.q.z = s1[3];
-        } else {
-          bd.v = V(s0[0], s0[1], s0[2]);
-          bd.w = V(s1[0], s1[1], s1[2]);
-        }
-      }
-      wave_lds_sync();
+  if ((flags & POB_F_STAGED) && 4 * N * 13 <= POB_HSTAGE_FLOATS) {
+    // all four arrays in one round trip (pos | rot | vel | ang of the wave's envs)
+    const int n3 = nenv * N * 3, n4 = nenv * N * 4;
+    stage_load<QT>(in.pos, (size_t)b_first * N * 3, n3, stg, lane);
+    stage_load<QT>(in.rot, (size_t)b_first * N * 4, n4, stg + n3, lane);
+    stage_load<QT>(in.vel, (size_t)b_first * N * 3, n3, stg + n3 + n4, lane);
+    stage_load<QT>(in.ang, (size_t)b_first * N * 3, n3, stg + 2 * n3 + n4, lane);
+    wave_lds_sync();
+    if (act_lane) {
+      const float *sx = stg + (le * N + g) * 3, *sq = stg + n3 + (le * N + g) * 4;
+      const float *sv = stg + n3 + n4 + (le * N + g) * 3, *sw = stg + 2 * n3 + n4 + (le * N + g) * 3;
+      bd.x = V(sx[0], sx[1], sx[2]);
+      bd.q.w = sq[0]; bd.q.x = sq[1]; bd.q.y = sq[2]; bd.q.z = sq[3];
+      bd.v = V(sv[0], sv[1], sv[2]);
+      bd.w = V(sw[0], sw[1], sw[2]);
     }
+    wave_lds_sync();
   } else if (act_lane) {
     bd.x = ld3<QT>(in.pos, r3 + 3 * g);
     bd.q = ld4<QT>(in.rot, r4 + 4 * g);

@@ -111,14 +111,13 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 // contact search: same operations in the same order, but the square root, normal and
 // compare run only when d2 < T = r^2 (1 + 2^-20) (or d2 is NaN).  Exact: d2 >= T gives
 // sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
-POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
-                     bool &bsel, v3 &bpe) {
-  const float2 r01 = *reinterpret_cast<const float2 *>(R);
-  const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
-  const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
-  const float c = r23.x, s = r23.y;
-  const v3 h = V(r45.x, r45.y, S.wall_hz);
-  v3 d = vsub(p, V(r01.x, r01.y, S.wall_cz));
+// (the row's six floats given as values: LDS rows for a per-lane wall walk, the system
+// table's scalars for a wave-uniform one)
+POB_D void qwall_end_v(csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
+                       const float hy, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn, bool &bsel,
+                       v3 &bpe) {
+  const v3 h = V(hx, hy, S.wall_hz);
+  v3 d = vsub(p, V(cx, cy, S.wall_cz));
   float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
   float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
@@ -143,6 +142,13 @@ POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on,
       bpe = p;
     }
   }
+}
+POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
+                     bool &bsel, v3 &bpe) {
+  const float2 r01 = *reinterpret_cast<const float2 *>(R);
+  const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
+  const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
+  qwall_end_v(S, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, p, r, T, on, q1, best, bn, bsel, bpe);
 }
 
 // Contact detection of a collide substep on a lane quad.  Walls: every lane keeps a mask

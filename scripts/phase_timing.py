@@ -23,7 +23,7 @@ for _ in range(5):
     jumpy.random_actions_(key, B, 0, act)
     s = env.step_(s, act)
 torch.cuda.synchronize()
-LPE = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if B <= 16384 else 4)  # lanes per env (octet / quad kernel)
+LPE = int(sys.argv[3]) if len(sys.argv) > 3 else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
 W = (B * LPE + 63) // 64
 buf = np.zeros((W, 8), np.uint64)
 f = _lib.lib.pob_debug_timing
