@@ -249,7 +249,7 @@ def main() -> int:
     ks = kern_ms * 1e-3
     hbm_gbs = bpe * B / ks / 1e9
     tflops = f_ref * B / ks / 1e12
-    kname = "k_step_mixed" if args.env == "mixed" else f"k_step_quad<{args.env}>"
+    kname = "k_step_mixed" if args.env == "mixed" else f"{step_kernel(B)}<{args.env}>"
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TF, "unit": "TFLOP/s",
         "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
@@ -317,6 +317,17 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def step_kernel(B: int) -> str:
+    """The step kernel pob_step launches for a batch of B envs (pob_kernels.hip pob_step:
+    sixteen lanes per env up to POB_HEXA_MAX_B (8 192), eight up to POB_OCTET_MAX_B (16 384),
+    four above)."""
+    if B <= int(os.environ.get("POB_HEXA_MAX_B", "8192")):
+        return "k_step_hex"
+    if B <= int(os.environ.get("POB_OCTET_MAX_B", "16384")):
+        return "k_step_oct"
+    return "k_step_quad"
 
 
 def committed_profile(env: str, B: int, qp: str):

@@ -334,8 +334,27 @@ struct GaQuad {
   int slot[4];   // sensor slot written by this lane's object j (-1: none)
   float val[4];  // and the value
 };
+// The lane's objects' input positions, read from the env's staged pos rows (LDS) during the
+// state load, or loaded here when the load was not staged (pre == nullptr).
 template <typename QT>
-POB_D void ga_quad_objects(csys_t &S, const StatePtrs &in, const size_t r3, const v3 x0, const q4 q0, const int k,
+POB_D void ga_quad_prefetch(csys_t &S, const StatePtrs &in, const size_t r3, const float *srow, const int k,
+                            v3 (&op)[4]) {
+  using QQ = Q<QT>;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int obj = k + 4 * j;
+    op[j] = V(0.0f, 0.0f, 0.0f);
+    if (obj < S.n_obj) {
+      if (srow) op[j] = V(srow[3 * (11 + obj)], srow[3 * (11 + obj) + 1], srow[3 * (11 + obj) + 2]);
+      else {
+        const size_t row = r3 + 3 * (11 + obj);
+        op[j] = V(QQ::ld(in.pos, row), QQ::ld(in.pos, row + 1), QQ::ld(in.pos, row + 2));
+      }
+    }
+  }
+}
+template <typename QT>
+POB_D void ga_quad_objects(csys_t &S, const v3 (&op)[4], const size_t r3, const v3 x0, const q4 q0, const int k,
                            float *opos, GaQuad &g, TaskOut &t) {
   using QQ = Q<QT>;
   const float ori = ga_orientation(q0);
@@ -347,7 +366,7 @@ POB_D void ga_quad_objects(csys_t &S, const StatePtrs &in, const size_t r3, cons
     g.slot[j] = -1; g.val[j] = 0.0f;
     if (obj < S.n_obj) {
       const size_t row = r3 + 3 * (11 + obj);
-      const float ox = QQ::ld(in.pos, row), oy = QQ::ld(in.pos, row + 1), oz = QQ::ld(in.pos, row + 2);
+      const float ox = op[j].x, oy = op[j].y, oz = op[j].z;
       const float dk = dist2d(x0.x, x0.y, ox, oy);
       g.slot[j] = ga_reading_slot(S, obj, ox, oy, dk, ori, g.val[j]);
       const bool c = dk <= S.ga_catch_range;
@@ -722,7 +741,9 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   if (ga_quad && act_lane) {
     // functional mode: the object rows of out.pos are written here (the frozen-row copy
     // below skips them)
-    ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
+    v3 gop[4];
+    ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
+    ga_quad_objects<QT>(S, gop, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
   }
   const int P = POB_STAGE_FLOATS / D < 16 ? POB_STAGE_FLOATS / D : 16;
   for (int p0 = 0; p0 < nenv; p0 += P) {
@@ -895,8 +916,11 @@ POB_D const void *uniform_ptr(const void *p) {
   return (const void *)(size_t)(((uint64_t)hi << 32) | lo);
 }
 
+#ifndef POB_MIXED_MIN_WAVES
+#define POB_MIXED_MIN_WAVES 3  // config 5 runs 2 waves per SIMD: 170 VGPRs, no spills (128: 144 B of scratch, +6 %)
+#endif
 template <typename QT>
-__global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_mixed(const MixArgs A, const uint32_t flags,
+__global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const MixArgs A, const uint32_t flags,
                                                                         const int L) {
   __shared__ float lds[QL_FLOATS * 256];
   __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
@@ -975,8 +999,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   // ---- state load: coalesced loads of the 8 envs' rows into LDS (pairs of arrays), then
   // every lane picks its two bodies; per-lane loads when the qp pointers are not aligned
   OBody bd;
+  v3 gop[4];  // AntGather: this lane's objects' input positions (A lanes)
+  bool gop_ok = false;
   constexpr int NMAX = KIND == POB_HEAVENHELL ? 14 : (KIND == POB_TAG ? 12 : (KIND == POB_ANT ? 10 : POB_MAXB));
   if ((flags & POB_F_STAGED) && 8 * N * 7 <= POB_OSTAGE_FLOATS) {
+    gop_ok = true;
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       const int c0 = 3, c1 = pr == 0 ? 4 : 3;
@@ -984,6 +1011,8 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       stage_load<QT>(pr == 0 ? in.pos : in.vel, (size_t)b_first * N * c0, n0, stg, lane);
       stage_load<QT>(pr == 0 ? in.rot : in.ang, (size_t)b_first * N * c1, n1, stg + n0, lane);
       wave_lds_sync();
+      if (KIND == POB_GATHER && pr == 0 && act_lane && isA && S.n_obj <= POB_GA_QUAD_MAX)
+        ga_quad_prefetch<QT>(S, in, r3, stg + le * N * 3, k, gop);
       if (act_lane) {
 #pragma unroll
         for (int sl = 0; sl < ONB; ++sl) {
@@ -1071,7 +1100,10 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   t.ga_done_quad = false;
   const bool ga_quad = KIND == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
   GaQuad gq;
-  if (ga_quad && act_lane && isA) ga_quad_objects<QT>(S, in, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
+  if (ga_quad && act_lane && isA) {
+    if (!gop_ok) ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
+    ga_quad_objects<QT>(S, gop, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
+  }
   const int P = POB_OSTAGE_FLOATS / D < 8 ? POB_OSTAGE_FLOATS / D : 8;
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
@@ -1245,7 +1277,10 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   // ---- state load: coalesced loads of the 4 envs' rows into LDS (pairs of arrays), then
   // every lane picks its body; per-lane loads when the qp pointers are not aligned
   HBody bd;
+  v3 gop[4];  // AntGather: this lane's objects' input positions (torso lanes)
+  bool gop_ok = false;
   if ((flags & POB_F_STAGED) && 4 * N * 13 <= POB_HSTAGE_FLOATS) {
+    gop_ok = true;
     // all four arrays in one round trip (pos | rot | vel | ang of the wave's envs)
     const int n3 = nenv * N * 3, n4 = nenv * N * 4;
     stage_load<QT>(in.pos, (size_t)b_first * N * 3, n3, stg, lane);
@@ -1253,6 +1288,8 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     stage_load<QT>(in.vel, (size_t)b_first * N * 3, n3, stg + n3 + n4, lane);
     stage_load<QT>(in.ang, (size_t)b_first * N * 3, n3, stg + 2 * n3 + n4, lane);
     wave_lds_sync();
+    if (KIND == POB_GATHER && act_lane && r < 4 && S.n_obj <= POB_GA_QUAD_MAX)
+      ga_quad_prefetch<QT>(S, in, r3, stg + le * N * 3, r, gop);
     if (act_lane) {
       const float *sx = stg + (le * N + g) * 3, *sq = stg + n3 + (le * N + g) * 4;
       const float *sv = stg + n3 + n4 + (le * N + g) * 3, *sw = stg + 2 * n3 + n4 + (le * N + g) * 3;
@@ -1328,7 +1365,10 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   t.ga_done_quad = false;
   const bool ga_quad = KIND == POB_GATHER && S.n_obj <= POB_GA_QUAD_MAX;
   GaQuad gq;
-  if (ga_quad && act_lane && r < 4) ga_quad_objects<QT>(S, in, r3, bd.x, bd.q, r, out.pos, gq, t);
+  if (ga_quad && act_lane && r < 4) {
+    if (!gop_ok) ga_quad_prefetch<QT>(S, in, r3, nullptr, r, gop);
+    ga_quad_objects<QT>(S, gop, r3, bd.x, bd.q, r, out.pos, gq, t);
+  }
   const int P = POB_HSTAGE_FLOATS / D < 4 ? POB_HSTAGE_FLOATS / D : 4;
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
