@@ -100,6 +100,23 @@ template <typename QT> POB_D void st4(float *p, size_t i, q4 q) {
 template <typename QT> POB_D void cpq(float *dst, const float *src, size_t i, int n) {
   for (int k = 0; k < n; ++k) Q<QT>::st(dst, i + k, Q<QT>::ld(src, i + k));
 }
+// body g's four qp rows written by its owner lane: the computed state, or the env's
+// first_qp rows when the AutoResetWrapper resets it (r3 / r4: the env's row offsets)
+template <typename QT>
+POB_D void store_body(const StatePtrs &in, const StatePtrs &out, const size_t r3, const size_t r4, const int g,
+                      const bool reset_rows, const v3 x, const q4 q, const v3 v, const v3 w) {
+  if (reset_rows) {
+    cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
+    cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
+    cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
+    cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
+  } else {
+    st3<QT>(out.pos, r3 + 3 * g, x);
+    st4<QT>(out.rot, r4 + 4 * g, q);
+    st3<QT>(out.vel, r3 + 3 * g, v);
+    st3<QT>(out.ang, r3 + 3 * g, w);
+  }
+}
 
 template <int KIND>
 POB_D int n_bodies(csys_t &S) {
@@ -809,6 +826,16 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#ifdef POB_EXP_DIRECT_STORE
+  if (act_lane) {
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      if (l == 0 && k != 0) continue;
+      store_body<QT>(in, out, r3, r4, qbody_global(l, k), reset_rows, bd.x[l], bd.q[l], bd.v[l], bd.w[l]);
+    }
+  }
+  if (false)
+#endif
 #pragma unroll
   for (int arr = 0; arr < 4; ++arr) {
     const int c = arr == 1 ? 4 : 3;
@@ -1169,6 +1196,16 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#ifdef POB_EXP_DIRECT_STORE
+  if (act_lane) {
+#pragma unroll
+    for (int sl = 0; sl < ONB; ++sl) {
+      if (sl == 0 && !lane0) continue;
+      store_body<QT>(in, out, r3, r4, sl == 0 ? g0 : g1, reset_rows, bd.x[sl], bd.q[sl], bd.v[sl], bd.w[sl]);
+    }
+  }
+  if (false)
+#endif
 #pragma unroll
   for (int arr = 0; arr < 4; ++arr) {
     const int c = arr == 1 ? 4 : 3;
@@ -1428,6 +1465,9 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+#ifdef POB_EXP_DIRECT_STORE
+  if (act_lane && canon) store_body<QT>(in, out, r3, r4, g, reset_rows, bd.x, bd.q, bd.v, bd.w);
+#else
 #pragma unroll
   for (int arr = 0; arr < 4; ++arr) {
     const int c = arr == 1 ? 4 : 3;
@@ -1448,6 +1488,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
                                 stg, lane);
     wave_lds_sync();
   }
+#endif
 
   POB_TS(4);
   // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
@@ -2152,9 +2193,15 @@ int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, voi
   return hip_check(hipGetLastError(), "k_reset launch");
 }
 
-// the coalesced staged state load needs 16-B aligned qp rows and 16 envs' rows of the
-// widest array (rot) to fit the wave's staging area
+// The coalesced LDS-staged state load (POB_F_STAGED) is opt-in (POB_STAGE=1, read at every
+// launch): since the quad / octet / hexa kernels hold every body in its owner lane, per-lane
+// loads of the owned rows (one round trip, no LDS pass, frozen rows never read) are as fast
+// or faster at every batch size and kind -- HH B = 65 536 0.0935 -> 0.0914 ms, GA B = 16 384
+// 0.0766 -> 0.0728 ms, GA B = 65 536 0.132 -> 0.125 ms (profiles/r2q).  Staging needs 16-B
+// aligned qp rows and 16 envs' rows of the widest array (rot) to fit the wave's region.
 static bool can_stage(const pob_env *e, const pob_state *in) {
+  const char *ev = getenv("POB_STAGE");
+  if (!ev || atoi(ev) == 0) return false;
   const uintptr_t m = (uintptr_t)in->pos | (uintptr_t)in->rot | (uintptr_t)in->vel | (uintptr_t)in->ang;
   return (m & 15u) == 0 && 16 * e->sys.N * 4 <= POB_STAGE_FLOATS;
 }

@@ -172,10 +172,40 @@ def test_stock_ant_env_surface():
     assert torch.equal(vel[:, :3], s.qp.vel[:, 0])          # torso velocity
 
 
+@pytest.mark.parametrize("B", [70, 9000, 16400])  # sixteen- / eight- / four-lane kernels, ragged tails
+@pytest.mark.parametrize("qp_dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("name", NAMES)
+def test_staged_load_equals_per_lane_load(name, qp_dtype, B, monkeypatch):
+    """The opt-in LDS-staged state load (POB_STAGE=1) and the default per-lane loads give the
+    same step bit for bit (autoreset chain, three steps, every output field)."""
+    from po_brax_amd import envs
+    env = envs.create(name, batch_size=B, episode_length=2, qp_dtype=qp_dtype)
+    s0 = env.reset(torch.from_numpy(_keys(B, 21)).cuda())
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    acts = [torch.rand((B, 8), device="cuda", generator=gen) * 2 - 1 for _ in range(3)]
+    outs = []
+    for stage in ("0", "1"):
+        monkeypatch.setenv("POB_STAGE", stage)
+        s = s0
+        for a in acts:
+            s = env.step(s, a)
+        torch.cuda.synchronize()
+        outs.append(s)
+    a, b = outs
+    for f in QP:
+        assert torch.equal(getattr(a.qp, f), getattr(b.qp, f)), f
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done)
+    for k in a.aux:
+        if isinstance(a.aux[k], torch.Tensor):
+            assert torch.equal(a.aux[k], b.aux[k]), k
+
+
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather"])
-def test_unaligned_state_uses_fallback_loads(name):
-    """qp tensors that are not 16-B aligned take the per-lane load path (no vector loads);
-    results must equal the aligned (staged) path bit for bit."""
+def test_unaligned_state_uses_fallback_loads(name, monkeypatch):
+    """qp tensors that are not 16-B aligned take the per-lane load path (no vector loads)
+    even with the staged load enabled; results must equal the aligned (staged) path bit for
+    bit."""
+    monkeypatch.setenv("POB_STAGE", "1")
     from po_brax_amd import envs
     B = 70  # ragged: the last wave holds 6 envs
     env = envs.create(name, batch_size=B, episode_length=50)
