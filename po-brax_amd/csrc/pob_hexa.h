@@ -58,10 +58,6 @@ POB_D v3 hx_mirror3(v3 a) { return V(hx_mirror(a.x), hx_mirror(a.y), hx_mirror(a
 POB_D q4 hx_pair4(q4 q) {
   q4 r; r.w = hx_pair(q.w); r.x = hx_pair(q.x); r.y = hx_pair(q.y); r.z = hx_pair(q.z); return r;
 }
-POB_D v3 vsel3(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
-POB_D q4 qsel(bool c, q4 a, q4 b) {
-  q4 r; r.w = c ? a.w : b.w; r.x = c ? a.x : b.x; r.y = c ? a.y : b.y; r.z = c ? a.z : b.z; return r;
-}
 
 struct HBody {
   v3 x, v, w;

@@ -40,6 +40,7 @@ struct pob_env {
   float *d_grid = nullptr;
   uint32_t *d_scratch = nullptr;  // any-done word for pob_reset_where_done without a flag
   int device = 0;
+  int n_cu = 256;  // compute units of the device (SIMDs = 4 x n_cu)
 };
 
 #define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
@@ -99,23 +100,6 @@ template <typename QT> POB_D void st4(float *p, size_t i, q4 q) {
 // copy n qp elements (exact in either storage)
 template <typename QT> POB_D void cpq(float *dst, const float *src, size_t i, int n) {
   for (int k = 0; k < n; ++k) Q<QT>::st(dst, i + k, Q<QT>::ld(src, i + k));
-}
-// body g's four qp rows written by its owner lane: the computed state, or the env's
-// first_qp rows when the AutoResetWrapper resets it (r3 / r4: the env's row offsets)
-template <typename QT>
-POB_D void store_body(const StatePtrs &in, const StatePtrs &out, const size_t r3, const size_t r4, const int g,
-                      const bool reset_rows, const v3 x, const q4 q, const v3 v, const v3 w) {
-  if (reset_rows) {
-    cpq<QT>(out.pos, in.first_pos, r3 + 3 * g, 3);
-    cpq<QT>(out.rot, in.first_rot, r4 + 4 * g, 4);
-    cpq<QT>(out.vel, in.first_vel, r3 + 3 * g, 3);
-    cpq<QT>(out.ang, in.first_ang, r3 + 3 * g, 3);
-  } else {
-    st3<QT>(out.pos, r3 + 3 * g, x);
-    st4<QT>(out.rot, r4 + 4 * g, q);
-    st3<QT>(out.vel, r3 + 3 * g, v);
-    st3<QT>(out.ang, r3 + 3 * g, w);
-  }
 }
 
 template <int KIND>
@@ -232,6 +216,7 @@ struct TaskOut {
   float reward, done, trunc, steps, m0, m1, m2;
   uint32_t rng0, rng1;
   float xb, ctrl, contact;  // stock ant inputs: torso x before the step, costs
+  float ob0, ob1;           // the task's obs entries (HH heaven direction, TAG target xy)
   // AntGather objects already handled by the env's four lanes (ga_quad_objects)
   bool ga_done_quad, ga_any_a, ga_any_b, ga_all_wait;
   int ga_na, ga_nb;
@@ -265,7 +250,7 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     done = reward != 0.0f ? 1.0f : 0.0f;
     const float tx = QQ::ld(ip, r3 + 33);
     const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
-    o[base] = in2 ? sgn : 0.0f;
+    t.ob0 = in2 ? sgn : 0.0f;
     m2 = done;  // metrics['hits']
   } else if (KIND == POB_GATHER) {
     // ant_gather.py:125-150 (obs from pre-relocation positions)
@@ -324,7 +309,7 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     QQ::st(opos, r3 + 30, nx); QQ::st(opos, r3 + 31, ny); QQ::st(opos, r3 + 32, 1.0f);
     rng0 = n0; rng1 = n1;
     const bool vis = dist2d(nx, ny, ax, ay) <= S.tag_visible_radius;
-    o[base] = vis ? nx : 0.0f; o[base + 1] = vis ? ny : 0.0f;
+    t.ob0 = vis ? nx : 0.0f; t.ob1 = vis ? ny : 0.0f;
     const float tag = dist2d(ax, ay, nx, ny) <= S.tag_tag_radius ? 1.0f : 0.0f;
     m0 = tag;
     if (tag > 0.0f) reward = 1.0f;
@@ -433,6 +418,12 @@ POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const i
   else if (kind == POB_TAG) task_step<POB_TAG, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
   else task_step<POB_ANT, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
 }
+// the task's obs entries into the env's obs row (HH: heaven direction, TAG: target xy; the
+// AntGather readings are written by the object pass)
+POB_D void task_obs_write(const int kind, float *o, const int base, const TaskOut &t) {
+  if (kind == POB_HEAVENHELL) o[base] = t.ob0;
+  else if (kind == POB_TAG) { o[base] = t.ob0; o[base + 1] = t.ob1; }
+}
 
 // ------------------------------------------------------------------ step, lane quads
 // Same fused step with FOUR lanes per env (pob_quad.h): lane k owns the torso (replica)
@@ -448,6 +439,12 @@ POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const i
 // buffer for coalesced state I/O while the other waves of the block still run physics.
 #define POB_STAGE_FLOATS (QL_FLOATS * 64)
 POB_D void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// envs per obs pass of a wave's staging region (cap floats, rows of D floats, at most maxe):
+// a multiple of 4 when it is below maxe, so that every pass's rows start 16-B aligned
+POB_D int pass_envs(const int cap, const int D, const int maxe) {
+  const int p = cap / D;
+  return p >= maxe ? maxe : (p >= 4 ? p & ~3 : p);
+}
 
 // Coalesced copy of n_el consecutive qp elements (from element el0) into stg: 16 B (f32)
 // / 8 B (f16) vector loads by all 64 lanes.
@@ -560,21 +557,23 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
 }
 #ifdef POB_EXP_TIMING
 #define POB_TS_WAVES 65536
-__device__ unsigned long long pob_ts_buf[POB_TS_WAVES * 8];  // timing experiment only
-#define POB_TS_DECL() unsigned long long pob_ts[6]
+// per wave: hw id, xcc id, then POB_TS_N stamps (unset stamps are 0)
+#define POB_TS_N 10
+__device__ unsigned long long pob_ts_buf[POB_TS_WAVES * (POB_TS_N + 2)];  // timing experiment only
+#define POB_TS_DECL() unsigned long long pob_ts[POB_TS_N] = {}
 #define POB_TS(i) pob_ts[i] = __builtin_amdgcn_s_memtime()
 #define POB_TS_WRITE()                                                                   \
   do {                                                                                   \
-    POB_TS(5);                                                                           \
+    POB_TS(POB_TS_N - 1);                                                                \
     if ((threadIdx.x & 63) == 0) {                                                       \
       unsigned hwid, xcc;                                                                \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));                 \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                 \
       const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);      \
       if (w < POB_TS_WAVES) {                                                            \
-        unsigned long long *r = pob_ts_buf + w * 8;                                      \
+        unsigned long long *r = pob_ts_buf + w * (POB_TS_N + 2);                         \
         r[0] = hwid; r[1] = xcc;                                                         \
-        for (int i = 0; i < 6; ++i) r[2 + i] = pob_ts[i];                                \
+        for (int i = 0; i < POB_TS_N; ++i) r[2 + i] = pob_ts[i];                         \
       }                                                                                  \
     }                                                                                    \
   } while (0)
@@ -583,6 +582,40 @@ __device__ unsigned long long pob_ts_buf[POB_TS_WAVES * 8];  // timing experimen
 #define POB_TS(i) ((void)0)
 #define POB_TS_WRITE() ((void)0)
 #endif
+// dynamic qp rows of a lane quad's wave: the computed state (or the env's first_qp rows when
+// the AutoResetWrapper resets it) staged in the wave's LDS region and stored coalesced
+template <typename QT>
+__device__ __forceinline__ void quad_store_dyn(const StatePtrs &in, const StatePtrs &out, const QBody &bd,
+                                               const bool act_lane, const int k, const int le, const int b_first,
+                                               const int nenv, const int N, const size_t r3, const size_t r4,
+                                               float *stg, const int lane, const bool reset_rows) {
+#pragma unroll
+  for (int arr = 0; arr < 4; ++arr) {
+    const int c = arr == 1 ? 4 : 3;
+    if (act_lane) {
+#pragma unroll
+      for (int l = 0; l < QNB; ++l) {
+        if (l == 0 && k != 0) continue;
+        const int g = qbody_global(l, k);
+        float *o = stg + (le * POB_NDYN + g) * c;
+        if (reset_rows) {
+          const float *F = arr == 0 ? in.first_pos : (arr == 1 ? in.first_rot : (arr == 2 ? in.first_vel : in.first_ang));
+          const size_t src = (arr == 1 ? r4 : r3) + (size_t)g * c;
+          for (int q = 0; q < c; ++q) o[q] = Q<QT>::ld(F, src + q);
+        } else if (arr == 0) { o[0] = bd.x[l].x; o[1] = bd.x[l].y; o[2] = bd.x[l].z; }
+        else if (arr == 1) { o[0] = bd.q[l].w; o[1] = bd.q[l].x; o[2] = bd.q[l].y; o[3] = bd.q[l].z; }
+        else if (arr == 2) { o[0] = bd.v[l].x; o[1] = bd.v[l].y; o[2] = bd.v[l].z; }
+        else { o[0] = bd.w[l].x; o[1] = bd.w[l].y; o[2] = bd.w[l].z; }
+      }
+    }
+    wave_lds_sync();
+    if (arr == 1) stage_store_dyn<QT, 4>(out.rot, (size_t)b_first * N * 4, N, nenv, stg, lane);
+    else stage_store_dyn<QT, 3>(arr == 0 ? out.pos : (arr == 2 ? out.vel : out.ang), (size_t)b_first * N * 3, N,
+                                nenv, stg, lane);
+    wave_lds_sync();
+  }
+}
+
 template <int KIND, typename QT, bool LEG = false>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
@@ -762,7 +795,34 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
     ga_quad_objects<QT>(S, gop, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
   }
-  const int P = POB_STAGE_FLOATS / D < 16 ? POB_STAGE_FLOATS / D : 16;
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(3);  // timing experiment: the GA objects apart from the obs rows
+#endif
+  // The task tail runs once, before the obs passes (it writes no obs row itself: its entries
+  // come back in t.ob0 / t.ob1), except for AntGather with more objects than the quad pass
+  // handles, whose readings loop writes the row.
+  const bool task_in_pass = kind == POB_GATHER && !ga_quad;
+  if (act_lane && k == 0 && out.pos != in.pos) {
+    // functional mode: carry the frozen rows over before the task tail moves the TAG target
+    // or the AntGather objects (the quad object pass has written those rows already)
+    for (int i = POB_NDYN; i < N; ++i) {
+      if (!(ga_quad && i >= 11)) cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);
+      cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
+      cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
+      cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
+    }
+  }
+  if (!task_in_pass && act_lane) {
+    if (k == 0) {
+      task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, nullptr, flags, L, t);
+      done = t.done;
+    }
+    done = quad_bcast<0>(done);  // the quad's four lanes are active together here
+  }
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(4);
+#endif
+  const int P = pass_envs(POB_STAGE_FLOATS, D, 16);
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
     if (act_lane && le >= p0 && le < p0 + pn) {
@@ -789,27 +849,27 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         o[sh + 3] = bd.q[0].w; o[sh + 4] = bd.q[0].x; o[sh + 5] = bd.q[0].y; o[sh + 6] = bd.q[0].z;
         o[sh + 15] = bd.v[0].x; o[sh + 16] = bd.v[0].y; o[sh + 17] = bd.v[0].z;
         o[sh + 18] = bd.w[0].x; o[sh + 19] = bd.w[0].y; o[sh + 20] = bd.w[0].z;
-        if (out.pos != in.pos) {  // functional mode: carry the frozen rows over (the task
-          for (int i = POB_NDYN; i < N; ++i) {  // tail then moves GA objects / the TAG target)
-            if (!(ga_quad && i >= 11)) cpq<QT>(out.pos, in.pos, r3 + 3 * i, 3);  // (objects: below)
-            cpq<QT>(out.vel, in.vel, r3 + 3 * i, 3);
-            cpq<QT>(out.ang, in.ang, r3 + 3 * i, 3);
-            cpq<QT>(out.rot, in.rot, r4 + 4 * i, 4);
-          }
-        }
       }
       if (ga_quad) ga_quad_scatter(S, gq, k, o + 29 + 6 * N);
-      if (k == 0) {
-        task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
-        done = t.done;
+      if (task_in_pass) {
+        if (k == 0) {
+          task_dispatch<KIND, QT>(S, kind, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
+          done = t.done;
+        }
+        done = quad_bcast<0>(done);  // the quad's four lanes are active together here
+      } else if (k == 0) {
+        task_obs_write(kind, o, 29 + 6 * N, t);
       }
-      done = quad_bcast<0>(done);  // the quad's four lanes are active together here
-      // AutoResetWrapper: the row of a reset env is first_obs (written last, same lane order)
-      if (k == 0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+      // AutoResetWrapper: the row of a reset env is first_obs, copied by the env's four lanes
+      // after every other write of the row (program order within the wave)
+      if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+        for (int q = k; q < D; q += 4) o[q] = in.first_obs[(size_t)b * D + q];
       }
     }
+#ifdef POB_EXP_TIMING_OBS
+    if (p0 == 0) POB_TS(5);
+#endif
     wave_lds_sync();
     float *dst = out.obs + (size_t)(b_first + p0) * D;
     const int n = pn * D;
@@ -821,48 +881,25 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       for (int i = lane; i < n; i += 64) dst[i] = stg[i];
     }
     wave_lds_sync();
-  }
-
-  POB_TS(3);
-  // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
-  const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
-#ifdef POB_EXP_DIRECT_STORE
-  if (act_lane) {
-#pragma unroll
-    for (int l = 0; l < QNB; ++l) {
-      if (l == 0 && k != 0) continue;
-      store_body<QT>(in, out, r3, r4, qbody_global(l, k), reset_rows, bd.x[l], bd.q[l], bd.v[l], bd.w[l]);
-    }
-  }
-  if (false)
+#ifdef POB_EXP_TIMING_OBS
+    if (p0 == 0) POB_TS(6);
 #endif
-#pragma unroll
-  for (int arr = 0; arr < 4; ++arr) {
-    const int c = arr == 1 ? 4 : 3;
-    if (act_lane) {
-#pragma unroll
-      for (int l = 0; l < QNB; ++l) {
-        if (l == 0 && k != 0) continue;
-        const int g = qbody_global(l, k);
-        float *o = stg + (le * POB_NDYN + g) * c;
-        if (reset_rows) {
-          const float *F = arr == 0 ? in.first_pos : (arr == 1 ? in.first_rot : (arr == 2 ? in.first_vel : in.first_ang));
-          const size_t src = (arr == 1 ? r4 : r3) + (size_t)g * c;
-          for (int q = 0; q < c; ++q) o[q] = Q<QT>::ld(F, src + q);
-        } else if (arr == 0) { o[0] = bd.x[l].x; o[1] = bd.x[l].y; o[2] = bd.x[l].z; }
-        else if (arr == 1) { o[0] = bd.q[l].w; o[1] = bd.q[l].x; o[2] = bd.q[l].y; o[3] = bd.q[l].z; }
-        else if (arr == 2) { o[0] = bd.v[l].x; o[1] = bd.v[l].y; o[2] = bd.v[l].z; }
-        else { o[0] = bd.w[l].x; o[1] = bd.w[l].y; o[2] = bd.w[l].z; }
-      }
-    }
-    wave_lds_sync();
-    if (arr == 1) stage_store_dyn<QT, 4>(out.rot, (size_t)b_first * N * 4, N, nenv, stg, lane);
-    else stage_store_dyn<QT, 3>(arr == 0 ? out.pos : (arr == 2 ? out.vel : out.ang), (size_t)b_first * N * 3, N,
-                                nenv, stg, lane);
-    wave_lds_sync();
   }
 
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(7);
+#else
+  POB_TS(3);
+#endif
+  // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets (after
+  // the obs passes: stored before them, HH B = 65 536 measured 0.0922 -> 0.0943 ms)
+  const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
+  quad_store_dyn<QT>(in, out, bd, act_lane, k, le, b_first, nenv, N, r3, r4, stg, lane, reset_rows);
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(8);
+#else
   POB_TS(4);
+#endif
   // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
   if (act_lane && k == 0) {
     if (reset_rows) {  // frozen rows from first_qp
@@ -906,6 +943,21 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
                            (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
+}
+
+// AntGather at most three waves per SIMD (B <= 3 x 16 x SIMDs): the same kernel with the
+// register budget of three waves -- at four its object / sensor / 211-wide obs passes spill
+// (128 B of scratch per lane), and three fit the whole launch anyway (B = 32 768: 0.0998 ->
+// 0.0947 ms, interleaved A/B, profiles/r2t)
+template <typename QT>
+__global__ __launch_bounds__(256, 3) void k_step_quad_ga3(const void *sysp, const int B, const StatePtrs in,
+                                                          const float *__restrict__ act, const StatePtrs out,
+                                                          const uint32_t flags, const int L) {
+  __shared__ float lds[QL_FLOATS * 256];
+  __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
+  stage_leg_table((csys_t *)(size_t)sysp, legtab);
+  step_quad_body<POB_GATHER, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                 (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
 }
 
 // The same fused step with the legacy spring dynamics (pob_params.legacy_spring; pob_quad.h
@@ -983,7 +1035,9 @@ __global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const M
 // The same fused step with EIGHT lanes per env (pob_octet.h) for small batches: one wave =
 // 8 envs, one wave per block.  Lane m of an env: A_m (m < 4: hip joint m, torso + Aux) or
 // B_(7-m) (m >= 4: knee joint, Aux + lower leg).  Lane A_0 runs the per-env POMDP tail.
-#define POB_OSTAGE_FLOATS (OL_FLOATS * 64)
+// (8 AntGather obs rows of the default 8 + 8 objects, 8 x 211 floats, fit: one obs pass)
+#define POB_OSTAGE_FLOATS (27 * 64)
+static_assert(POB_OSTAGE_FLOATS >= OL_FLOATS * 64, "the octet staging region holds the lanes' LDS slots");
 template <int KIND, typename QT>
 __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, const StatePtrs in,
                                                  const float *__restrict__ act, const StatePtrs out,
@@ -1065,6 +1119,12 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       bd.v[sl] = ld3<QT>(in.vel, r3 + 3 * g);
       bd.w[sl] = ld3<QT>(in.ang, r3 + 3 * g);
     }
+    // AntGather: the A lanes' object positions ride along with the state loads (one round
+    // trip; the registers are free at the octet kernel's occupancy)
+    if (KIND == POB_GATHER && isA && S.n_obj <= POB_GA_QUAD_MAX) {
+      ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
+      gop_ok = true;
+    }
   }
   (void)NMAX;
   POB_TS(1);
@@ -1131,7 +1191,10 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     if (!gop_ok) ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
     ga_quad_objects<QT>(S, gop, r3, bd.x[0], bd.q[0], k, out.pos, gq, t);
   }
-  const int P = POB_OSTAGE_FLOATS / D < 8 ? POB_OSTAGE_FLOATS / D : 8;
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(3);  // timing experiment: the GA objects apart from the obs rows
+#endif
+  const int P = pass_envs(POB_OSTAGE_FLOATS, D, 8);
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
     if (act_lane && le >= p0 && le < p0 + pn) {
@@ -1167,6 +1230,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       if (ga_quad && isA) ga_quad_scatter(S, gq, k, o + 29 + 6 * N);
       if (lane0) {
         task_step<KIND, QT>(S, in, b, r3, N, bd.x[0], bd.q[0], out.pos, o, flags, L, t);
+        task_obs_write(KIND, o, 29 + 6 * N, t);
         done = t.done;
       }
       {  // the env's done to all eight lanes: A quad from A_0, B quad via A_0 -> B_0 (lane 7)
@@ -1174,10 +1238,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
         const float d2 = quad_bcast<3>(oct_swap(d1));
         done = isA ? d1 : d2;
       }
-      // AutoResetWrapper: the row of a reset env is first_obs (written last)
-      if (lane0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+      // AutoResetWrapper: the row of a reset env is first_obs, copied by the env's eight lanes
+      // after every other write of the row
+      if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+        for (int q = m; q < D; q += 8) o[q] = in.first_obs[(size_t)b * D + q];
       }
     }
     wave_lds_sync();
@@ -1193,19 +1258,13 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     wave_lds_sync();
   }
 
+#ifdef POB_EXP_TIMING_OBS
+  POB_TS(4);
+#else
   POB_TS(3);
+#endif
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
-#ifdef POB_EXP_DIRECT_STORE
-  if (act_lane) {
-#pragma unroll
-    for (int sl = 0; sl < ONB; ++sl) {
-      if (sl == 0 && !lane0) continue;
-      store_body<QT>(in, out, r3, r4, sl == 0 ? g0 : g1, reset_rows, bd.x[sl], bd.q[sl], bd.v[sl], bd.w[sl]);
-    }
-  }
-  if (false)
-#endif
 #pragma unroll
   for (int arr = 0; arr < 4; ++arr) {
     const int c = arr == 1 ? 4 : 3;
@@ -1232,7 +1291,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     wave_lds_sync();
   }
 
+#ifndef POB_EXP_TIMING_OBS
   POB_TS(4);
+#endif
   // ---- per-env tail (A_0): frozen rows, first_*, scalar outputs
   if (act_lane && lane0) {
     if (reset_rows) {
@@ -1341,6 +1402,11 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     bd.q = ld4<QT>(in.rot, r4 + 4 * g);
     bd.v = ld3<QT>(in.vel, r3 + 3 * g);
     bd.w = ld3<QT>(in.ang, r3 + 3 * g);
+    // AntGather: lanes 0..3's object positions ride along with the state loads
+    if (KIND == POB_GATHER && r < 4 && S.n_obj <= POB_GA_QUAD_MAX) {
+      ga_quad_prefetch<QT>(S, in, r3, nullptr, r, gop);
+      gop_ok = true;
+    }
   }
   POB_TS(1);
 
@@ -1406,7 +1472,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     if (!gop_ok) ga_quad_prefetch<QT>(S, in, r3, nullptr, r, gop);
     ga_quad_objects<QT>(S, gop, r3, bd.x, bd.q, r, out.pos, gq, t);
   }
-  const int P = POB_HSTAGE_FLOATS / D < 4 ? POB_HSTAGE_FLOATS / D : 4;
+  const int P = pass_envs(POB_HSTAGE_FLOATS, D, 4);
   for (int p0 = 0; p0 < nenv; p0 += P) {
     const int pn = nenv - p0 < P ? nenv - p0 : P;
     if (act_lane && le >= p0 && le < p0 + pn) {
@@ -1440,13 +1506,15 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
       if (ga_quad && r < 4) ga_quad_scatter(S, gq, r, o + 29 + 6 * N);
       if (lane0) {
         task_step<KIND, QT>(S, in, b, r3, N, bd.x, bd.q, out.pos, o, flags, L, t);
+        task_obs_write(KIND, o, 29 + 6 * N, t);
         done = t.done;
       }
       done = __shfl(done, lane & ~15);  // the env's done to its sixteen lanes
-      // AutoResetWrapper: the row of a reset env is first_obs (written last)
-      if (lane0 && (flags & POB_F_AUTORESET) && done != 0.0f) {
+      // AutoResetWrapper: the row of a reset env is first_obs, copied by the env's sixteen
+      // lanes after every other write of the row
+      if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = 0; q < D; ++q) o[q] = in.first_obs[(size_t)b * D + q];
+        for (int q = r; q < D; q += 16) o[q] = in.first_obs[(size_t)b * D + q];
       }
     }
     wave_lds_sync();
@@ -1465,9 +1533,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   POB_TS(3);
   // ---- dynamic qp rows: computed state, or first_qp when the AutoResetWrapper resets
   const bool reset_rows = (flags & POB_F_AUTORESET) && done != 0.0f;
-#ifdef POB_EXP_DIRECT_STORE
-  if (act_lane && canon) store_body<QT>(in, out, r3, r4, g, reset_rows, bd.x, bd.q, bd.v, bd.w);
-#else
 #pragma unroll
   for (int arr = 0; arr < 4; ++arr) {
     const int c = arr == 1 ? 4 : 3;
@@ -1488,7 +1553,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
                                 stg, lane);
     wave_lds_sync();
   }
-#endif
 
   POB_TS(4);
   // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
@@ -2085,8 +2149,8 @@ static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, con
   }
 }
 template <typename QT>
-static void launch_step_quad(int kind, bool legacy, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
-                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
+static void launch_step_quad(int kind, bool legacy, int n_cu, hipStream_t st, const void *sp, int B,
+                             const StatePtrs &pi, const float *act, const StatePtrs &po, uint32_t flags, int L) {
   // Batches of at most one wave per CU launch one-wave blocks, so each wave gets a CU (its
   // scalar unit, LDS and instruction cache) to itself instead of four waves sharing 1/4 of
   // the CUs; larger batches use 256-thread blocks (the kernel is block-size agnostic)
@@ -2099,6 +2163,10 @@ static void launch_step_quad(int kind, bool legacy, hipStream_t st, const void *
       case POB_TAG: hipLaunchKernelGGL((k_step_legacy<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
       default: hipLaunchKernelGGL((k_step_legacy<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
     }
+    return;
+  }
+  if (kind == POB_GATHER && (size_t)4 * B <= (size_t)3 * 64 * 4 * n_cu) {
+    hipLaunchKernelGGL((k_step_quad_ga3<QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
     return;
   }
   switch (kind) {
@@ -2129,6 +2197,8 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   e->params = prm;
   if (const char *msg = pob::build_system(kind, prm, e->sys)) { delete e; return fail(POB_EINVAL, msg); }
   int rc = hip_check(hipGetDevice(&e->device), "hipGetDevice");
+  if (!rc) rc = hip_check(hipDeviceGetAttribute(&e->n_cu, hipDeviceAttributeMultiprocessorCount, e->device),
+                          "hipDeviceGetAttribute(CUs)");
   if (rc) { delete e; return rc; }
   rc = hip_check(hipMalloc(&e->d_scratch, 64), "hipMalloc(scratch)");
   if (rc) { delete e; return rc; }
@@ -2236,8 +2306,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   else if (hex) launch_step_hex<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
-  else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);
-  else launch_step_quad<float>(e->sys.kind, e->sys.legacy, st, sp, B, pi, act, po, flags, episode_length);
+  else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
+  else launch_step_quad<float>(e->sys.kind, e->sys.legacy, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");
 }
 
@@ -2368,6 +2438,6 @@ int pob_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, fl
 // timing experiment only: per wave [HW_ID, XCC_ID, t0..t5] of the last step launch
 extern "C" __attribute__((visibility("default"))) int pob_debug_timing(unsigned long long *host, int waves) {
   if (waves > POB_TS_WAVES) waves = POB_TS_WAVES;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pob_ts_buf), sizeof(unsigned long long) * 8 * waves) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pob_ts_buf), sizeof(unsigned long long) * (POB_TS_N + 2) * waves) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -76,6 +76,12 @@ POB_D v3 vload(const float *p) { return V(p[0], p[1], p[2]); }
 // min(max(x, -h), h) for h >= 0 as one v_med3_f32 (equal to the oracle's fminf(fmaxf(..))
 // for every non-NaN x; no canonicalising moves)
 POB_D float clamp_sym(float x, float h) { return __builtin_amdgcn_fmed3f(x, -h, h); }
+// component-wise selects of vectors / quaternions: a ternary on the structs may be lowered
+// to a select of their addresses, i.e. a private array in scratch memory
+POB_D v3 vsel3(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+POB_D q4 qsel(bool c, q4 a, q4 b) {
+  q4 r; r.w = c ? a.w : b.w; r.x = c ? a.x : b.x; r.y = c ? a.y : b.y; r.z = c ? a.z : b.z; return r;
+}
 
 // brax.math.rotate(v, q) = 2 (u.v) u + (s^2 - u.u) v + 2 s (u x v)
 POB_D v3 qrot(v3 v, q4 q) {

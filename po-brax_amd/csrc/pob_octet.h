@@ -87,8 +87,8 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
 template <bool WALLS>
 POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslot1, const OBody &b, OContacts &ct) {
   {
-    const v3 xg = gslot1 ? b.x[1] : b.x[0];
-    const q4 qg = gslot1 ? b.q[1] : b.q[0];
+    const v3 xg = vsel3(gslot1, b.x[1], b.x[0]);
+    const q4 qg = qsel(gslot1, b.q[1], b.q[0]);
     ct.gpe = vadd(xg, qrot_xy(OTV(OT, OT_G), qg));
     ct.gpen = OT[OT_G + 3] - ct.gpe.z;
   }
@@ -329,10 +329,10 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       const v3 t0 = quad_bcast3<0>(tt), t2 = quad_bcast3<1>(tt), t4 = quad_bcast3<2>(tt), t6 = quad_bcast3<3>(tt);
       const v3 torso = vsub(vsub(vsub(vsub(V(0.0f, 0.0f, 0.0f), t0), t2), t4), t6);
       // aux (A slot 1, B slot 0): (0 + t_hip) - t_knee; B slot 1 (leg): 0 + t_knee
-      const v3 thip = isA ? tt : tpart, tknee = isA ? tpart : tt;
+      const v3 thip = vsel3(isA, tt, tpart), tknee = vsel3(isA, tpart, tt);
       const v3 aux = vsub(vadd(V(0.0f, 0.0f, 0.0f), thip), tknee);
-      dw[0] = isA ? torso : aux;
-      dw[1] = isA ? aux : vadd(V(0.0f, 0.0f, 0.0f), tt);
+      dw[0] = vsel3(isA, torso, aux);
+      dw[1] = vsel3(isA, aux, vadd(V(0.0f, 0.0f, 0.0f), tt));
     }
     csys_t &S = *OLAUNDER(Sp);
 #pragma unroll
@@ -368,8 +368,8 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       const v3 tp = vadd(J.xp, J.s), tc = vadd(J.xc, J.s);
       const v3 Pp = oct_swap3(J.P);
       const v3 Tp = oct_swap3(isA ? tc : tp);
-      const v3 Phip = isA ? J.P : Pp, Pknee = isA ? Pp : J.P;
-      const v3 Thip = isA ? tc : Tp, Tknee = isA ? Tp : tp;
+      const v3 Phip = vsel3(isA, J.P, Pp), Pknee = vsel3(isA, Pp, J.P);
+      const v3 Thip = vsel3(isA, tc, Tp), Tknee = vsel3(isA, Tp, tp);
       // aux (inverse mass im_aux: A's child = B's parent): hip child term, then knee parent term
       const float imaux = isA ? imc : imp;
       const v3 dx_aux = vfma(Pknee, imaux, vfma(Phip, -imaux, V(0.0f, 0.0f, 0.0f)));
@@ -384,8 +384,8 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       // leg (B slot 1): knee child term
       const v3 dx_leg = vfma(J.P, -imc, V(0.0f, 0.0f, 0.0f));
       const v3 da_leg = vsub(V(0.0f, 0.0f, 0.0f), tc);
-      DX[0] = isA ? dxt : dx_aux; DA[0] = isA ? dat : da_aux;
-      DX[1] = isA ? dx_aux : dx_leg; DA[1] = isA ? da_aux : da_leg;
+      DX[0] = vsel3(isA, dxt, dx_aux); DA[0] = vsel3(isA, dat, da_aux);
+      DX[1] = vsel3(isA, dx_aux, dx_leg); DA[1] = vsel3(isA, da_aux, da_leg);
     }
     if (COLLIDE) {
       odetect<WALLS>(Sp, OT, WT, gslot1, b, ct);

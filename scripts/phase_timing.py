@@ -25,24 +25,25 @@ for _ in range(5):
 torch.cuda.synchronize()
 LPE = int(sys.argv[3]) if len(sys.argv) > 3 else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
 W = (B * LPE + 63) // 64
-buf = np.zeros((W, 8), np.uint64)
+NTS = 10  # POB_TS_N
+buf = np.zeros((W, NTS + 2), np.uint64)
 f = _lib.lib.pob_debug_timing
 f.argtypes = [C.c_void_p, C.c_int]
 assert f(buf.ctypes.data, W) == 0
 hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:].astype(np.int64)
+cols = [i for i in range(NTS) if (t[:, i] != 0).all()]  # the stamps this build records
+t = t[:, cols]
 d = np.diff(t, axis=1)
-names = ["load", "phys", "obs", "dyn", "tail"]
-print(f"{NAME} B={B} waves={W}")
-for i, n in enumerate(names):
-    print(f"{n:5s} ticks p0 {np.percentile(d[:, i], 0):9.0f} p50 {np.percentile(d[:, i], 50):9.0f} "
+print(f"{NAME} B={B} waves={W} stamps={cols}")
+for i in range(d.shape[1]):
+    n = f"{cols[i]}->{cols[i + 1]}"
+    print(f"{n:6s} ticks p0 {np.percentile(d[:, i], 0):9.0f} p50 {np.percentile(d[:, i], 50):9.0f} "
           f"p90 {np.percentile(d[:, i], 90):9.0f} max {d[:, i].max():9.0f}")
-tot = t[:, 5] - t[:, 0]
+tot = t[:, -1] - t[:, 0]
 print(f"total p0 {tot.min()} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 for x in np.unique(xcc):
     m = xcc == x
     st = t[m, 0] - t[m, 0].min()
-    en = t[m, 5] - t[m, 0].min()
-    print(f"xcc {x}: waves {m.sum()} start spread p50 {np.median(st):.0f} max {st.max()} end max {en.max()} "
-          f"phys p50 {np.median(d[m, 1]):.0f}")
-simd = (hw >> 4) & 3
+    en = t[m, -1] - t[m, 0].min()
+    print(f"xcc {x}: waves {m.sum()} start spread p50 {np.median(st):.0f} max {st.max()} end max {en.max()}")
 print("start offset vs duration corr", np.corrcoef((t[:, 0] - t[:, 0].min()), tot)[0, 1])

@@ -62,8 +62,11 @@ def _per_step(name, B, T=4, L=3, seed=0):
 
 @pytest.mark.parametrize("name,B", [("ant_heavenhell", 65536), ("ant_tag", 65536), ("ant_gather", 16384),
                                     ("ant_heavenhell", 16385), ("ant_heavenhell", 4096), ("ant_heavenhell", 4097),
-                                    ("ant_gather", 4097), ("ant_tag", 4097), ("ant", 4097)])
+                                    ("ant_gather", 4097), ("ant_tag", 4097), ("ant", 4097),
+                                    ("ant_gather", 16385), ("ant_gather", 49153)])
 def test_per_step_parity_bench_sizes(name, B):
+    """(AntGather on the four-lane kernel: B <= 3 waves per SIMD takes the three-wave build
+    k_step_quad_ga3, B = 49 153 the four-wave one on a 256-CU device.)"""
     _per_step(name, B)
 
 
