@@ -31,7 +31,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "po-brax_amd"))
+# (POB_PKG_ROOT: another checkout's package directory, for interleaved A/B runs of two builds)
+sys.path.insert(0, os.environ.get("POB_PKG_ROOT", os.path.join(ROOT, "po-brax_amd")))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 4
+#define POB_ABI_VERSION 5
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -110,6 +110,14 @@ typedef struct pob_state {
   uint32_t *rng;                /* info['rng'] (B,2) */
   float *first_pos, *first_rot, *first_vel, *first_ang, *first_obs; /* AutoResetWrapper (optional) */
   uint32_t *any_done;           /* optional: step ORs 1 into *any_done when any env is done */
+  /* Optional typed copies of step outputs, written by pob_step / pob_step_mixed next to the
+   * float32 fields so that the caller needs no conversion kernels for the reference's dtypes
+   * (ABI v5): AntTag's bool done (done != 0 as bytes 0/1, ant_tag.py:127) and int32 truncation
+   * (EpisodeWrapper on a bool done [ext]); AntGather's int32 apples / bombs counts
+   * (ant_gather.py:147-148) as (int32) m0 / m1.  The reset entry points ignore them. */
+  uint8_t *done_u8;
+  int32_t *trunc_i32;
+  int32_t *m0_i32, *m1_i32;
 } pob_state;
 
 typedef struct pob_env pob_env;

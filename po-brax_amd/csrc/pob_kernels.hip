@@ -49,13 +49,16 @@ struct pob_env {
 // ---------------------------------------------------------------------------- state
 #define POB_STATE_FIELDS(X)                                                                    \
   X(pos) X(rot) X(vel) X(ang) X(obs) X(reward) X(done) X(steps) X(truncation) X(m0) X(m1) X(m2) \
-  X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done)
+  X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done) X(done_u8) X(trunc_i32) \
+  X(m0_i32) X(m1_i32)
 
 struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
   uint32_t *rng;
   float *first_pos, *first_rot, *first_vel, *first_ang, *first_obs;
   uint32_t *any_done;
+  uint8_t *done_u8;  // typed copies of step outputs (optional, pob.h)
+  int32_t *trunc_i32, *m0_i32, *m1_i32;
 };
 static StatePtrs to_ptrs(const pob_state &s) {
   StatePtrs p;
@@ -100,6 +103,52 @@ template <typename QT> POB_D void st4(float *p, size_t i, q4 q) {
 // copy n qp elements (exact in either storage)
 template <typename QT> POB_D void cpq(float *dst, const float *src, size_t i, int n) {
   for (int k = 0; k < n; ++k) Q<QT>::st(dst, i + k, Q<QT>::ld(src, i + k));
+}
+// The same copy by the L lanes of an env's lane group (this lane: j), U loads in flight per
+// lane before their stores: a done env's first_qp / first_obs rows cost a few memory round
+// trips instead of one per element on one lane (a wave holding a done env was otherwise the
+// launch's last by up to 9 us)
+template <typename QT, int L, int U>
+POB_D void group_cpq(float *dst, const float *src, const size_t i, const int n, const int j) {
+  for (int q0 = j; q0 < n; q0 += L * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = q0 + L * u < n ? Q<QT>::ld(src, i + q0 + L * u) : 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q0 + L * u < n) Q<QT>::st(dst, i + q0 + L * u, v[u]);
+  }
+}
+// float rows (obs): dst may be the wave's LDS staging row
+template <int L, int U>
+POB_D void group_copy(float *dst, const float *src, const int n, const int j) {
+  for (int q0 = j; q0 < n; q0 += L * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = q0 + L * u < n ? src[q0 + L * u] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q0 + L * u < n) dst[q0 + L * u] = v[u];
+  }
+}
+// a done env's frozen qp rows from first_qp, and (functional mode with distinct first_*
+// buffers) the first_qp / first_obs carry-over, by the env's L lanes (j: this lane)
+template <typename QT, int L, int U = 4>
+POB_D void tail_copies(const StatePtrs &in, const StatePtrs &out, const uint32_t flags, const bool reset_rows,
+                       const int b, const int N, const int D, const size_t r3, const size_t r4, const int j) {
+  if (reset_rows) {
+    group_cpq<QT, L, U>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN), j);
+    group_cpq<QT, L, U>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN), j);
+    group_cpq<QT, L, U>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN), j);
+    group_cpq<QT, L, U>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN), j);
+  }
+  if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
+    group_cpq<QT, L, U>(out.first_pos, in.first_pos, r3, 3 * N, j);
+    group_cpq<QT, L, U>(out.first_vel, in.first_vel, r3, 3 * N, j);
+    group_cpq<QT, L, U>(out.first_ang, in.first_ang, r3, 3 * N, j);
+    group_cpq<QT, L, U>(out.first_rot, in.first_rot, r4, 4 * N, j);
+    group_copy<L, U>(out.first_obs + (size_t)b * D, in.first_obs + (size_t)b * D, D, j);
+  }
 }
 
 template <int KIND>
@@ -418,6 +467,13 @@ POB_D void task_dispatch(csys_t &S, const int kind, const StatePtrs &in, const i
   else if (kind == POB_TAG) task_step<POB_TAG, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
   else task_step<POB_ANT, QT>(S, in, b, r3, N, x0, q0, opos, o, flags, L, t);
 }
+// the typed copies of the step outputs the caller asked for (pob.h, ABI v5)
+POB_D void write_typed(const StatePtrs &out, const int b, const TaskOut &t) {
+  if (out.done_u8) out.done_u8[b] = t.done != 0.0f ? 1 : 0;
+  if (out.trunc_i32) out.trunc_i32[b] = (int32_t)t.trunc;
+  if (out.m0_i32) out.m0_i32[b] = (int32_t)t.m0;
+  if (out.m1_i32) out.m1_i32[b] = (int32_t)t.m1;
+}
 // the task's obs entries into the env's obs row (HH: heaven direction, TAG: target xy; the
 // AntGather readings are written by the object pass)
 POB_D void task_obs_write(const int kind, float *o, const int base, const TaskOut &t) {
@@ -559,8 +615,11 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
 #define POB_TS_WAVES 65536
 // per wave: hw id, xcc id, then POB_TS_N stamps (unset stamps are 0)
 #define POB_TS_N 10
-__device__ unsigned long long pob_ts_buf[POB_TS_WAVES * (POB_TS_N + 2)];  // timing experiment only
-#define POB_TS_DECL() unsigned long long pob_ts[POB_TS_N] = {}
+#define POB_TS_ROW (POB_TS_N + 4)  // + the wave's start / end on the device-wide 100 MHz clock
+__device__ unsigned long long pob_ts_buf[POB_TS_WAVES * POB_TS_ROW];  // timing experiment only
+#define POB_TS_DECL() \
+  unsigned long long pob_ts[POB_TS_N] = {}; \
+  const unsigned long long pob_rt0 = __builtin_amdgcn_s_memrealtime()
 #define POB_TS(i) pob_ts[i] = __builtin_amdgcn_s_memtime()
 #define POB_TS_WRITE()                                                                   \
   do {                                                                                   \
@@ -571,9 +630,10 @@ __device__ unsigned long long pob_ts_buf[POB_TS_WAVES * (POB_TS_N + 2)];  // tim
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                 \
       const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);      \
       if (w < POB_TS_WAVES) {                                                            \
-        unsigned long long *r = pob_ts_buf + w * (POB_TS_N + 2);                         \
+        unsigned long long *r = pob_ts_buf + w * POB_TS_ROW;                             \
         r[0] = hwid; r[1] = xcc;                                                         \
         for (int i = 0; i < POB_TS_N; ++i) r[2 + i] = pob_ts[i];                         \
+        r[POB_TS_N + 2] = pob_rt0; r[POB_TS_N + 3] = __builtin_amdgcn_s_memrealtime();    \
       }                                                                                  \
     }                                                                                    \
   } while (0)
@@ -864,7 +924,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       // after every other write of the row (program order within the wave)
       if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = k; q < D; q += 4) o[q] = in.first_obs[(size_t)b * D + q];
+        group_copy<4, 4>(o, in.first_obs + (size_t)b * D, D, k);
       }
     }
 #ifdef POB_EXP_TIMING_OBS
@@ -900,21 +960,9 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #else
   POB_TS(4);
 #endif
-  // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
+  // ---- per-env tail: frozen rows, first_* (the env's lanes), scalar outputs (lane 0)
+  if (act_lane) tail_copies<QT, 4, 2>(in, out, flags, reset_rows, b, N, D, r3, r4, k);
   if (act_lane && k == 0) {
-    if (reset_rows) {  // frozen rows from first_qp
-      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
-    }
-    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
-      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
-      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
-      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
-      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
-    }
     out.reward[b] = t.reward;
     out.done[b] = t.done;
     if (out.steps) out.steps[b] = t.steps;
@@ -924,6 +972,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     if (out.m2) out.m2[b] = t.m2;
     out.rng[2 * b] = t.rng0;
     out.rng[2 * b + 1] = t.rng1;
+    write_typed(out, b, t);
   }
   if (out.any_done) {
     const unsigned long long m = __ballot(act_lane && k == 0 && done != 0.0f);
@@ -1242,7 +1291,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       // after every other write of the row
       if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = m; q < D; q += 8) o[q] = in.first_obs[(size_t)b * D + q];
+        group_copy<8, 4>(o, in.first_obs + (size_t)b * D, D, m);
       }
     }
     wave_lds_sync();
@@ -1294,21 +1343,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 #ifndef POB_EXP_TIMING_OBS
   POB_TS(4);
 #endif
-  // ---- per-env tail (A_0): frozen rows, first_*, scalar outputs
+  // ---- per-env tail: frozen rows, first_* (the env's lanes), scalar outputs (A_0)
+  if (act_lane) tail_copies<QT, 8>(in, out, flags, reset_rows, b, N, D, r3, r4, m);
   if (act_lane && lane0) {
-    if (reset_rows) {
-      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
-    }
-    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
-      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
-      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
-      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
-      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
-    }
     out.reward[b] = t.reward;
     out.done[b] = t.done;
     if (out.steps) out.steps[b] = t.steps;
@@ -1318,6 +1355,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     if (out.m2) out.m2[b] = t.m2;
     out.rng[2 * b] = t.rng0;
     out.rng[2 * b + 1] = t.rng1;
+    write_typed(out, b, t);
   }
   if (out.any_done) {
     const unsigned long long mk = __ballot(act_lane && lane0 && done != 0.0f);
@@ -1514,7 +1552,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
       // lanes after every other write of the row
       if ((flags & POB_F_AUTORESET) && done != 0.0f) {
         wave_lds_sync();
-        for (int q = r; q < D; q += 16) o[q] = in.first_obs[(size_t)b * D + q];
+        group_copy<16, 2>(o, in.first_obs + (size_t)b * D, D, r);
       }
     }
     wave_lds_sync();
@@ -1555,21 +1593,9 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   }
 
   POB_TS(4);
-  // ---- per-env tail (lane 0): frozen rows, first_*, scalar outputs
+  // ---- per-env tail: frozen rows, first_* (the env's lanes), scalar outputs (lane 0)
+  if (act_lane) tail_copies<QT, 16>(in, out, flags, reset_rows, b, N, D, r3, r4, r);
   if (act_lane && lane0) {
-    if (reset_rows) {
-      cpq<QT>(out.pos, in.first_pos, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.vel, in.first_vel, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.ang, in.first_ang, r3 + 3 * POB_NDYN, 3 * (N - POB_NDYN));
-      cpq<QT>(out.rot, in.first_rot, r4 + 4 * POB_NDYN, 4 * (N - POB_NDYN));
-    }
-    if ((flags & POB_F_AUTORESET) && out.first_pos != in.first_pos) {
-      cpq<QT>(out.first_pos, in.first_pos, r3, 3 * N);
-      cpq<QT>(out.first_vel, in.first_vel, r3, 3 * N);
-      cpq<QT>(out.first_ang, in.first_ang, r3, 3 * N);
-      cpq<QT>(out.first_rot, in.first_rot, r4, 4 * N);
-      for (int q = 0; q < D; ++q) out.first_obs[(size_t)b * D + q] = in.first_obs[(size_t)b * D + q];
-    }
     out.reward[b] = t.reward;
     out.done[b] = t.done;
     if (out.steps) out.steps[b] = t.steps;
@@ -1579,6 +1605,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     if (out.m2) out.m2[b] = t.m2;
     out.rng[2 * b] = t.rng0;
     out.rng[2 * b + 1] = t.rng1;
+    write_typed(out, b, t);
   }
   if (out.any_done) {
     const unsigned long long mk = __ballot(act_lane && lane0 && done != 0.0f);
@@ -2438,6 +2465,6 @@ int pob_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, fl
 // timing experiment only: per wave [HW_ID, XCC_ID, t0..t5] of the last step launch
 extern "C" __attribute__((visibility("default"))) int pob_debug_timing(unsigned long long *host, int waves) {
   if (waves > POB_TS_WAVES) waves = POB_TS_WAVES;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pob_ts_buf), sizeof(unsigned long long) * (POB_TS_N + 2) * waves) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pob_ts_buf), sizeof(unsigned long long) * POB_TS_ROW * waves) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -40,6 +40,11 @@ class AntEnv(PoBraxEnv):
         _common_params(self._params, p)
 
     def _metric_dtypes(self, metrics, after_step):
+        # reward_survive is a constant (1 after a step, 0 after reset): one cached tensor per
+        # batch shape, so that a step launches no fill kernel
         ref = metrics["reward_forward"]
-        survive = torch.ones_like(ref) if after_step else torch.zeros_like(ref)
-        return {**metrics, "reward_survive": survive}
+        key = (after_step, tuple(ref.shape), ref.device)
+        cache = self.__dict__.setdefault("_survive", {})
+        if key not in cache:
+            cache[key] = torch.ones_like(ref) if after_step else torch.zeros_like(ref)
+        return {**metrics, "reward_survive": cache[key]}

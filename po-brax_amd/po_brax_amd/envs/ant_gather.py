@@ -30,6 +30,7 @@ class AntGatherEnv(PoBraxEnv):
 
     kind = "ant_gather"
     slot_names = ("apples", "bombs", "objects")
+    int_metrics = (0, 1)  # ant_gather.py:147-148: in_range.sum() -> int32 after step
     reset_metrics = ("apples", "bombs", "objects")
     step_metrics = ("apples", "bombs", "objects")
 
@@ -70,9 +71,4 @@ class AntGatherEnv(PoBraxEnv):
         return (list(ANT_BODIES) + ["Arena"] + [f"Target_{i + 1}" for i in range(self.n_apples)]
                 + [f"Bomb_{i + 1}" for i in range(self.n_bombs)])
 
-    def _metric_dtypes(self, metrics, after_step):
-        if after_step:  # ant_gather.py:147-148: in_range.sum() -> int32
-            metrics = dict(metrics)
-            metrics["apples"] = metrics["apples"].to(torch.int32)
-            metrics["bombs"] = metrics["bombs"].to(torch.int32)
-        return metrics
+

@@ -190,6 +190,7 @@ class PoBraxEnv(Env):
     step_metrics: tuple = ()     # metric keys after step
     done_dtype = torch.float32
     info_rng = True              # info['rng'] is part of the State (False: stock brax ant)
+    int_metrics: tuple = ()      # engine slots (m0, m1) whose public metric is int32 after step
 
     def __init__(self, device=None, qp_dtype=torch.float32, **params):
         """``qp_dtype`` (engine extension): storage type of qp / first_qp, float32 (the
@@ -306,6 +307,9 @@ class PoBraxEnv(Env):
                      first_obs=state.info["first_obs"])
         if "any_done" in a:
             b["any_done"] = a["any_done"]
+        for k in _TYPED:  # the typed step outputs of a previous in-place step (reused)
+            if k in a:
+                b[k] = a[k]
         for k, t in b.items():
             if t is not None and not t.is_contiguous():
                 raise ValueError(f"state tensor {k} must be contiguous")
@@ -314,15 +318,35 @@ class PoBraxEnv(Env):
                 raise ValueError(f"state tensor {k} is {b[k].dtype}; this env stores qp as {self.qp_dtype}")
         return b
 
+    def _typed_outputs(self, b: dict, B: int, episode: bool) -> None:
+        """Step outputs in the reference's dtypes, written by the step kernel itself (C ABI
+        v5 typed fields) instead of conversion kernels after it: AntTag's bool done and int32
+        truncation, AntGather's int32 apples / bombs.  In-place steps reuse the buffers."""
+        want = []
+        if self.done_dtype is torch.bool:
+            want.append(("done_u8", torch.uint8))
+            if episode:
+                want.append(("trunc_i32", torch.int32))
+        want += [(f"m{k}_i32", torch.int32) for k in self.int_metrics]
+        for k, dt in want:
+            if b.get(k) is None or b[k].shape[0] != B:
+                b[k] = torch.empty((B,), dtype=dt, device=self.device)
+
     def _state_of(self, b: dict, after_step: bool, squeeze: bool) -> State:
         names = self.step_metrics if after_step else self.reset_metrics
         metrics = {name: b[f"m{self.slot_names.index(name)}"] for name in names}
+        if after_step:
+            for k in self.int_metrics:
+                metrics[self.slot_names[k]] = b[f"m{k}_i32"]
         metrics = self._metric_dtypes(metrics, after_step)
         done = b["done"]
         if after_step and self.done_dtype is not torch.float32:
-            done = done != 0
+            done = b["done_u8"].view(torch.bool)
         info = {"rng": b["rng"]} if self.info_rng else {}
         aux = {"done": b["done"], "rng": b["rng"]}
+        for k in _TYPED:
+            if b.get(k) is not None:
+                aux[k] = b[k]
         for k in range(3):
             aux[f"m{k}"] = b[f"m{k}"]
         if "steps" in b:
@@ -330,7 +354,7 @@ class PoBraxEnv(Env):
             trunc = b["truncation"]
             aux["truncation"] = trunc
             if after_step and self.done_dtype is not torch.float32:
-                trunc = trunc.to(torch.int32)  # 1 - bool -> int32 in EpisodeWrapper
+                trunc = b["trunc_i32"]  # 1 - bool -> int32 in EpisodeWrapper
             info["truncation"] = trunc
         if "first_pos" in b:
             info["first_qp"] = QP(b["first_pos"], b["first_rot"], b["first_vel"], b["first_ang"])
@@ -397,6 +421,7 @@ class PoBraxEnv(Env):
             if "first_pos" in bin_:  # immutable: shared, not copied
                 for k in ("first_pos", "first_rot", "first_vel", "first_ang", "first_obs"):
                     bout[k] = bin_[k]
+        self._typed_outputs(bout, B, "steps" in bin_)
         ci, co = self._cstate(bin_), self._cstate(bout)
         if _CAPTURE is not None:
             # MixedEnv collects the launch (envs/mixed.py) and builds the State after it:
@@ -424,6 +449,8 @@ class PoBraxEnv(Env):
 
 # set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here
 _CAPTURE = None
+# typed step-output fields of pob_state (C ABI v5)
+_TYPED = ("done_u8", "trunc_i32", "m0_i32", "m1_i32")
 
 
 def as_key(rng) -> torch.Tensor:

@@ -6,13 +6,16 @@ set -o pipefail
 shopt -s nullglob
 mkdir -p gpurun_out/ab
 R=${R:-3}
-libs="po-brax_amd/po_brax_amd/libpob.so $(ls build_variants/*.so 2>/dev/null)"
+# (a directory build_variants/NAME/ holding a whole po_brax_amd package with its libpob.so is
+# run as variant NAME through POB_PKG_ROOT: A/B of Python-side changes too)
+libs="po-brax_amd/po_brax_amd/libpob.so $(echo build_variants/*.so build_variants/*/)"  # (nullglob)
 for env in ${ENVS:-ant_heavenhell}; do
   for B in ${BS:-65536}; do
     for r in $(seq $R); do
       for lib in $libs; do
         tag=$(basename $lib .so)
-        POB_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-200} --env $env --batch $B \
+        if [ -d $lib ]; then pk="POB_PKG_ROOT=$PWD/$lib POB_LIB=$PWD/$lib/po_brax_amd/libpob.so"; else pk="POB_LIB=$PWD/$lib"; fi
+        env $pk timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-200} --env $env --batch $B \
           > gpurun_out/ab/$tag.$env.$B.$r.json 2>/dev/null || exit 1
       done
     done

@@ -226,3 +226,43 @@ def test_unaligned_state_uses_fallback_loads(name, monkeypatch):
     for f in QP:
         assert torch.equal(getattr(a.qp, f), getattr(b2.qp, f)), f
     assert torch.equal(a.obs, b2.obs) and torch.equal(a.reward, b2.reward)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_typed_step_outputs(inplace):
+    """The reference's dtypes come from the step kernel's typed outputs (C ABI v5), not
+    conversion kernels: AntTag done bool + truncation int32, AntGather apples / bombs int32;
+    each equals the conversion of the engine's float32 buffer, in single-kind and mixed
+    launches, functional and in-place."""
+    from po_brax_amd import envs
+    B = 300
+    keys = torch.from_numpy(_keys(3 * B, 31)).cuda()
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    kinds = ["ant_tag", "ant_gather", "ant_heavenhell"]
+
+    def check(name, s):
+        a = s.aux
+        if name == "ant_tag":
+            assert s.done.dtype == torch.bool and torch.equal(s.done, a["done"] != 0)
+            assert s.info["truncation"].dtype == torch.int32
+            assert torch.equal(s.info["truncation"], a["truncation"].to(torch.int32))
+        elif name == "ant_gather":
+            for k, slot in (("apples", "m0"), ("bombs", "m1")):
+                assert s.metrics[k].dtype == torch.int32 and torch.equal(s.metrics[k], a[slot].to(torch.int32)), k
+        else:
+            assert s.done.dtype == torch.float32
+
+    mixed = envs.create_mixed(kinds, episode_length=3)
+    ms = mixed.reset(torch.tensor([0, 31], dtype=torch.uint32), [B, B, B])
+    for i, name in enumerate(kinds):
+        env = envs.create(name, batch_size=B, episode_length=3)
+        s = env.reset(keys[i * B:(i + 1) * B].contiguous())
+        for _ in range(4):  # step 3 autoresets every env (done / truncation flip)
+            act = torch.rand((B, 8), device="cuda", generator=gen) * 2 - 1
+            s = env.step_(s, act) if inplace else env.step(s, act)
+            check(name, s)
+    for _ in range(4):
+        acts = [torch.rand((B, 8), device="cuda", generator=gen) * 2 - 1 for _ in kinds]
+        ms = mixed.step_(ms, acts) if inplace else mixed.step(ms, acts)
+        for name, s in zip(kinds, ms):
+            check(name, s)

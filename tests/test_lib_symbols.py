@@ -31,7 +31,7 @@ def test_lib_exports_every_declared_symbol():
     exported = set(re.findall(r" T (pob_\w+)", out))
     assert set(_declared()) <= exported
     from po_brax_amd import _lib
-    assert lib.pob_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.pob_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_python_binding_covers_header():
@@ -53,3 +53,22 @@ def test_errors_are_reported_without_gpu():
     with pytest.raises(ValueError):
         _lib.check(_lib.lib.pob_reset(None, 4, None, None, None))
     assert b"env is NULL" in _lib.lib.pob_last_error()
+
+
+def _struct_fields(name):
+    """Field names of `typedef struct name {...} name;` in include/pob.h, in order."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, flags=re.S).group(1)
+    fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if decl:
+            fields += [re.sub(r"[\s*]|\[.*\]", "", d.split()[-1] if i == 0 else d) for i, d in enumerate(decl.split(","))]
+    return fields
+
+
+def test_ctypes_state_layout_matches_header():
+    """The ctypes mirror of pob_state lists the header's fields in the header's order (every
+    field is a pointer, so equal order means equal layout)."""
+    from po_brax_amd import _lib
+    assert [n for n, _ in _lib.pob_state._fields_] == _struct_fields("pob_state")
