@@ -118,6 +118,10 @@ typedef struct pob_state {
   uint8_t *done_u8;
   int32_t *trunc_i32;
   int32_t *m0_i32, *m1_i32;
+  /* Optional (ABI v5): pob_reset_where_done[_shard] zeroes *any_done_clear, so that a caller
+   * double-buffering the any-done word (step k ORs into word k % 2, its masked reset reads
+   * that word and clears the other) needs no fill kernel per step. */
+  uint32_t *any_done_clear;
 } pob_state;
 
 typedef struct pob_env pob_env;

@@ -50,7 +50,7 @@ struct pob_env {
 #define POB_STATE_FIELDS(X)                                                                    \
   X(pos) X(rot) X(vel) X(ang) X(obs) X(reward) X(done) X(steps) X(truncation) X(m0) X(m1) X(m2) \
   X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done) X(done_u8) X(trunc_i32) \
-  X(m0_i32) X(m1_i32)
+  X(m0_i32) X(m1_i32) X(any_done_clear)
 
 struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
@@ -59,6 +59,7 @@ struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   uint32_t *any_done;
   uint8_t *done_u8;  // typed copies of step outputs (optional, pob.h)
   int32_t *trunc_i32, *m0_i32, *m1_i32;
+  uint32_t *any_done_clear;  // pob_reset_where_done zeroes it (optional)
 };
 static StatePtrs to_ptrs(const pob_state &s) {
   StatePtrs p;
@@ -1974,6 +1975,9 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   const int k = lane & 3;
   const int e0 = (int)blockIdx.x * (BS / 4);  // first env of this wave
   const int b = e0 + (lane >> 2);
+  // the next step's any-done word (gym wrapper, double-buffered): the step before this launch
+  // used the other word, and the next launch on the stream reads this one after it is zero
+  if (s.any_done_clear && blockIdx.x == 0 && lane == 0) *s.any_done_clear = 0u;
   if (mode == RESET_GYM) {
     const bool any = *any_flag != 0u;
     if (b == 0 && k == 0 && gym_out) {
@@ -1984,18 +1988,18 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     if (!any) return;  // block-uniform
   }
   bool active = b < B;
+  if (active && mode != RESET_FULL) active = s.done[b] != 0.0f;
+  const uint64_t lanes = __ballot(active && k == 0);
+  if (lanes == 0ull) return;  // block-uniform (a masked reset with no done env in this wave)
+  // keys of the envs to reset only (a gym key is a threefry hash: a wave without a done env
+  // computes none)
   uint32_t k0 = 0u, k1 = 0u;
   if (active) {
     if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
-    else {
-      active = s.done[b] != 0.0f;
-      if (mode == RESET_GYM)
-        tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
-      else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
-    }
+    else if (mode == RESET_GYM)
+      tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
+    else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
   }
-  const uint64_t lanes = __ballot(active && k == 0);
-  if (lanes == 0ull) return;  // block-uniform (a masked reset with no done env in this wave)
   uint32_t rows = 0u;  // bit e: env e0 + e is reset
 #pragma unroll
   for (int e = 0; e < 16; ++e) rows |= (uint32_t)((lanes >> (4 * e)) & 1ull) << e;

@@ -47,7 +47,7 @@ class pob_state(C.Structure):
     _fields_ = [(n, _VP) for n in (
         "pos", "rot", "vel", "ang", "obs", "reward", "done", "steps", "truncation",
         "m0", "m1", "m2", "rng", "first_pos", "first_rot", "first_vel", "first_ang",
-        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32")]
+        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32", "any_done_clear")]
 
 
 # Every symbol include/pob.h declares (checked by tests/test_lib_symbols.py).

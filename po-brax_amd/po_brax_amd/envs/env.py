@@ -305,8 +305,9 @@ class PoBraxEnv(Env):
             fq = state.info["first_qp"]
             b.update(first_pos=fq.pos, first_rot=fq.rot, first_vel=fq.vel, first_ang=fq.ang,
                      first_obs=state.info["first_obs"])
-        if "any_done" in a:
-            b["any_done"] = a["any_done"]
+        for k in ("any_done", "any_done_clear"):
+            if k in a:
+                b[k] = a[k]
         for k in _TYPED:  # the typed step outputs of a previous in-place step (reused)
             if k in a:
                 b[k] = a[k]

@@ -257,7 +257,12 @@ class AutoresetVmapGymWrapper(VmapGymWrapper):
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
-        self._any = torch.zeros(4, dtype=torch.uint32, device=self.device)
+        # two any-done words (16 B apart), used by alternate steps: step k's kernel ORs into
+        # word k % 2 and its masked reset reads that word and zeroes the other one for step
+        # k + 1 (pob_state.any_done_clear), so no fill kernel runs per step
+        self._words = torch.zeros(8, dtype=torch.uint32, device=self.device)
+        self._parity = 0
+        self._any = self._words[0:4]
         self._key2 = torch.empty(2, dtype=torch.uint32, device=self.device)
 
     def step(self, action):
@@ -271,10 +276,12 @@ class AutoresetVmapGymWrapper(VmapGymWrapper):
     # the two halves of step (the cross-rank any-done reduction goes between them)
     def _step_local(self, action):
         s = self._state
-        self._any.zero_()
-        s.aux["any_done"] = self._any
+        p = self._parity
+        self._any = self._words[4 * p:4 * p + 4]  # zero: initial, or cleared by the last reset
+        nxt = self._words[4 * (1 - p):4 * (1 - p) + 4]
+        s.aux["any_done"], s.aux["any_done_clear"] = self._any, nxt
         self._state = s = self._env._chain_step(s, action, 0, 0, True)
-        s.aux["any_done"] = self._any
+        s.aux["any_done"], s.aux["any_done_clear"] = self._any, nxt
         return s
 
     def _autoreset(self):
@@ -282,6 +289,7 @@ class AutoresetVmapGymWrapper(VmapGymWrapper):
         self._env.unwrapped._reset_where_done(s, _lib.RESET_GYM, self._key, self._key2,
                                               total=self.total_envs, first=sh.lo if sh is not None else 0)
         self._key, self._key2 = self._key2, self._key
+        self._parity ^= 1
         return s.obs, s.reward, s.done, s.metrics
 
 
