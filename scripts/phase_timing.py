@@ -26,11 +26,12 @@ torch.cuda.synchronize()
 LPE = int(sys.argv[3]) if len(sys.argv) > 3 else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
 W = (B * LPE + 63) // 64
 NTS = 10  # POB_TS_N
-buf = np.zeros((W, NTS + 2), np.uint64)
+buf = np.zeros((W, NTS + 4), np.uint64)
 f = _lib.lib.pob_debug_timing
 f.argtypes = [C.c_void_p, C.c_int]
 assert f(buf.ctypes.data, W) == 0
-hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:].astype(np.int64)
+hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:2 + NTS].astype(np.int64)
+rt = buf[:, 2 + NTS:].astype(np.int64)  # device-wide 100 MHz clock: wave start, end
 cols = [i for i in range(NTS) if (t[:, i] != 0).all()]  # the stamps this build records
 t = t[:, cols]
 d = np.diff(t, axis=1)
@@ -41,9 +42,10 @@ for i in range(d.shape[1]):
           f"p90 {np.percentile(d[:, i], 90):9.0f} max {d[:, i].max():9.0f}")
 tot = t[:, -1] - t[:, 0]
 print(f"total p0 {tot.min()} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
-for x in np.unique(xcc):
-    m = xcc == x
-    st = t[m, 0] - t[m, 0].min()
-    en = t[m, -1] - t[m, 0].min()
-    print(f"xcc {x}: waves {m.sum()} start spread p50 {np.median(st):.0f} max {st.max()} end max {en.max()}")
-print("start offset vs duration corr", np.corrcoef((t[:, 0] - t[:, 0].min()), tot)[0, 1])
+# device-wide clock (10 ns ticks): when waves start and end relative to the first start
+r0 = rt[:, 0] - rt[:, 0].min()
+r1 = rt[:, 1] - rt[:, 0].min()
+pct = lambda a: " ".join(f"p{q} {np.percentile(a, q) / 100:.1f}" for q in (0, 10, 50, 90, 100))
+print(f"wave start us: {pct(r0)}")
+print(f"wave end   us: {pct(r1)}")
+print(f"wave life  us: {pct(r1 - r0)}")

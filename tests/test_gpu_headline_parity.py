@@ -185,3 +185,30 @@ def test_wall_stress_256_thread_blocks(name):
         so = o.step(_state_np(s), act, flags=FLAGS, episode_length=1000, nthreads=NT)
         s = env.step(s, torch.from_numpy(act).cuda())
         compare_states(s, so, f"{name} wall B={B} step {t}")
+
+
+@pytest.mark.parametrize("lanes,B", [(16, 70), (8, 9000), (4, 70)])
+def test_out_of_range_inputs_take_exact_fallbacks(monkeypatch, lanes, B):
+    """The kernels' fast reciprocal / square root / quaternion normalisation fall back to
+    the IEEE forms behind wave-uniform guards (pob_math.h pob_rcp, qnormalize).  States that
+    take the fallbacks -- a torso at 1e25 m/s (joint anchors drift beyond 2^96), a zero
+    quaternion (normalisation fallback), a 1e30 rad/s spin -- must still match the oracle
+    bit for bit (NaN / inf included), in the lanes that hold them and in their neighbours,
+    on the sixteen-, eight- and four-lane kernels."""
+    if lanes <= 8:
+        monkeypatch.setenv("POB_HEXA_MAX_B", "0")
+    if lanes == 4:
+        monkeypatch.setenv("POB_OCTET_MAX_B", "0")
+    for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
+        env = _envs().create(name, batch_size=B, episode_length=1000)
+        keys = _keys(B, 40 + lanes)
+        s = env.reset(torch.from_numpy(keys).cuda())
+        with torch.no_grad():
+            s.qp.vel[1, 0, 0] = 1e25
+            s.qp.rot[2, 1] = 0.0
+            s.qp.ang[3, 2, 1] = 1e30
+        o = orc.OracleEnv(name)
+        for t, act in enumerate(_actions(lanes + 2, B, 2)):
+            so = o.step(_state_np(s), act, flags=FLAGS, episode_length=1000, nthreads=NT)
+            s = env.step(s, torch.from_numpy(act).cuda())
+            compare_states(s, so, f"{name} B={B} lanes={lanes} step {t}")
