@@ -1936,6 +1936,19 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
 template <typename QT>
 POB_D void reset_store_rows(float *X, float *FX, const size_t b0, const int W, const int nrows, const int WP,
                             const float *stg, const uint32_t rows, const int lane) {
+  if (4 * __popc(rows) < nrows) {
+    // a masked reset (typically one done env per wave): the set rows only, each stored by the
+    // whole wave (a few iterations instead of a pass over all 16 rows' elements)
+    for (uint32_t m = rows; m != 0u; m &= m - 1u) {
+      const int rr = __builtin_ctz(m);
+      for (int e0 = lane; e0 < W; e0 += 64) {
+        const float v = stg[rr * WP + e0];
+        Q<QT>::st(X, (b0 + rr) * W + e0, v);
+        if (FX) Q<QT>::st(FX, (b0 + rr) * W + e0, v);
+      }
+    }
+    return;
+  }
   int r = 0, e = lane;
   while (e >= W) { e -= W; ++r; }
   for (int i = lane; i < nrows * W; i += 64) {
@@ -1964,6 +1977,8 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
                                               uint32_t *gym_out, const uint32_t *any_flag, const StatePtrs s,
                                               const int total, const int first, const int WP) {
   static_assert(BS == 64, "k_reset stages one wave's rows per block");
+  POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING; waves with nothing to reset exit unrecorded)
+  POB_TS(0);
   __shared__ uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
   // per-lane sorted lists, then the merged choice per env (POB_MAXOBJ x 16 envs)
   __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS + POB_MAXOBJ * (BS / 4) : 1];
@@ -2000,6 +2015,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
       tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
     else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
   }
+  POB_TS(1);
   uint32_t rows = 0u;  // bit e: env e0 + e is reset
 #pragma unroll
   for (int e = 0; e < 16; ++e) rows |= (uint32_t)((lanes >> (4 * e)) & 1ull) << e;
@@ -2008,6 +2024,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   const float *WT = legtab + 4 * POB_LEG_FLOATS;
   QReset R;
   if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx);
+  POB_TS(2);
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
   const bool full = mode == RESET_FULL && s.first_pos;
@@ -2027,6 +2044,9 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     else reset_store_rows<QT>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
     wave_lds_sync();
   }
+  POB_TS(3);
+  POB_TS(8);  // (marks the row as a reset wave's: the step kernels do not set stamp 8)
+  POB_TS_WRITE();
   if (!active || k != 0) return;
   if (mode == RESET_FULL) {
     s.rng[2 * b] = R.rng0; s.rng[2 * b + 1] = R.rng1;

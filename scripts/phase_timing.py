@@ -15,15 +15,24 @@ from po_brax_amd import _lib, envs, jumpy  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 NAME = sys.argv[2] if len(sys.argv) > 2 else "ant_heavenhell"
-env = envs.create(NAME, batch_size=B, episode_length=1000)
+GYM = len(sys.argv) > 3 and sys.argv[3] == "gym"  # time the gym path's masked reset kernel instead
 key = jumpy.random_prngkey(0)
-s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
 act = torch.empty((B, 8), device="cuda")
-for _ in range(5):
-    jumpy.random_actions_(key, B, 0, act)
-    s = env.step_(s, act)
+if GYM:
+    gym = envs.create_gym_env(NAME, batch_size=B, seed=0, episode_length=1000)
+    gym.reset()
+    for _ in range(30):
+        jumpy.random_actions_(key, B, 0, act)
+        gym.step(act)
+else:
+    env = envs.create(NAME, batch_size=B, episode_length=1000)
+    s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
+    for _ in range(5):
+        jumpy.random_actions_(key, B, 0, act)
+        s = env.step_(s, act)
 torch.cuda.synchronize()
-LPE = int(sys.argv[3]) if len(sys.argv) > 3 else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
+LPE = 4 if GYM else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
+
 W = (B * LPE + 63) // 64
 NTS = 10  # POB_TS_N
 buf = np.zeros((W, NTS + 4), np.uint64)
@@ -32,6 +41,10 @@ f.argtypes = [C.c_void_p, C.c_int]
 assert f(buf.ctypes.data, W) == 0
 hw, xcc, t = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2:2 + NTS].astype(np.int64)
 rt = buf[:, 2 + NTS:].astype(np.int64)  # device-wide 100 MHz clock: wave start, end
+# waves that recorded (a masked reset's idle waves exit first; its rows carry stamp 8)
+rec = (t[:, 8] != 0) if GYM else (t != 0).any(axis=1)
+hw, xcc, t, rt = hw[rec], xcc[rec], t[rec], rt[rec]
+print(f"recorded waves {rec.sum()} of {W}")
 cols = [i for i in range(NTS) if (t[:, i] != 0).all()]  # the stamps this build records
 t = t[:, cols]
 d = np.diff(t, axis=1)
