@@ -605,11 +605,30 @@ POB_D void stage_store_dyn(float *X, size_t el0, int N, int nenv, const float *s
   }
 }
 
+// Copy N floats of the system table into LDS with every load of the thread in flight before
+// its LDS writes (a strided loop waited for each load in turn: ~10 memory round trips in a
+// one-wave block's prologue).  stride = the block size, >= 64.
+template <int N>
+POB_D void stage_table(float *dst, const __attribute__((address_space(4))) float *src, const int tid,
+                       const int stride) {
+  constexpr int M = (N + 63) / 64;
+  float v[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int i = tid + stride * m;
+    v[m] = i < N ? src[i] : 0.0f;
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int i = tid + stride * m;
+    if (i < N) dst[i] = v[m];
+  }
+}
 // stage the block table (leg rows, then wall rows) in LDS (all threads of the block;
 // before any divergence)
 POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
   const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];  // leg[4][..], wall_row[..][8]
-  for (int i = (int)threadIdx.x; i < POB_TAB_FLOATS; i += (int)blockDim.x) legtab[i] = src[i];
+  stage_table<POB_TAB_FLOATS>(legtab, src, (int)threadIdx.x, (int)blockDim.x);
   __syncthreads();
 }
 #ifdef POB_EXP_TIMING
@@ -1098,13 +1117,6 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   __shared__ float stg[POB_OSTAGE_FLOATS];
   __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
-  {
-    const __attribute__((address_space(4))) float *src = &Sp->oct[0][0];
-    for (int i = (int)threadIdx.x; i < 8 * OT_FLOATS; i += 64) otab[i] = src[i];
-    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
-    for (int i = (int)threadIdx.x; i < POB_MAXW * POB_WALL_FLOATS; i += 64) otab[8 * OT_FLOATS + i] = wsrc[i];
-    __syncthreads();
-  }
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
   const int m = lane & 7;
@@ -1112,10 +1124,6 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   const int k = isA ? m : 7 - m;              // the leg
   const int jown = isA ? 2 * k : 2 * k + 1;    // the lane's joint
   const int g0 = isA ? 0 : 2 * k + 1, g1 = isA ? 2 * k + 1 : 2 * k + 2;  // its slots' bodies
-  float OT[OT_FLOATS];  // the lane's role row, in registers (constant indices only)
-#pragma unroll
-  for (int i = 0; i < OT_FLOATS; ++i) OT[i] = otab[(isA ? k : 4 + k) * OT_FLOATS + i];
-  const float *WT = otab + 8 * OT_FLOATS;
   const Lds Ls{stg, 64, lane};
   const int b_first = (int)blockIdx.x * 8;
   const int b = b_first + (lane >> 3);
@@ -1177,6 +1185,19 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     }
   }
   (void)NMAX;
+  // the role table, staged after the state loads are issued (both in flight together; the
+  // block is one wave, so an LDS wait orders the table writes before its reads)
+  {
+    const __attribute__((address_space(4))) float *src = &Sp->oct[0][0];
+    stage_table<8 * OT_FLOATS>(otab, src, (int)threadIdx.x, 64);
+    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
+    stage_table<POB_MAXW * POB_WALL_FLOATS>(otab + 8 * OT_FLOATS, wsrc, (int)threadIdx.x, 64);
+    wave_lds_sync();
+  }
+  float OT[OT_FLOATS];  // the lane's role row, in registers (constant indices only)
+#pragma unroll
+  for (int i = 0; i < OT_FLOATS; ++i) OT[i] = otab[(isA ? k : 4 + k) * OT_FLOATS + i];
+  const float *WT = otab + 8 * OT_FLOATS;
   POB_TS(1);
 
   // ---- physics (10 substeps in registers + the lane's LDS slots)
@@ -1380,13 +1401,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   __shared__ float stg[POB_HSTAGE_FLOATS];
   __shared__ __attribute__((aligned(16))) float htab[HT_TAB_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
-  {
-    const __attribute__((address_space(4))) float *src = &Sp->hex[0][0];
-    for (int i = (int)threadIdx.x; i < 16 * HT_FLOATS; i += 64) htab[i] = src[i];
-    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
-    for (int i = (int)threadIdx.x; i < POB_MAXW * POB_WALL_FLOATS; i += 64) htab[16 * HT_FLOATS + i] = wsrc[i];
-    __syncthreads();
-  }
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
   const int r = lane & 15;
@@ -1396,10 +1410,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   const int g = hip ? (isP ? 0 : 2 * k + 1) : (isP ? 2 * k + 1 : 2 * k + 2);  // its body
   // the lane that writes the body's rows: the torso's lane 0, an Aux's child side, a lower leg
   const bool canon = r == 0 || (hip && !isP) || (!hip && !isP);
-  float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
-#pragma unroll
-  for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
-  const float *WT = htab + 16 * HT_FLOATS;
   const Lds Ls{stg, 64, lane};
   const int b_first = (int)blockIdx.x * 4;
   const int le = lane >> 4;
@@ -1447,6 +1457,18 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
       gop_ok = true;
     }
   }
+  // the role table, staged after the state loads are issued (as in the eight-lane kernel)
+  {
+    const __attribute__((address_space(4))) float *src = &Sp->hex[0][0];
+    stage_table<16 * HT_FLOATS>(htab, src, (int)threadIdx.x, 64);
+    const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
+    stage_table<POB_MAXW * POB_WALL_FLOATS>(htab + 16 * HT_FLOATS, wsrc, (int)threadIdx.x, 64);
+    wave_lds_sync();
+  }
+  float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
+#pragma unroll
+  for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
+  const float *WT = htab + 16 * HT_FLOATS;
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
