@@ -1691,6 +1691,9 @@ struct QReset {
   float tx, ty;           // TAG target xy
   int hh_first;           // HH: goal order of choice(rng3, hhp[:2], 2)
   uint32_t rng0, rng1;    // new info['rng']
+#ifdef POB_EXP_TIMING
+  unsigned long long ts[4];  // timing experiment only: stamps inside qreset_compute
+#endif
 };
 
 // minimum over the env's lane quad (exact and order-free; all four lanes active)
@@ -1765,6 +1768,9 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
     if (i < (int)ns) tf_split(k0, k1, ns, (uint32_t)i, r[i][0], r[i][1]);
     else { r[i][0] = 0u; r[i][1] = 0u; }
   }
+#ifdef POB_EXP_TIMING
+  R.ts[0] = __builtin_amdgcn_s_memtime();
+#endif
   // System.default_qp forward kinematics of this lane's leg (joints 2k, 2k + 1), the torso
   // at the origin (oracle fk / kernel fk op order)
   QBody &b = R.bd;
@@ -1801,6 +1807,9 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
   zmin = quad_min(zmin);
 #pragma unroll
   for (int l = 0; l < QNB; ++l) b.x[l].z = b.x[l].z - zmin;
+#ifdef POB_EXP_TIMING
+  R.ts[1] = __builtin_amdgcn_s_memtime();
+#endif
   R.ax = 0.0f; R.ay = 0.0f; R.tx = 0.0f; R.ty = 0.0f; R.hh_first = 0;
   if (KIND == POB_HEAVENHELL) {
     // ant_heavenhell.py:87-103
@@ -1840,6 +1849,9 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { b.x[l].x = b.x[l].x + R.ax; b.x[l].y = b.x[l].y + R.ay; }
   }
+#ifdef POB_EXP_TIMING
+  R.ts[2] = __builtin_amdgcn_s_memtime();
+#endif
   // sys.info(qp).contact: contact detection + velocity-level solve at the static qp
   QContacts ct;
   qdetect<KIND != POB_ANT>(Sp, LT, WT, b, ct);
@@ -1847,6 +1859,9 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
   for (int l = 0; l < QNB; ++l) { R.cv[l] = V(0.0f, 0.0f, 0.0f); R.ca[l] = V(0.0f, 0.0f, 0.0f); }
   if (S.legacy) qlegacy_contacts(Sp, LT, b, ct, R.cv, R.ca);  // legacy sys.info: the colliders' impulses
   else qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca);
+#ifdef POB_EXP_TIMING
+  R.ts[3] = __builtin_amdgcn_s_memtime();
+#endif
   // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
   for (int jl = 0; jl < QNJ; ++jl) {
@@ -2047,6 +2062,14 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   QReset R;
   if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx);
   POB_TS(2);
+#ifdef POB_EXP_TIMING
+  {  // the first active lane's stamps inside the compute (stamps 4..7 of the wave's row)
+    const int src = __builtin_ctzll(lanes);
+    for (int i = 0; i < 4; ++i)
+      pob_ts[4 + i] = ((unsigned long long)__shfl((int)(R.ts[i] >> 32), src) << 32) |
+                      (unsigned int)__shfl((int)(unsigned int)R.ts[i], src);
+  }
+#endif
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
   const bool full = mode == RESET_FULL && s.first_pos;

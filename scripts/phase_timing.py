@@ -53,6 +53,7 @@ for i in range(d.shape[1]):
     n = f"{cols[i]}->{cols[i + 1]}"
     print(f"{n:6s} ticks p0 {np.percentile(d[:, i], 0):9.0f} p50 {np.percentile(d[:, i], 50):9.0f} "
           f"p90 {np.percentile(d[:, i], 90):9.0f} max {d[:, i].max():9.0f}")
+print("stamp - stamp0 p50: " + " ".join(f"{c}:{np.median(t[:, i] - t[:, 0]):.0f}" for i, c in enumerate(cols)))
 tot = t[:, -1] - t[:, 0]
 print(f"total p0 {tot.min()} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 # device-wide clock (10 ns ticks): when waves start and end relative to the first start
