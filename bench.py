@@ -85,6 +85,8 @@ def main() -> int:
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 ('nccl' = RCCL; 'gloo' lets several ranks share "
                          "one GPU for a functional rehearsal, not a measurement)")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="graph rollout: env groups stepped on their own streams (rollout.GraphRollout)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
                          "hipGraph (po_brax_amd.rollout); the gym and --gather-obs paths are always eager")
@@ -176,7 +178,8 @@ def main() -> int:
     roll = None
     if use_graph:  # capture the K timed steps (capture does not run them)
         from po_brax_amd.rollout import GraphRollout
-        roll = GraphRollout(env, state, acts[args.warmup:args.warmup + args.steps])
+        roll = GraphRollout(env, state, acts[args.warmup:args.warmup + args.steps],
+                            groups=args.groups if args.env != "mixed" else 1)
 
     # timed region: K steps.  Eager: events bracket each step's kernels (and, with
     # --gather-obs, the all-gather after them) on torch's current stream, which the kernels

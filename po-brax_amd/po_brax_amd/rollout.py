@@ -24,33 +24,87 @@ from typing import Sequence
 import torch
 
 
+def _slice_state(state, lo: int, hi: int, B: int):
+    """The State of envs [lo, hi): every per-env tensor (first dim B, batch-major, so the
+    slice is a contiguous view) sliced, the same object -> the same view (the engine tells
+    its public tensors from caller replacements by identity, envs/env.py _bufs_of)."""
+    from .envs.env import QP, State
+    memo = {}
+
+    def sl(x):
+        if isinstance(x, torch.Tensor):
+            if x.dim() >= 1 and x.shape[0] == B:
+                if id(x) not in memo:
+                    memo[id(x)] = x[lo:hi]
+                return memo[id(x)]
+            return x
+        if isinstance(x, QP):
+            return QP(sl(x.pos), sl(x.rot), sl(x.vel), sl(x.ang))
+        if isinstance(x, dict):
+            return {k: sl(v) for k, v in x.items()}
+        return x
+
+    return State(sl(state.qp), sl(state.obs), sl(state.reward), sl(state.done), sl(state.metrics),
+                 sl(state.info), sl(state.aux))
+
+
 class GraphRollout:
-    def __init__(self, env, state, actions: torch.Tensor, warmup: bool = False):
+    def __init__(self, env, state, actions: torch.Tensor, warmup: bool = False, groups: int = 1):
         """Capture ``actions.shape[0]`` in-place steps of ``env`` on ``state``.
 
         Capture does not execute the kernels; ``warmup=True`` first runs one eager step on a
         side stream (needed only when the env has never been stepped in this process, so
-        that lazily initialised state is set up outside the capture)."""
+        that lazily initialised state is set up outside the capture).
+
+        ``groups = G > 1`` (single-kind envs): the batch is split into G contiguous env groups
+        whose step chains are captured on G streams -- the groups are independent, so group
+        g's step t + 1 may start while group g' still finishes step t, filling the SIMDs a
+        launch's last waves leave idle.  Every env still takes exactly the same steps with
+        the same kernels and actions (results bit-identical to ``groups = 1``)."""
         if actions.dim() != 3:
             raise ValueError("actions must be (T, B, A)")
         self.env, self.state, self.actions = env, state, actions
         self.steps = int(actions.shape[0])
         dev = actions.device
+        B = int(actions.shape[1])
+        groups = max(1, min(int(groups), B))
+        if groups > 1 and isinstance(state, (list, tuple)):
+            raise ValueError("groups > 1 needs a single-kind env")
         if warmup:
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
-                self._step(0)
+                self.state = self.env.step_(self.state, self.actions[0])
             torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
+        if groups == 1:
+            with torch.cuda.graph(self.graph):
+                for t in range(self.steps):
+                    # follow the returned State: its public typed outputs (TAG done, GA
+                    # counts) are the buffers the captured kernels write
+                    self.state = self.env.step_(self.state, self.actions[t])
+            return
+        bounds = [(B * g // groups, B * (g + 1) // groups) for g in range(groups)]
+        # the typed step outputs (TAG bool done, GA int32 counts) live in the whole batch's
+        # buffers, so that the groups write slices of them
+        u = env.unwrapped
+        u._typed_outputs(self.state.aux, B, "steps" in self.state.info)
+        parts = [_slice_state(self.state, lo, hi, B) for lo, hi in bounds]
+        streams = [None] + [torch.cuda.Stream(dev) for _ in range(groups - 1)]
         with torch.cuda.graph(self.graph):
+            cap = torch.cuda.current_stream(dev)
+            for st in streams[1:]:
+                st.wait_stream(cap)  # fork from the capture stream
             for t in range(self.steps):
-                self._step(t)
-
-    def _step(self, t: int):
-        # (a MixedEnv splits the (B_total, A) rows into its per-kind blocks itself)
-        self.env.step_(self.state, self.actions[t])
+                for g, (lo, hi) in enumerate(bounds):
+                    with torch.cuda.stream(streams[g] or cap):
+                        parts[g] = self.env.step_(parts[g], self.actions[t, lo:hi])
+            for st in streams[1:]:
+                cap.wait_stream(st)  # join
+        self.parts = parts
+        # the whole batch's State after a step (public fields in the reference's dtypes)
+        self.state = u._state_of(u._bufs_of(self.state), True, False)
 
     def replay(self):
         """Run the captured steps (stream-ordered on torch's current stream)."""
