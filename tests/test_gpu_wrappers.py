@@ -213,3 +213,37 @@ def test_state_replace_done_is_honoured():
     s2 = env.step(s, torch.from_numpy(act[2]).cuda())
     compare_states(s2, so, "after replace(done=1)")
     assert bool((s2.info["steps"] == 1).all())
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag"])
+def test_inplace_fast_path(name):
+    """step_ on a State the engine returned from an in-place step reuses its cached C state
+    (envs/env.py fast path) and returns the same object: equal to functional steps bit for
+    bit over an autoreset episode, and a brax-style edit (state.replace(done=...)) between
+    in-place steps still reaches the kernel (the oracle step from the edited state)."""
+    envs = _envs()
+    B, L = 96, 4
+    keys = torch.from_numpy(_keys(B, 8)).cuda()
+    e1, e2 = (envs.create(name, batch_size=B, episode_length=L) for _ in range(2))
+    s1, s2 = e1.reset(keys), e2.reset(keys)
+    act = np.random.default_rng(3).uniform(-1, 1, (9, B, 8)).astype(np.float32)
+    for t in range(8):
+        a = torch.from_numpy(act[t]).cuda()
+        s1 = e1.step(s1, a)
+        prev = s2
+        s2 = e2.step_(s2, a)
+        if t >= 2:
+            assert s2 is prev  # the fast path returns the stepped State itself
+        assert "_fast" in s2.aux
+    for f in ("pos", "rot", "vel", "ang"):
+        assert torch.equal(getattr(s1.qp, f), getattr(s2.qp, f)), f
+    assert torch.equal(s1.obs, s2.obs) and torch.equal(s1.reward, s2.reward) and torch.equal(s1.done, s2.done)
+    for k in s1.metrics:
+        assert torch.equal(s1.metrics[k], s2.metrics[k]), k
+    # an edit between in-place steps takes the full path and is honoured
+    s3 = s2.replace(done=torch.ones_like(s2.done))
+    ref = _state_np(s3)
+    ref["done"] = np.ones(B, np.float32)
+    so = orc.OracleEnv(name).step(ref, act[8], flags=FLAGS, episode_length=L)
+    s4 = e2.step_(s3, torch.from_numpy(act[8]).cuda())
+    compare_states(s4, so, f"{name}: in-place after replace(done=1)")
