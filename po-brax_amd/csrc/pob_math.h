@@ -64,6 +64,20 @@ POB_D float pob_sqrt(float x) {
   return r;
 }
 
+// s = sqrt(x) and inv = 1 / s (for use where s > 0) under ONE range guard: x in
+// [2^-96, 2^96] puts s in [2^-48, 2^48], inside the reciprocal's fast range, so the
+// separate guard of pob_rcp(pob_sqrt(x)) never fires there.  Same values as the pair.
+POB_D void pob_sqrt_rcp(float x, float &s, float &inv) {
+  s = pob_sqrt_fast(x);
+  inv = pob_rcp_fast(s);
+  const bool slow = !pob_fast_range(x);
+  if (__builtin_expect(__any(slow), 0)) {
+    if (slow) s = pob_sqrt_ieee(x);
+    const float r = pob_rcp_fast(s);
+    inv = pob_fast_range(s) ? r : pob_rcp_ieee(s);
+  }
+}
+
 // a / b of the physics step as a * (1 / b) with the correctly rounded reciprocal (spec:
 // the oracle spells a * (1.0f / b)); <= 1.5 ulp, and a quarter of an IEEE division's cost
 #define POB_DIV(a, b) ((a) * pob_rcp(b))

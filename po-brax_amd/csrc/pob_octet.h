@@ -149,9 +149,9 @@ POB_D void oground_position(csys_t &S, const float pen, const v3 pe, const float
   DA = V(DA.x + rr.y * lam, DA.y + -(rr.x * lam), DA.z);  // rr x P
   const v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
   const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
-  const float lt = pob_sqrt(FMA(dpy, dpy, dpx * dpx));
+  float lt, inv;
+  pob_sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
   if (lt > 0.0f) {
-    const float inv = pob_rcp(lt);
     const float tx = dpx * inv, ty = dpy * inv;
     const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
     const float wt = im + vdot(ctn, ctn);
@@ -179,9 +179,10 @@ POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, c
   v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
   v3 dp = vsub(cp, cprev);
   v3 dpt = vfma(n, -vdot(dp, n), dp);
-  float lt = pob_sqrt(vdot(dpt, dpt));
+  float lt, ilt;
+  pob_sqrt_rcp(vdot(dpt, dpt), lt, ilt);
   if (lt > 0.0f) {
-    v3 t = vdivs(dpt, lt);
+    v3 t = vscl(dpt, ilt);
     v3 ctn = vcross(rr, t);
     float wt = im + vdot(ctn, ctn);
     float lamt = POB_DIV(lt, wt);
@@ -220,26 +221,29 @@ POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const
   v3 dv = V(0.0f, 0.0f, 0.0f);
   if (ground) {
     const float vn = vr.z;
-    const float lt = pob_sqrt(FMA(vr.y, vr.y, vr.x * vr.x));
+    float lt, ilt;
+    pob_sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
     if (lt > 0.0f) {
       const float fr = fminf(S.friction * pen * S.inv_h, lt);
-      const float k = -POB_DIV(fr, lt);
+      const float k = -(fr * ilt);
       dv = V(vr.x * k, vr.y * k, 0.0f);
     }
     if (vn < 0.0f) dv.z = -vn;
   } else {
     float vn = vdot(vr, n);
     v3 vt = vfma(n, -vn, vr);
-    float lt = pob_sqrt(vdot(vt, vt));
+    float lt, ilt;
+    pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
     if (lt > 0.0f) {
       float fr = fminf(S.friction * pen * S.inv_h, lt);
-      dv = vscl(vt, -POB_DIV(fr, lt));
+      dv = vscl(vt, -(fr * ilt));
     }
     if (vn < 0.0f) dv = vfma(n, -vn, dv);
   }
-  float D = pob_sqrt(vdot(dv, dv));
+  float D, iD;
+  pob_sqrt_rcp(vdot(dv, dv), D, iD);
   if (D > 0.0f) {
-    v3 dh = vdivs(dv, D);
+    v3 dh = vscl(dv, iD);
     v3 cd = vcross(rr, dh);
     float wgt = im + vdot(cd, cd);
     v3 P = vdivs(dv, wgt);

@@ -79,8 +79,8 @@ POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
   float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
   float pen, nx, ny, nz;
   if (d2 > 0.0f) {
-    float dist = pob_sqrt(d2);
-    const float inv = pob_rcp(dist);
+    float dist, inv;
+    pob_sqrt_rcp(d2, dist, inv);
     pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
   } else {
     float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
@@ -182,16 +182,18 @@ POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&
       v3 vr = vadd(b.v[i], vcross(b.w[i], rr));
       float vn = vdot(vr, n);
       v3 vt = vfma(n, -vn, vr);
-      float lt = pob_sqrt(vdot(vt, vt));
+      float lt, ilt;
+      pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
       v3 dv = V(0.0f, 0.0f, 0.0f);
       if (lt > 0.0f) {
         float fr = fminf(S.friction * pen * S.inv_h, lt);
-        dv = vscl(vt, -POB_DIV(fr, lt));
+        dv = vscl(vt, -(fr * ilt));
       }
       if (vn < 0.0f) dv = vfma(n, -vn, dv);
-      float D = pob_sqrt(vdot(dv, dv));
+      float D, iD;
+      pob_sqrt_rcp(vdot(dv, dv), D, iD);
       if (D > 0.0f) {
-        v3 dh = vdivs(dv, D);
+        v3 dh = vscl(dv, iD);
         v3 cd = vcross(rr, dh);
         float w = im + vdot(cd, cd);
         v3 P = vdivs(dv, w);

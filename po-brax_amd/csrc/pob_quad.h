@@ -125,8 +125,8 @@ POB_D void qwall_end_v(csys_t &S, const float cx, const float cy, const float c,
   if (!(d2 >= T)) {
     float pen, nx, ny, nz;
     if (d2 > 0.0f) {
-      float dist = pob_sqrt(d2);
-      const float inv = pob_rcp(dist);
+      float dist, inv;
+      pob_sqrt_rcp(d2, dist, inv);
       pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
     } else {
       float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
@@ -272,9 +272,9 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
         DA[l] = V(DA[l].x + rr.y * lam, DA[l].y + -(rr.x * lam), DA[l].z);  // rr x P
         const v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
         const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
-        const float lt = pob_sqrt(FMA(dpy, dpy, dpx * dpx));
+        float lt, inv;
+        pob_sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
         if (lt > 0.0f) {
-          const float inv = pob_rcp(lt);
           const float tx = dpx * inv, ty = dpy * inv;
           const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
           const float wt = im + vdot(ctn, ctn);
@@ -299,9 +299,10 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
       v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
       v3 dp = vsub(cp, cprev);
       v3 dpt = vfma(n, -vdot(dp, n), dp);
-      float lt = pob_sqrt(vdot(dpt, dpt));
+      float lt, ilt;
+      pob_sqrt_rcp(vdot(dpt, dpt), lt, ilt);
       if (lt > 0.0f) {
-        v3 t = vdivs(dpt, lt);
+        v3 t = vscl(dpt, ilt);
         v3 ctn = vcross(rr, t);
         float wt = im + vdot(ctn, ctn);
         float lamt = POB_DIV(lt, wt);
@@ -336,26 +337,29 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
       if (c < 2) {
         // ground, n = (0, 0, 1) (zero products dropped, as in the position pass)
         const float vn = vr.z;
-        const float lt = pob_sqrt(FMA(vr.y, vr.y, vr.x * vr.x));
+        float lt, ilt;
+        pob_sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
         if (lt > 0.0f) {
           const float fr = fminf(S.friction * pen * S.inv_h, lt);
-          const float k = -POB_DIV(fr, lt);
+          const float k = -(fr * ilt);
           dv = V(vr.x * k, vr.y * k, 0.0f);
         }
         if (vn < 0.0f) dv.z = -vn;
       } else {
         float vn = vdot(vr, n);
         v3 vt = vfma(n, -vn, vr);
-        float lt = pob_sqrt(vdot(vt, vt));
+        float lt, ilt;
+        pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
         if (lt > 0.0f) {
           float fr = fminf(S.friction * pen * S.inv_h, lt);
-          dv = vscl(vt, -POB_DIV(fr, lt));
+          dv = vscl(vt, -(fr * ilt));
         }
         if (vn < 0.0f) dv = vfma(n, -vn, dv);
       }
-      float D = pob_sqrt(vdot(dv, dv));
+      float D, iD;
+      pob_sqrt_rcp(vdot(dv, dv), D, iD);
       if (D > 0.0f) {
-        v3 dh = vdivs(dv, D);
+        v3 dh = vscl(dv, iD);
         v3 cd = vcross(rr, dh);
         float w = im + vdot(cd, cd);
         v3 P = vdivs(dv, w);
