@@ -78,8 +78,8 @@ struct HContacts {
 // penetration < 0, and the strict ">" of the deepest-contact search keeps the oracle's
 // (wall, end) order.  (Per-body boxes would not shorten the walk: the wave iterates over the
 // most walls any of its lanes is near, a lower leg's.)
-template <bool WALLS>
-POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
+template <bool WALLS, class G>
+POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
   ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
   // (both wall loops are unrolled over POB_MAXW with wave-uniform guards, so the walls' boxes
@@ -115,8 +115,8 @@ POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, 
       const bool on = ((m >> w) & 1u) != 0u;
       if (__any(on)) {
         const auto &R = S.wall_row[w];
-        qwall_end_v(S, R[0], R[1], R[2], R[3], R[4], R[5], pe0, r, T, on, false, best, bn, bsel, bpe);
-        qwall_end_v(S, R[0], R[1], R[2], R[3], R[4], R[5], pe1, r, T, on, true, best, bn, bsel, bpe);
+        qwall_end_v(g, S, R[0], R[1], R[2], R[3], R[4], R[5], pe0, r, T, on, false, best, bn, bsel, bpe);
+        qwall_end_v(g, S, R[0], R[1], R[2], R[3], R[4], R[5], pe1, r, T, on, true, best, bn, bsel, bpe);
       }
     }
   }
@@ -128,9 +128,9 @@ POB_D void hdetect(csys_t &S, const float *HT, const float *WT, const HBody &b, 
 }
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
-template <bool WALLS>
-POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, const float act, v3 &cv, v3 &ca,
-                        const bool COLLIDE) {
+template <bool WALLS, class G>
+POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, HBody &b, const float act, v3 &cv,
+                        v3 &ca, const bool COLLIDE) {
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
   const bool torso = isP && hip, leg = !isP && !hip;
   const v3 px = b.x;
@@ -164,7 +164,7 @@ POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, c
     q4 q = b.q;
     q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
     q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
-    b.q = qnormalize(q);
+    b.q = g.qnorm(q);
   }
   // 3. position projection
   HContacts ct;
@@ -188,11 +188,11 @@ POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, c
       if (L2 > 0.0f) {
         const v3 ep = vcross(rp, d), ec = vcross(rc, d);
         const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
-        const float k = POB_DIV(L2 * S.s_pos, den);
+        const float k = (L2 * S.s_pos) * g.rcp(den);
         P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
       }
       const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
-      const float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+      const float psi = pob_atan2f_g(g, vdot(vcross(fp, fc), ap), vdot(fp, fc));
       float dl = 0.0f;
       if (psi < HT[HT_LO]) dl = psi - HT[HT_LO];
       else if (psi > HT[HT_HI]) dl = psi - HT[HT_HI];
@@ -220,16 +220,16 @@ POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, c
       DA = torso ? dat : (leg ? dal : daa);
     }
     if (COLLIDE) {
-      hdetect<WALLS>(S, HT, WT, b, ct);
+      hdetect<WALLS>(g, S, HT, WT, b, ct);
       const float im = HT[HT_IM];
-      if (ct.gpen > 0.0f) oground_position(S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
-      if (ct.pen > 0.0f) owall_position(S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+      if (ct.gpen > 0.0f) oground_position(g, S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
+      if (ct.pen > 0.0f) owall_position(g, S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
     }
     b.x = vadd(b.x, DX);
     qadd_half(b.q, qmul_vq(DA, b.q), 1.0f);
   }
   // 4. velocity projection
-  b.q = qnormalize(b.q);
+  b.q = g.qnorm(b.q);
   b.v = vscl(vsub(b.x, px), S.inv_h);
   {
     const q4 dq = qmul(b.q, qinv(pq));
@@ -242,11 +242,11 @@ POB_D void hpbd_substep(csys_t &S, const float *HT, const float *WT, HBody &b, c
     v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
     const float im = HT[HT_IM];
     if (ct.gpen > 0.0f)
-      ocontact_vel_one(S, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+      ocontact_vel_one(g, S, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
     if (ct.pen > 0.0f) {
       const v3 e0 = HTV(HT, HT_E0);
       const v3 e = ct.sel ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(S, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
+      ocontact_vel_one(g, S, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
     }
     b.v = vadd(b.v, dV); b.w = vadd(b.w, dW);
     cv = vadd(cv, dV);

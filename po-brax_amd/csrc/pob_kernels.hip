@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 // block; lane r of an env owns one body and one side of one joint (P_hip_r / C_hip_(7-r) /
 // P_knee_(r-8) / C_knee_(15-r)).  Lane 0 (P_hip_0, the torso) runs the per-env POMDP tail.
 #define POB_HSTAGE_FLOATS (OL_FLOATS * 64)
-template <int KIND, typename QT>
+template <int KIND, typename QT, bool GACC>
 __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, const StatePtrs in,
                                                  const float *__restrict__ act, const StatePtrs out,
                                                  const uint32_t flags, const int L) {
@@ -1480,12 +1480,32 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     const float a = act[(size_t)b * POB_NJ + jown];
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    GuardBranch gb;
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
-    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    GuardBranch gb;
+    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
 #else
+    if constexpr (!GACC) {
+      GuardBranch gb;
 #pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+    } else {
+    // one wave per SIMD (GACC): the substeps without guard branches (GuardAcc, pob_math.h); a wave any of whose lanes
+    // met an operand outside the fast forms' range reruns them from the loaded state with
+    // the branch guards (bit-identical for every lane that stayed in range)
+    const HBody b0 = bd;
+    GuardAcc ga;
+#pragma nounroll
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(ga, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+    if (__builtin_expect(__any(ga.bad()), 0)) {
+      bd = b0;
+      cvl = V(0.0f, 0.0f, 0.0f); cal = cvl;
+      GuardBranch gb;
+#pragma nounroll
+      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+    }
+    }
 #endif
     {  // joint angle / velocity obs of the lane's joint (a3), on both of its lanes
       const q4 qo = hx_pair4(bd.q);
@@ -2222,16 +2242,28 @@ static int hexa_max_batch() {
   const char *e = getenv("POB_HEXA_MAX_B");
   return e ? atoi(e) : 8192;
 }
-template <typename QT>
-static void launch_step_hex(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
-                            const StatePtrs &po, uint32_t flags, int L) {
+template <typename QT, bool GACC>
+static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
+                              const StatePtrs &po, uint32_t flags, int L) {
   const dim3 g((unsigned)((B + 3) / 4)), b(64);
   switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_hex<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step_hex<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_TAG: hipLaunchKernelGGL((k_step_hex<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    default: hipLaunchKernelGGL((k_step_hex<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_hex<POB_HEAVENHELL, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_hex<POB_GATHER, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_hex<POB_TAG, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_hex<POB_ANT, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
+}
+// Up to one wave per SIMD (B <= the SIMD count x 4 envs) the wave's dependency chain is the
+// step time and the guard branches split it (GuardAcc, measured HH B=4 096 -3.5 %); with two
+// or more waves per SIMD the other wave hides them and the accumulator's VALU operations cost
+// (B = 8 192: TAG / GA +1 %), so the branch guards stay.  POB_HEX_GACC=0/1 forces either.
+template <typename QT>
+static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+                            const float *act, const StatePtrs &po, uint32_t flags, int L) {
+  const char *f = getenv("POB_HEX_GACC");
+  const bool acc = f ? atoi(f) != 0 : (B + 3) / 4 <= 4 * n_cu;
+  if (acc) launch_step_hex_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
+  else launch_step_hex_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
 }
 template <typename QT>
 static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
@@ -2398,8 +2430,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   const void *sp = (const void *)e->d_sys;
   const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch();  // legacy: lane quads only
   const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();
-  if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
-  else if (hex) launch_step_hex<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
+  else if (hex) launch_step_hex<float>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
   else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);

@@ -229,10 +229,11 @@ POB_D void qadd_half(q4 &acc, q4 d, float sign) {
 // polynomial on [0, 1] (7.2e-8 relative), then pi/2 - r, pi - r and the sign of y by selects:
 // <= 4 ulp against atan2 over the whole plane (no divergent branches, no division).  NaN
 // inputs give NaN.
-POB_D float pob_atan2f(float y, float x) {
+template <class G>
+POB_D float pob_atan2f_g(G &g, float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
   const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-  float t = mn * pob_rcp(mx);
+  float t = mn * g.rcp(mx);
   t = mx > 0.0f ? t : 0.0f;
   const float s = t * t;
   float p = FMA(s, -0.0047533135f, 0.024452504f);
@@ -247,6 +248,47 @@ POB_D float pob_atan2f(float y, float x) {
   r = x < 0.0f ? 3.1415927f - r : r;
   r = __builtin_copysignf(r, y);
   return r + (x * 0.0f + y * 0.0f);  // + 0, or NaN for NaN / infinite inputs
+}
+
+// Range-guard policies of the exact fast forms (pob_rcp / pob_sqrt_rcp / qnormalize).
+// GuardBranch: each operation checks its operand and takes the exact slow form behind its
+// own wave-uniform branch.  GuardAcc: no branches -- every operand's magnitude bits are
+// folded into one per-lane register (distance above the range's low end, shifted so the
+// sign drops out: out of range <=> above 0xC0000000), and the caller reruns the whole
+// computation under GuardBranch when any lane of the wave saw an operand out of range.
+// In range both give the same bits (the fast forms are exact there), so a rerun changes
+// nothing for the lanes that were in range.  The branches split the latency-bound
+// kernels' basic blocks; the accumulator is one or two VALU operations off the chain.
+struct GuardBranch {
+  POB_D float rcp(float x) { return pob_rcp(x); }
+  POB_D void sqrt_rcp(float x, float &s, float &i) { pob_sqrt_rcp(x, s, i); }
+  POB_D q4 qnorm(q4 q) { return qnormalize(q); }
+};
+struct GuardAcc {
+  uint32_t m = 0u;
+  POB_D void note(float x) {  // |x| in [2^-96, 2^96] <=> (bits << 1) - bits(2^-96) << 1 <= 0xC0000000
+    const uint32_t t = (__float_as_uint(x) << 1) - 0x1F000000u;
+    m = m > t ? m : t;
+  }
+  POB_D bool bad() const { return m > 0xC0000000u; }
+  POB_D float rcp(float x) { note(x); return pob_rcp_fast(x); }
+  POB_D void sqrt_rcp(float x, float &s, float &i) {
+    note(x);
+    s = pob_sqrt_fast(x);
+    i = pob_rcp_fast(s);
+  }
+  POB_D q4 qnorm(q4 q) {  // qnormalize's polynomial; |e| > 2^-6 (or NaN) maps above 2^96
+    const float n2 = FMA(q.z, q.z, FMA(q.y, q.y, FMA(q.x, q.x, q.w * q.w)));
+    const float e = n2 - 1.0f;
+    const float inv = FMA(FMA(FMA(-0.3125f, e, 0.375f), e, -0.5f), e, 1.0f);
+    note(FMA(fabsf(e), 0x1p102f, 1.0f));
+    q4 r; r.w = q.w * inv; r.x = q.x * inv; r.y = q.y * inv; r.z = q.z * inv;
+    return r;
+  }
+};
+POB_D float pob_atan2f(float y, float x) {
+  GuardBranch g;
+  return pob_atan2f_g(g, y, x);
 }
 // Cephes-form sinf/cosf (Cody-Waite reduction by pi/4)
 POB_D void pob_sincosf(float x, float *s, float *c) {

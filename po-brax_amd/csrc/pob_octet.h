@@ -139,23 +139,24 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
 }
 
 // position-level ground contact (n = +z; qcontact_position's ground branch) on body (x, q)
-POB_D void oground_position(csys_t &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
+template <class G = GuardBranch>
+POB_D void oground_position(G &g, csys_t &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
                             const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
   const v3 cp = V(pe.x, pe.y, pe.z - rad);
   const v3 rr = vsub(cp, x);
   const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
-  const float lam = POB_DIV(pen, w);
+  const float lam = (pen * g.rcp(w));
   DX.z = FMA(lam, im, DX.z);  // P = (0, 0, lam)
   DA = V(DA.x + rr.y * lam, DA.y + -(rr.x * lam), DA.z);  // rr x P
   const v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
   const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
   float lt, inv;
-  pob_sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
+  g.sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
   if (lt > 0.0f) {
     const float tx = dpx * inv, ty = dpy * inv;
     const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
     const float wt = im + vdot(ctn, ctn);
-    const float lamt = POB_DIV(lt, wt);
+    const float lamt = (lt * g.rcp(wt));
     if (lamt < S.friction * lam) {
       const float px_ = tx * -lamt, py_ = ty * -lamt;
       DX.x = FMA(px_, im, DX.x);
@@ -166,13 +167,14 @@ POB_D void oground_position(csys_t &S, const float pen, const v3 pe, const float
 }
 
 // position-level wall contact (qcontact_position's general branch)
-POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
+template <class G = GuardBranch>
+POB_D void owall_position(G &g, csys_t &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
                           const v3 x, const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
   v3 cp = vfma(n, -rad, pe);
   v3 rr = vsub(cp, x);
   v3 cn = vcross(rr, n);
   float w = im + vdot(cn, cn);
-  float lam = POB_DIV(pen, w);
+  float lam = (pen * g.rcp(w));
   v3 P = vscl(n, lam);
   DX = vfma(P, im, DX);
   DA = vadd(DA, vcross(rr, P));
@@ -180,12 +182,12 @@ POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, c
   v3 dp = vsub(cp, cprev);
   v3 dpt = vfma(n, -vdot(dp, n), dp);
   float lt, ilt;
-  pob_sqrt_rcp(vdot(dpt, dpt), lt, ilt);
+  g.sqrt_rcp(vdot(dpt, dpt), lt, ilt);
   if (lt > 0.0f) {
     v3 t = vscl(dpt, ilt);
     v3 ctn = vcross(rr, t);
     float wt = im + vdot(ctn, ctn);
-    float lamt = POB_DIV(lt, wt);
+    float lamt = (lt * g.rcp(wt));
     if (lamt < S.friction * lam) {
       v3 Pt = vscl(t, -lamt);
       DX = vfma(Pt, im, DX);
@@ -197,6 +199,7 @@ POB_D void owall_position(csys_t &S, const float pen, const v3 pe, const v3 n, c
 // contact processing order of one body = the oracle's: ground contact first, then wall
 POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const v3 (&pxs)[ONB],
                              const q4 (&pqs)[ONB], const OContacts &ct, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
+  GuardBranch gb;
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
@@ -205,14 +208,15 @@ POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, con
     const q4 pq = pqs[s];
     const v3 px = pxs[s];
     const bool g = (s == 1) == gslot1;  // this slot holds the lane's ground body
-    if (g && ct.gpen > 0.0f) oground_position(S, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+    if (g && ct.gpen > 0.0f) oground_position(gb, S, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
     if (ct.pen[s] > 0.0f)
-      owall_position(S, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+      owall_position(gb, S, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
   }
 }
 
 // velocity-level contact (qcontact_velocity's body of one contact); e = the body-frame end
-POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
+template <class G = GuardBranch>
+POB_D void ocontact_vel_one(G &g, csys_t &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
                             const float im, const v3 x, const q4 q, const v3 v, const v3 w, v3 &dV, v3 &dW) {
   v3 pe = vadd(x, qrot_xy(e, q));
   v3 cp = vfma(n, -rad, pe);
@@ -222,7 +226,7 @@ POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const
   if (ground) {
     const float vn = vr.z;
     float lt, ilt;
-    pob_sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
+    g.sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
     if (lt > 0.0f) {
       const float fr = fminf(S.friction * pen * S.inv_h, lt);
       const float k = -(fr * ilt);
@@ -233,7 +237,7 @@ POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const
     float vn = vdot(vr, n);
     v3 vt = vfma(n, -vn, vr);
     float lt, ilt;
-    pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
+    g.sqrt_rcp(vdot(vt, vt), lt, ilt);
     if (lt > 0.0f) {
       float fr = fminf(S.friction * pen * S.inv_h, lt);
       dv = vscl(vt, -(fr * ilt));
@@ -241,12 +245,12 @@ POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const
     if (vn < 0.0f) dv = vfma(n, -vn, dv);
   }
   float D, iD;
-  pob_sqrt_rcp(vdot(dv, dv), D, iD);
+  g.sqrt_rcp(vdot(dv, dv), D, iD);
   if (D > 0.0f) {
     v3 dh = vscl(dv, iD);
     v3 cd = vcross(rr, dh);
     float wgt = im + vdot(cd, cd);
-    v3 P = vdivs(dv, wgt);
+    v3 P = vscl(dv, g.rcp(wgt));
     dV = vfma(P, im, dV);
     dW = vadd(dW, vcross(rr, P));
   }
@@ -254,6 +258,7 @@ POB_D void ocontact_vel_one(csys_t &S, const bool ground, const float pen, const
 
 POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const OContacts &ct,
                              v3 (&dV)[ONB], v3 (&dW)[ONB]) {
+  GuardBranch gb;
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
@@ -261,12 +266,12 @@ POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, con
     const float im = OT[OT_B(s)];
     const bool g = (s == 1) == gslot1;
     if (g && ct.gpen > 0.0f)
-      ocontact_vel_one(S, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
+      ocontact_vel_one(gb, S, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
                        b.w[s], dV[s], dW[s]);
     if (ct.pen[s] > 0.0f) {
       const v3 e0 = OTV(OT, OT_B(s) + 2);
       const v3 e = ct.sel[s] ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(S, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
+      ocontact_vel_one(gb, S, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
                        dW[s]);
     }
   }

@@ -113,7 +113,8 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 // sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
 // (the row's six floats given as values: LDS rows for a per-lane wall walk, the system
 // table's scalars for a wave-uniform one)
-POB_D void qwall_end_v(csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
+template <class G = GuardBranch>
+POB_D void qwall_end_v(G &g, csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
                        const float hy, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn, bool &bsel,
                        v3 &bpe) {
   const v3 h = V(hx, hy, S.wall_hz);
@@ -126,7 +127,7 @@ POB_D void qwall_end_v(csys_t &S, const float cx, const float cy, const float c,
     float pen, nx, ny, nz;
     if (d2 > 0.0f) {
       float dist, inv;
-      pob_sqrt_rcp(d2, dist, inv);
+      g.sqrt_rcp(d2, dist, inv);
       pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
     } else {
       float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
@@ -148,7 +149,8 @@ POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on,
   const float2 r01 = *reinterpret_cast<const float2 *>(R);
   const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
   const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
-  qwall_end_v(S, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, p, r, T, on, q1, best, bn, bsel, bpe);
+  GuardBranch g;
+  qwall_end_v(g, S, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, p, r, T, on, q1, best, bn, bsel, bpe);
 }
 
 // Contact detection of a collide substep on a lane quad.  Walls: every lane keeps a mask
