@@ -95,11 +95,11 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
 #endif
 #pragma unroll
     for (int w = 0; w < POB_MAXW; ++w) {
-      if (w < nw) {
-        const bool near = b.x.x <= S.wall_hi[w][0] && b.x.x >= S.wall_lo[w][0] && b.x.y <= S.wall_hi[w][1] &&
-                          b.x.y >= S.wall_lo[w][1];
-        m |= near ? 1u << w : 0u;
-      }
+      // every wall's box is loaded (the table always holds POB_MAXW rows) and w < nw is a
+      // predicate: loads behind a per-wall branch were one scalar round trip per wall
+      const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
+      const bool near = (b.x.x <= hx) & (b.x.x >= lx) & (b.x.y <= hy) & (b.x.y >= ly);
+      m |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
   float best = 0.0f;
@@ -110,13 +110,18 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
     const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
     const float r = HT[HT_R];
     const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
+    // every wall row in one scalar round trip (not one per near wall inside its branch)
+    float R[POB_MAXW][POB_WALL_FLOATS];
+#pragma unroll
+    for (int w = 0; w < POB_MAXW; ++w)
+#pragma unroll
+      for (int k = 0; k < POB_WALL_FLOATS; ++k) R[w][k] = S.wall_row[w][k];
 #pragma unroll
     for (int w = 0; w < POB_MAXW; ++w) {
       const bool on = ((m >> w) & 1u) != 0u;
       if (__any(on)) {
-        const auto &R = S.wall_row[w];
-        qwall_end_v(g, S, R[0], R[1], R[2], R[3], R[4], R[5], pe0, r, T, on, false, best, bn, bsel, bpe);
-        qwall_end_v(g, S, R[0], R[1], R[2], R[3], R[4], R[5], pe1, r, T, on, true, best, bn, bsel, bpe);
+        qwall_end_v(g, S, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
+        qwall_end_v(g, S, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
       }
     }
   }

@@ -102,10 +102,13 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
 #else
     const int nw = S.n_walls;
 #endif
-    for (int w = 0; w < nw; ++w) {
-      const bool near = mnx <= S.wall_hi[w][0] && mxx >= S.wall_lo[w][0] && mny <= S.wall_hi[w][1] &&
-                        mxy >= S.wall_lo[w][1];
-      lane_mask |= near ? 1u << w : 0u;
+#pragma unroll
+    for (int w = 0; w < POB_MAXW; ++w) {
+      // all POB_MAXW boxes loaded at once, w < nw as a predicate (a runtime loop waited
+      // one scalar-load round trip per wall)
+      const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
+      const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
+      lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
   const bool any_near = WALLS && __any(lane_mask != 0u);
