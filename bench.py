@@ -337,7 +337,7 @@ def step_kernel(B: int) -> str:
 def committed_profile(env: str, B: int, qp: str):
     """Counters per launch from the newest committed PMC profile of this exact config
     (profiles/*_traffic.json, written by profiles/summarize.py); None if there is none."""
-    best = None
+    best, key = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
         try:
             t = json.load(open(p))
@@ -345,7 +345,9 @@ def committed_profile(env: str, B: int, qp: str):
             continue
         if t.get("env") == env and t.get("batch") == B and t.get("qp_storage", "f32") == qp and \
                 "k_step" in (t.get("kernel") or ""):
-            best = t
+            k = (t.get("generated", 0.0), p)  # newest by the summary's timestamp, then name
+            if key is None or k > key:
+                best, key = t, k
     return best
 
 

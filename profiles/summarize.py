@@ -11,6 +11,7 @@ import json
 import os
 import shutil
 import sys
+import time
 
 
 def main(src, dst_prefix):
@@ -61,6 +62,7 @@ def main(src, dst_prefix):
                    "waves": mean("SQ_WAVES"),
                    "kernel_avg_ns": next((float(r["AverageNs"]) for r in stats if "k_step" in r["Name"]), None),
                    "source": os.path.basename(dst_prefix) + "_summary.md"}
+        traffic["generated"] = time.time()  # bench.committed_profile takes the newest
         json.dump(traffic, open(dst_prefix + "_traffic.json", "w"), indent=1)
     for j in ("trace.bench.json",):
         p = os.path.join(src, j)

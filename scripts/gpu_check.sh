@@ -17,6 +17,7 @@ run() {  # name, bench args...
   timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err || exit 1
 }
 run hh_4096 --batch 4096 &&
+run tag_8192 --env ant_tag --batch 8192 &&
 run ga_16384 --env ant_gather --batch 16384 &&
 run tag_65536 --env ant_tag --batch 65536 &&
 run mixed_f16_32768 --env mixed --qp-dtype f16 --batch 32768 &&
