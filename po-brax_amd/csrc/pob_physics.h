@@ -25,13 +25,13 @@ struct Contacts {
   bool sel[POB_NDYN];
 };
 
-// Hide the table pointer from loop-invariant code motion: without this the compiler
-// hoists every table value of an unrolled block into SGPRs and spills them.
-// Re-laundering per joint / contact keeps each value's scalar load next to its use
-// (scalar-cache hits).
+// launder(): with POB_LAUNDER the table pointer is hidden from loop-invariant code motion
+// (each table value's scalar load stays next to its use).  Round 1 needed it against SGPR
+// spills; with the scheduling fences and the current kernels the compiler's own placement
+// measured 0.7-0.9 % faster at B = 65 536 (HH, TAG, ant; no new scratch), so it is off.
 typedef __attribute__((address_space(4))) const pob_sys csys_t;  // constant address space
 POB_D csys_t *launder(csys_t *p) {
-#ifndef POB_NO_LAUNDER
+#ifdef POB_LAUNDER
   asm volatile("" : "+s"(p));
 #endif
   return p;
