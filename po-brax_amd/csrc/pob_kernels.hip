@@ -2050,6 +2050,9 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   // the next step's any-done word (gym wrapper, double-buffered): the step before this launch
   // used the other word, and the next launch on the stream reads this one after it is zero
   if (s.any_done_clear && blockIdx.x == 0 && lane == 0) *s.any_done_clear = 0u;
+  bool active = b < B;
+  // the env's done flag is loaded together with the any-done word (one round trip, not two)
+  const float dn = active && mode != RESET_FULL ? s.done[b] : 1.0f;
   if (mode == RESET_GYM) {
     const bool any = *any_flag != 0u;
     if (b == 0 && k == 0 && gym_out) {
@@ -2059,10 +2062,20 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     }
     if (!any) return;  // block-uniform
   }
-  bool active = b < B;
-  if (active && mode != RESET_FULL) active = s.done[b] != 0.0f;
+  active = active && dn != 0.0f;
   const uint64_t lanes = __ballot(active && k == 0);
   if (lanes == 0ull) return;  // block-uniform (a masked reset with no done env in this wave)
+  // the system table's loads are issued here and land in LDS after the key hashes below
+  constexpr int TPL = (POB_TAB_FLOATS + BS - 1) / BS;
+  float tabv[TPL];
+  {
+    const __attribute__((address_space(4))) float *src = &Sp->leg[0][0];
+#pragma unroll
+    for (int i = 0; i < TPL; ++i) {
+      const int j = lane + BS * i;
+      tabv[i] = j < POB_TAB_FLOATS ? src[j] : 0.0f;
+    }
+  }
   // keys of the envs to reset only (a gym key is a threefry hash: a wave without a done env
   // computes none)
   uint32_t k0 = 0u, k1 = 0u;
@@ -2076,7 +2089,12 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   uint32_t rows = 0u;  // bit e: env e0 + e is reset
 #pragma unroll
   for (int e = 0; e < 16; ++e) rows |= (uint32_t)((lanes >> (4 * e)) & 1ull) << e;
-  stage_leg_table(Sp, legtab);
+#pragma unroll
+  for (int i = 0; i < TPL; ++i) {
+    const int j = lane + BS * i;
+    if (j < POB_TAB_FLOATS) legtab[j] = tabv[i];
+  }
+  __syncthreads();
   const float *LT = legtab + k * POB_LEG_FLOATS;
   const float *WT = legtab + 4 * POB_LEG_FLOATS;
   QReset R;

@@ -22,11 +22,12 @@ for env in ${ENVS:-ant_heavenhell}; do
   done
 done
 python - <<'PY'
-import glob, json, collections, statistics
+import glob, json, collections, os, statistics
 d = collections.defaultdict(list)
 for f in glob.glob("gpurun_out/ab/*.json"):
     tag, env, B, r = f.split("/")[-1][:-5].rsplit(".", 3)
-    d[(env, B, tag)].append(json.load(open(f))["roofline"]["kernel_ms"])
+    j = json.load(open(f))
+    d[(env, B, tag)].append(j["ms_per_step"] if os.environ.get("FIELD") == "step" else j["roofline"]["kernel_ms"])
 for k in sorted(d):
     print(*k, "median %.4f" % statistics.median(d[k]), "runs", " ".join("%.4f" % x for x in sorted(d[k])))
 PY
