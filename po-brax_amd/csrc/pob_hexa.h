@@ -59,6 +59,13 @@ POB_D q4 hx_pair4(q4 q) {
   q4 r; r.w = hx_pair(q.w); r.x = hx_pair(q.x); r.y = hx_pair(q.y); r.z = hx_pair(q.z); return r;
 }
 
+// Walls a kind's table can hold (pob_system.cpp: the HH T-maze 8, the GA / TAG arenas 4,
+// the stock ant none): the sixteen-lane wall loops run over this many rows, and the launch
+// checks n_walls against it.
+__host__ __device__ constexpr int hex_max_walls(int kind) {
+  return kind == POB_ANT ? 0 : (kind == POB_HEAVENHELL ? POB_MAXW : 4);
+}
+
 struct HBody {
   v3 x, v, w;
   q4 q;
@@ -78,7 +85,7 @@ struct HContacts {
 // penetration < 0, and the strict ">" of the deepest-contact search keeps the oracle's
 // (wall, end) order.  (Per-body boxes would not shorten the walk: the wave iterates over the
 // most walls any of its lanes is near, a lower leg's.)
-template <bool WALLS, class G>
+template <int MW, class G>
 POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
   ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
@@ -87,14 +94,14 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
   // re-loads them each iteration, one scalar-load round trip per wall -- with four envs per
   // wave the union of the walls near any lane is as short as the longest per-lane walk)
   uint32_t m = 0u;
-  if (WALLS) {
+  if (MW > 0) {
 #ifdef POB_EXP_NO_WALLS
     const int nw = 0;  // timing experiment only
 #else
     const int nw = S.n_walls;
 #endif
 #pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w) {
+    for (int w = 0; w < MW; ++w) {
       // every wall's box is loaded (the table always holds POB_MAXW rows) and w < nw is a
       // predicate: loads behind a per-wall branch were one scalar round trip per wall
       const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
@@ -105,19 +112,19 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
   float best = 0.0f;
   v3 bn = V(0.0f, 0.0f, 0.0f), bpe = bn;
   bool bsel = false;
-  if (WALLS && __any(m != 0u)) {
+  if (MW > 0 && __any(m != 0u)) {
     const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
     const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
     const float r = HT[HT_R];
     const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
     // every wall row in one scalar round trip (not one per near wall inside its branch)
-    float R[POB_MAXW][POB_WALL_FLOATS];
+    float R[MW > 0 ? MW : 1][POB_WALL_FLOATS];
 #pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w)
+    for (int w = 0; w < MW; ++w)
 #pragma unroll
       for (int k = 0; k < POB_WALL_FLOATS; ++k) R[w][k] = S.wall_row[w][k];
 #pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w) {
+    for (int w = 0; w < MW; ++w) {
       const bool on = ((m >> w) & 1u) != 0u;
       if (__any(on)) {
         qwall_end_v(g, S, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
@@ -133,7 +140,7 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
 }
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
-template <bool WALLS, class G>
+template <int MW, class G>
 POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, HBody &b, const float act, v3 &cv,
                         v3 &ca, const bool COLLIDE) {
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
@@ -225,7 +232,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, HBody
       DA = torso ? dat : (leg ? dal : daa);
     }
     if (COLLIDE) {
-      hdetect<WALLS>(g, S, HT, WT, b, ct);
+      hdetect<MW>(g, S, HT, WT, b, ct);
       const float im = HT[HT_IM];
       if (ct.gpen > 0.0f) oground_position(g, S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
       if (ct.pen > 0.0f) owall_position(g, S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);

@@ -1481,15 +1481,15 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
     GuardBranch gb;
-    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
 #else
     if constexpr (!GACC) {
       GuardBranch gb;
 #pragma nounroll
-      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
     } else {
     // one wave per SIMD (GACC): the substeps without guard branches (GuardAcc, pob_math.h); a wave any of whose lanes
     // met an operand outside the fast forms' range reruns them from the loaded state with
@@ -1497,13 +1497,13 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     const HBody b0 = bd;
     GuardAcc ga;
 #pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(ga, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(ga, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
     if (__builtin_expect(__any(ga.bad()), 0)) {
       bd = b0;
       cvl = V(0.0f, 0.0f, 0.0f); cal = cvl;
       GuardBranch gb;
 #pragma nounroll
-      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<KIND != POB_ANT>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
     }
     }
 #endif
@@ -2446,7 +2446,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch();  // legacy: lane quads only
+  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch() &&  // legacy: lane quads only
+                   e->sys.n_walls <= hex_max_walls(e->sys.kind);
   const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();
   if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (hex) launch_step_hex<float>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
