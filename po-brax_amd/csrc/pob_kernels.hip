@@ -1211,12 +1211,12 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = V(0.0f, 0.0f, 0.0f); cal[sl] = V(0.0f, 0.0f, 0.0f); }
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
-    for (int it = 0; it < 0 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
 #else
 #pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<KIND != POB_ANT>(Sp, OT, WT, isA, bd, a, cvl, cal, (it & 1) != 0);
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, (it & 1) != 0);
 #endif
     {  // joint angle / velocity obs of the lane's joint (a3)
       const v3 ap = qrot(OTV(OT, OT_AXIS), bd.q[0]);
@@ -2448,7 +2448,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   const void *sp = (const void *)e->d_sys;
   const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch() &&  // legacy: lane quads only
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);
-  const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch();
+  const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch() &&
+                   e->sys.n_walls <= hex_max_walls(e->sys.kind);
   if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (hex) launch_step_hex<float>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);

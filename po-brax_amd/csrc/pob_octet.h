@@ -84,7 +84,7 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
 // Contact detection of a collide substep on one lane: the ground contact of its ground
 // body and, per slot, the deepest wall contact over the walls near the lane's two body
 // centres (qdetect's exact per-lane broadphase and d2 pre-cull, wall rows in LDS).
-template <bool WALLS>
+template <int MW>
 POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslot1, const OBody &b, OContacts &ct) {
   {
     const v3 xg = vsel3(gslot1, b.x[1], b.x[0]);
@@ -93,7 +93,7 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
     ct.gpen = OT[OT_G + 3] - ct.gpe.z;
   }
   uint32_t lane_mask = 0u;
-  if (WALLS) {
+  if (MW > 0) {
     const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
     const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
     csys_t &S = *OLAUNDER(Sp);
@@ -103,15 +103,15 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
     const int nw = S.n_walls;
 #endif
 #pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w) {
-      // all POB_MAXW boxes loaded at once, w < nw as a predicate (a runtime loop waited
+    for (int w = 0; w < MW; ++w) {
+      // all MW boxes loaded at once, w < nw as a predicate (a runtime loop waited
       // one scalar-load round trip per wall)
       const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
       const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
       lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
-  const bool any_near = WALLS && __any(lane_mask != 0u);
+  const bool any_near = MW > 0 && __any(lane_mask != 0u);
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     POB_FENCE();
@@ -317,7 +317,7 @@ POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &
 // (the substep-start poses px / pq and the Info.contact accumulators cv / ca stay in
 // registers: at one or two waves per SIMD there are registers to spare, and an LDS round
 // trip would sit on the lone wave's dependency chain)
-template <bool WALLS>
+template <int MW>
 POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool isA, OBody &b, const float act,
                         v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE) {
   v3 px[ONB];
@@ -400,7 +400,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       DX[1] = vsel3(isA, dx_aux, dx_leg); DA[1] = vsel3(isA, da_aux, da_leg);
     }
     if (COLLIDE) {
-      odetect<WALLS>(Sp, OT, WT, gslot1, b, ct);
+      odetect<MW>(Sp, OT, WT, gslot1, b, ct);
       ocontact_position(Sp, OT, gslot1, b, px, pq, ct, DX, DA);
     }
 #pragma unroll
