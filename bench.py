@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py -- env-steps/s of the fused MI355X rollout step (BASELINE.json metric).
 
-Workload (BASELINE.json configs / SURVEY.md §8(d)): AntHeavenHell, batch 65 536 per GPU,
-brax chain ``create('ant_heavenhell', batch_size=B)`` = AutoReset(Vmap(Episode(ActionRepeat
+Workload (BASELINE.json configs / SURVEY.md §8(d)): AntHeavenHell, batch 65 536 (the
+metric's "batch 65536 @1/2/4/8 GPU": the global batch split over the N ranks), brax chain ``create('ant_heavenhell', batch_size=B)`` = AutoReset(Vmap(Episode(ActionRepeat
 (env)))) with episode_length 1000, i.e. ONE fused HIP kernel per env-step (PBD physics,
 POMDP logic, obs, episode counter, autoreset).  Synthetic inputs as the survey prescribes:
 ``key = PRNGKey(0)``, reset keys ``split(key, B_total + 1)[1:]`` (sharded by index), per step
@@ -10,13 +10,15 @@ POMDP logic, obs, episode counter, autoreset).  Synthetic inputs as the survey p
 device by the threefry kernels BEFORE the timed region (inputs resident in HBM).
 
 Modes (other BASELINE configs):
-  --batch B              envs per GPU (weak scaling, the default: B = 65 536 per GPU)
-  --global-batch G       G envs split over the ranks (strong scaling): config 4 is
-                         ``--env ant_tag --global-batch 65536 --gather-obs`` and config 5
+  --global-batch G       G envs split over the ranks (strong scaling; the default, G = 65 536):
+                         config 4 is ``--env ant_tag --gather-obs`` and config 5
                          ``--env mixed --qp-dtype f16 --global-batch 262144``
-  --gather-obs           RCCL all-gather of the observation batch inside every timed step
+  --batch B              B envs PER GPU instead (weak scaling, opt-in; labelled "weak")
+  --gather-obs           RCCL all-gather of the observation batch of every timed step, on a
+                         side stream overlapped with the next step (sharding.ObsGatherer)
   --gym                  the create_gym_env path (AutoresetVmapGymWrapper: step kernel,
-                         cross-rank any-done all-reduce, masked gym reset kernel)
+                         cross-rank any-done all-reduce, masked gym reset kernel); on one
+                         GPU the K gym steps are replayed from a hipGraph too
 
 Multi-GPU: one process per GPU (torchrun); barrier + synchronize bracket the K timed steps
 and the max over ranks is reported.  Rank 0 prints ONE JSON line.
@@ -46,6 +48,7 @@ _TASK_READ = {"ant_heavenhell": 6, "ant_gather": 48, "ant_tag": 2, "ant": 0}
 _TASK_WRITE = {"ant_heavenhell": 0, "ant_gather": 48, "ant_tag": 3, "ant": 0}
 _OBS = {"ant_heavenhell": 114, "ant_gather": 211, "ant_tag": 103, "ant": 87}
 MIXED = ("ant_heavenhell", "ant_gather", "ant_tag")  # --env mixed (BASELINE.json config 5)
+HEADLINE_METRIC = "env-steps/sec AntHeavenHell batch 65536 @1/2/4/8 GPU; % HBM roofline"  # BASELINE.json
 VALU_PEAK_TF = 157.3   # FP32 vector peak, MI355X_MICROARCH.md (chip-level parameters)
 HBM_PEAK_GBS = 8000.0  # HBM3E spec peak
 SIMDS = 1024           # 256 CUs x 4 SIMDs
@@ -73,15 +76,16 @@ def main() -> int:
                     help="'mixed' = HH + GA + TAG batches (B split 3 ways) in one launch per step")
     ap.add_argument("--qp-dtype", default="f32", choices=["f32", "f16"],
                     help="qp storage (f16 = binary16 qp, float32 arithmetic)")
-    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU (weak scaling)")
-    ap.add_argument("--global-batch", type=int, default=0,
-                    help="total envs split over the ranks (strong scaling); overrides --batch")
+    ap.add_argument("--global-batch", type=int, default=65536,
+                    help="total envs split over the ranks (strong scaling, the default)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="envs PER GPU (weak scaling, opt-in); overrides --global-batch")
     ap.add_argument("--episode-length", type=int, default=1000)
     ap.add_argument("--gym", action="store_true", help="create_gym_env path (gym-side autoreset)")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU-baseline budget per leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-obs", action="store_true",
-                    help="RCCL all-gather of the obs batch inside every timed step (N>1)")
+                    help="RCCL all-gather of every timed step's obs batch, overlapped with the next step (N>1)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 ('nccl' = RCCL; 'gloo' lets several ranks share "
                          "one GPU for a functional rehearsal, not a measurement)")
@@ -89,7 +93,7 @@ def main() -> int:
                     help="graph rollout: env groups stepped on their own streams (rollout.GraphRollout)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
-                         "hipGraph (po_brax_amd.rollout); the gym and --gather-obs paths are always eager")
+                         "hipGraph (po_brax_amd.rollout); --gather-obs and the sharded gym path are eager")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,9 +111,9 @@ def main() -> int:
         ap.error("--gym runs one env kind")
 
     from po_brax_amd import envs, jumpy
-    from po_brax_amd.sharding import Shard, gather_obs, gather_obs_ragged, shard_keys
+    from po_brax_amd.sharding import ObsGatherer, Shard, shard_keys
 
-    strong = args.global_batch > 0
+    strong = args.batch <= 0
     total = args.global_batch if strong else args.batch * world
     shard = Shard(total, world, rank)
     lo, B = shard.lo, shard.size
@@ -156,38 +160,39 @@ def main() -> int:
         return torch.cat([s.obs.reshape(-1) for s in state]) if args.env == "mixed" else state.obs
 
     do_gather = args.gather_obs and world > 1 and args.env != "mixed"
-    equal = total % world == 0
+    gatherer = ObsGatherer(total, obs_of().shape[-1], device=dev) if do_gather else None
+    gather_ms = []
 
     def one_step(t):
         if gym is not None:
             gym.step(act_at(t))
         else:
             env.step_(state, act_at(t))
-
-    def gather():
-        o = obs_of()
-        return gather_obs(o) if equal else gather_obs_ragged(o, total)
+        if gatherer is not None:  # step t's obs gathered on the side stream during step t + 1
+            gatherer.submit(obs_of())
 
     for t in range(args.warmup):
         one_step(t)
-        if do_gather:
-            gather()
     torch.cuda.synchronize()
 
-    use_graph = not args.no_graph and gym is None and not do_gather and pre
+    # the gym path's K steps replay from a graph too when it has no cross-rank all-reduce
+    use_graph = not args.no_graph and not do_gather and pre and (gym is None or world == 1) and \
+        (gym is None or args.steps % 2 == 0)
     roll = None
     if use_graph:  # capture the K timed steps (capture does not run them)
-        from po_brax_amd.rollout import GraphRollout
-        roll = GraphRollout(env, state, acts[args.warmup:args.warmup + args.steps],
-                            groups=args.groups if args.env != "mixed" else 1)
+        from po_brax_amd.rollout import GraphRollout, GymGraphRollout
+        if gym is not None:
+            roll = GymGraphRollout(gym, acts[args.warmup:args.warmup + args.steps])
+        else:
+            roll = GraphRollout(env, state, acts[args.warmup:args.warmup + args.steps],
+                                groups=args.groups if args.env != "mixed" else 1)
 
-    # timed region: K steps.  Eager: events bracket each step's kernels (and, with
-    # --gather-obs, the all-gather after them) on torch's current stream, which the kernels
-    # use.  Graph: one replay of the K captured steps; the per-kernel time then comes from
-    # an eager pass of K more steps after the timed region.
+    # timed region: K steps.  Eager: events bracket each step's kernels on torch's current
+    # stream, which the kernels use (with --gather-obs the all-gathers run on their own
+    # stream, overlapped).  Graph: one replay of the K captured steps; the per-kernel time
+    # then comes from an eager pass of K more steps after the timed region.
     ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_c = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if do_gather else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -202,26 +207,30 @@ def main() -> int:
             ev_a[k].record()
             one_step(args.warmup + k)
             ev_b[k].record()
-            if do_gather:
-                gather()
-                ev_c[k].record()
+            if gatherer is not None:
+                p = (gatherer.k - 1) % gatherer.depth
+                gather_ms.append((gatherer._t0[p], gatherer._done[p]))
+        if gatherer is not None:  # the last gather belongs to the timed steps too
+            gatherer.result((gatherer.k - 1) % gatherer.depth)
     torch.cuda.synchronize()
+    if gatherer is not None:
+        gather_ms = [a.elapsed_time(b) for a, b in gather_ms]
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    if roll is not None:  # untimed: per-step kernel durations for the roofline
+    if roll is not None and gym is None:  # untimed: per-step kernel durations for the roofline
         for k in range(args.steps):
             ev_a[k].record()
             one_step(args.warmup + k)
             ev_b[k].record()
         torch.cuda.synchronize()
-    per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
-    eager_ms = sum(per) / len(per)
+    per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)] if roll is None or gym is None else []
+    eager_ms = sum(per) / len(per) if per else float("nan")
     # the dominant kernel's time per launch: from the graph replay (back-to-back launches, no
     # host gaps) when there is one -- an eager step's event pair also holds the host's launch
     # time whenever the kernel is shorter than it (small batches)
     kern_ms = g0.elapsed_time(g1) / args.steps if roll is not None else eager_ms
-    gather_ms = (sum(ev_b[k].elapsed_time(ev_c[k]) for k in range(args.steps)) / args.steps) if do_gather else None
+    gather_ms = (sum(gather_ms) / len(gather_ms)) if do_gather else None
     elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64,
                            device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
@@ -295,7 +304,8 @@ def main() -> int:
 
     par = f"env-shard x{world}" + (" (strong: global batch split)" if strong else " (weak: batch per GPU)")
     line = {
-        "metric": f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU"),
+        "metric": HEADLINE_METRIC if (args.env == "ant_heavenhell" and strong and total == 65536 and gym is None)
+                  else f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU"),
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -353,8 +363,10 @@ def committed_profile(env: str, B: int, qp: str):
 
 def cpu_baseline(name: str, B: int, seconds: float) -> dict:
     """The C restatement (kind "port": same algorithm, oracle/pob_oracle.c) compiled
-    -O3 -march=native on this host, timed on the same workload (this GPU's batch B):
-    one thread and all host threads (OpenMP over envs).  Time-boxed samples."""
+    -O3 -march=native on this host, timed on the same workload (this GPU's batch B), on
+    every core this process may run on (``sched_getaffinity``, SURVEY.md §8(d) "all cores";
+    the reported ``value``), on the launcher's per-process share (``OMP_NUM_THREADS``, 16 on
+    the GPU box) and on one thread (OpenMP over envs, static schedule).  Time-boxed samples."""
     import numpy as np
     import orc
     import pob_np as P
@@ -362,14 +374,13 @@ def cpu_baseline(name: str, B: int, seconds: float) -> dict:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         aff = os.cpu_count() or 1
-    # the process's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box
-    # sets 16), else every core this process may run on
-    cores = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff)))
+    share = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff)))
     e = orc.OracleEnv(name, native=True)
-    s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=cores)
+    s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=aff)
     acts = np.random.default_rng(0).uniform(-1, 1, (2, B, 8)).astype(np.float32)
+    legs = [("all", aff)] + ([("share", share)] if share not in (aff, 1) else []) + [("single", 1)]
     out = {}
-    for leg, nt in (("all", cores), ("single", 1)):
+    for leg, nt in legs:
         e.step(s, acts[0], flags=3, nthreads=nt, inplace=True)  # warm caches / the thread pool
         n, t0 = 0, time.perf_counter()
         while True:
@@ -378,15 +389,18 @@ def cpu_baseline(name: str, B: int, seconds: float) -> dict:
             if time.perf_counter() - t0 >= seconds:
                 break
         dt = time.perf_counter() - t0
-        out[leg] = (B * n / dt, n, dt)
-    v, n, dt = out["all"]
-    v1, n1, dt1 = out["single"]
-    return {"value": round(v, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "single_thread_value": round(v1, 1),
-            "sample": f"{name} B={B} (the GPU workload's batch): {n} steps in {dt:.1f} s on {cores} threads, "
-                      f"{n1} steps in {dt1:.1f} s on 1 thread; the same fused step (oracle/pob_oracle.c) "
-                      "gcc -O3 -march=native, OpenMP over envs",
-            "cpu": orc.cpu_model(), "nproc": os.cpu_count(), "affinity_cores": aff}
+        out[leg] = (B * n / dt, n, dt, nt)
+    v, n, dt, _ = out["all"]
+    res = {"value": round(v, 1), "unit": "env-steps/s", "cores": aff, "kind": "port",
+           "single_thread_value": round(out["single"][0], 1)}
+    if "share" in out:
+        res["share_threads"] = share
+        res["share_threads_value"] = round(out["share"][0], 1)
+    res["sample"] = (f"{name} B={B} (the GPU workload's batch), the same fused step (oracle/pob_oracle.c, "
+                     "gcc -O3 -march=native, OpenMP over envs): "
+                     + "; ".join(f"{o[1]} steps in {o[2]:.1f} s on {o[3]} thread(s)" for o in out.values()))
+    res.update(cpu=orc.cpu_model(), nproc=os.cpu_count(), affinity_cores=aff)
+    return res
 
 
 if __name__ == "__main__":

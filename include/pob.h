@@ -130,6 +130,9 @@ int pob_abi_version(void);
 const char *pob_last_error(void);
 int pob_default_params(pob_params *p);
 int pob_env_create(int kind, const pob_params *p, pob_env **out);
+/* Never calls the HIP runtime (safe while a stream is being captured into a hipGraph): the
+ * env's device tables are released by the next pob_env_create.  The caller must not destroy
+ * an env whose launches are still queued or captured in a graph it will replay. */
 void pob_env_destroy(pob_env *env);
 int pob_env_dims(const pob_env *env, int *n_bodies, int *obs_dim, int *act_dim);
 /* host copy of default_angle() (8 floats, radians): System.default_angle [ext] */
@@ -146,7 +149,10 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
                    int episode_length, void *stream);
 int pob_reset_where_done(pob_env *env, int B, int mode, const uint32_t *gym_key_in,
                          uint32_t *gym_key_out, const pob_state *s, void *stream);
-/* The same for a shard: this env batch holds rows [first, first + B) of a global batch of
+/* gym_key_in / gym_key_out must be distinct words, and s->any_done_clear (if set) must not
+ * be s->any_done (POB_EINVAL otherwise): the kernel's first block writes the outputs while
+ * every block reads the inputs.
+ * The same for a shard: this env batch holds rows [first, first + B) of a global batch of
  * `total` envs split over ranks (AutoresetVmapGymWrapper under index sharding).  Gym mode
  * keys are split(gym_key, total + 1)[1 + first + b]; s->any_done must then hold the GLOBAL
  * any-done flag (the caller all-reduces it, MAX, across ranks before this call). */

@@ -108,9 +108,10 @@ def choice_noreplace(key, a, k):
 
 
 def prngkey(seed):
-    """jax.random.PRNGKey(seed), x64 off: int32 seed, high word = logical shift by 32 = 0."""
+    """jax.random.PRNGKey(seed), x64 off: the seed goes through np.int64, then int32 (low 32
+    bits); high word = logical shift by 32 = 0.  Outside int64: OverflowError."""
     seed = int(seed)
-    if not -(1 << 31) <= seed < (1 << 31):
+    if not -(1 << 63) <= seed < (1 << 63):
         raise OverflowError(seed)
     return np.array([0, seed & 0xFFFFFFFF], U32)
 

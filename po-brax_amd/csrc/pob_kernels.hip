@@ -19,7 +19,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/pob.h"
 #include "pob_quad.h"
@@ -2333,9 +2335,27 @@ int pob_default_params(pob_params *p) {
   return POB_OK;
 }
 
+// Device tables of destroyed envs.  pob_env_destroy never calls the HIP runtime: a handle
+// may be dropped while some stream is being captured into a hipGraph (a Python finaliser run
+// by the garbage collector in the middle of a capture), and hipFree there invalidates the
+// capture (hipErrorStreamCaptureInvalidated).  The tables (~4 KB per env) are freed by the
+// next pob_env_create, which cannot itself run inside a capture (it allocates).
+static std::mutex g_grave_mu;
+static std::vector<void *> g_grave;
+
+static void drain_grave() {
+  std::vector<void *> dead;
+  {
+    std::lock_guard<std::mutex> lk(g_grave_mu);
+    dead.swap(g_grave);
+  }
+  for (void *p : dead) (void)hipFree(p);
+}
+
 int pob_env_create(int kind, const pob_params *p, pob_env **out) {
   if (!out) return fail(POB_EINVAL, "out is NULL");
   *out = nullptr;
+  drain_grave();
   pob_params prm;
   if (p) prm = *p; else pob::default_params(prm);
   pob_env *e = new (std::nothrow) pob_env();
@@ -2365,9 +2385,11 @@ int pob_env_create(int kind, const pob_params *p, pob_env **out) {
 
 void pob_env_destroy(pob_env *e) {
   if (!e) return;
-  if (e->d_grid) (void)hipFree(e->d_grid);
-  if (e->d_scratch) (void)hipFree(e->d_scratch);
-  if (e->d_sys) (void)hipFree(e->d_sys);
+  {
+    std::lock_guard<std::mutex> lk(g_grave_mu);
+    for (void *p : {(void *)e->d_grid, (void *)e->d_scratch, (void *)e->d_sys})
+      if (p) g_grave.push_back(p);
+  }
   delete e;
 }
 
@@ -2505,6 +2527,11 @@ int pob_reset_where_done_shard(pob_env *e, int B, int total, int first, int mode
   if (int rc = check_state(s, true)) return rc;
   if (mode != POB_RESET_GYM && mode != POB_RESET_OWN) return fail(POB_EINVAL, "unknown reset mode");
   if (mode == POB_RESET_GYM && (!gym_in || !gym_out)) return fail(POB_EINVAL, "gym mode needs gym_key_in/out");
+  // block 0 writes gym_out and clears *any_done_clear while every block reads gym_in / *any_done
+  if (mode == POB_RESET_GYM && gym_out < gym_in + 2 && gym_in < gym_out + 2)
+    return fail(POB_EINVAL, "gym_key_in and gym_key_out must not overlap");
+  if (s->any_done_clear && s->any_done_clear == s->any_done)
+    return fail(POB_EINVAL, "any_done_clear must not alias any_done");
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs p = to_ptrs(*s);
   const uint32_t *flag = s->any_done;

@@ -140,6 +140,31 @@ class _BodyIndex:
         self.index = {n: i for i, n in enumerate(names)}
 
 
+class _Handle:
+    """Owns one libpob env handle plus the facts System needs about it (device, dims).
+
+    Both the env and its System point here, never at each other, so an env is freed by
+    reference counting as soon as it is dropped -- not by a cyclic-GC pass that may fire in
+    the middle of a hipGraph capture.  ``pob_env_destroy`` itself never calls the HIP runtime
+    (the C side defers the device frees to the next ``pob_env_create``), so finalisation is
+    safe at any time, a capture included."""
+
+    def __init__(self, kind: int, params, device: torch.device):
+        h = C.c_void_p()
+        with torch.cuda.device(device):
+            check(lib.pob_env_create(kind, C.byref(params), C.byref(h)))
+        self.ptr, self.device = h, device
+        n, d, a = C.c_int(), C.c_int(), C.c_int()
+        check(lib.pob_env_dims(h, C.byref(n), C.byref(d), C.byref(a)))
+        self.N, self.D, self.A = n.value, d.value, a.value
+
+    def __del__(self):
+        h = getattr(self, "ptr", None)
+        if h is not None and lib is not None:
+            lib.pob_env_destroy(h)
+            self.ptr = None
+
+
 class System:
     """The parts of brax.System the reference envs and wrappers touch.
 
@@ -149,9 +174,9 @@ class System:
     ``default_qp(joint_angle, joint_velocity)`` (the latter runs the FK kernel).
     """
 
-    def __init__(self, env: "PoBraxEnv", body_names):
-        self._env = env
-        self.config = _Config(dt=0.05 * env._action_repeat, substeps=10 * env._action_repeat)
+    def __init__(self, owner: _Handle, body_names, action_repeat: int = 1):
+        self._owner = owner  # the engine handle, not the env (no env <-> System cycle)
+        self.config = _Config(dt=0.05 * action_repeat, substeps=10 * action_repeat)
         self.body = _BodyIndex(body_names)
         self.num_bodies = len(body_names)
         self.num_joint_dof = 8
@@ -159,20 +184,20 @@ class System:
 
     def default_angle(self) -> torch.Tensor:
         out = (C.c_float * 8)()
-        check(lib.pob_env_default_angle(self._env._handle, out))
-        return torch.tensor(list(out), dtype=torch.float32, device=self._env.device)
+        check(lib.pob_env_default_angle(self._owner.ptr, out))
+        return torch.tensor(list(out), dtype=torch.float32, device=self._owner.device)
 
     def default_qp(self, joint_angle=None, joint_velocity=None) -> QP:
-        e = self._env
+        e = self._owner
         qpos = self.default_angle() if joint_angle is None else torch.as_tensor(joint_angle)
         qpos = qpos.to(e.device, torch.float32)
         qvel = torch.zeros_like(qpos) if joint_velocity is None else torch.as_tensor(joint_velocity)
         qvel = qvel.to(e.device, torch.float32)
         squeeze = qpos.ndim == 1
         qpos, qvel = qpos.reshape(-1, 8).contiguous(), qvel.reshape(-1, 8).contiguous()
-        B, N = qpos.shape[0], e._N
+        B, N = qpos.shape[0], e.N
         out = [torch.empty((B, N, k), dtype=torch.float32, device=e.device) for k in (3, 4, 3, 3)]
-        check(lib.pob_default_qp(e._handle, B, qpos.data_ptr(), qvel.data_ptr(),
+        check(lib.pob_default_qp(e.ptr, B, qpos.data_ptr(), qvel.data_ptr(),
                                  *[o.data_ptr() for o in out], _lib.stream_handle(e.device)))
         if squeeze:
             out = [o[0] for o in out]
@@ -206,9 +231,9 @@ class PoBraxEnv(Env):
         self._params.qp_storage = _lib.QP_F16 if qp_dtype == torch.float16 else _lib.QP_F32
         self._set_params(params)
         self._action_repeat = 1
-        self._handle = None
+        self._owner = None
         self._create()
-        self.sys = System(self, self._body_names())
+        self.sys = System(self._owner, self._body_names())
 
     # subclasses map constructor kwargs onto pob_params
     def _set_params(self, params: dict) -> None:
@@ -218,32 +243,21 @@ class PoBraxEnv(Env):
         return list(self.body_names)
 
     def _create(self):
-        if self._handle is not None:
-            lib.pob_env_destroy(self._handle)
-            self._handle = None
         self._params.action_repeat = self._action_repeat
-        h = C.c_void_p()
-        with torch.cuda.device(self.device):
-            check(lib.pob_env_create(_lib.KINDS[self.kind], C.byref(self._params), C.byref(h)))
-        self._handle = h
-        n, d, a = C.c_int(), C.c_int(), C.c_int()
-        check(lib.pob_env_dims(self._handle, C.byref(n), C.byref(d), C.byref(a)))
-        self._N, self._D, self._A = n.value, d.value, a.value
+        self._owner = _Handle(_lib.KINDS[self.kind], self._params, self.device)
+        self._N, self._D, self._A = self._owner.N, self._owner.D, self._owner.A
+
+    @property
+    def _handle(self) -> C.c_void_p:
+        return self._owner.ptr
 
     def _set_action_repeat(self, action_repeat: int) -> None:
         """ActionRepeatWrapper (wrappers.py:16-24): dt and substeps scale by action_repeat."""
         self._action_repeat *= int(action_repeat)
         self._create()
+        self.sys._owner = self._owner
         self.sys.config.dt = 0.05 * self._action_repeat
         self.sys.config.substeps = 10 * self._action_repeat
-
-    def __del__(self):
-        h = getattr(self, "_handle", None)
-        if h is not None:
-            try:
-                lib.pob_env_destroy(h)
-            except Exception:
-                pass
 
     # ------------------------------------------------------------------ buffers
     def _empty(self, B: int, episode: bool, first: bool) -> dict:
@@ -396,13 +410,29 @@ class PoBraxEnv(Env):
                             _lib.stream_handle(self.device)))
         return self._state_of(b, False, squeeze)
 
-    def _fast_key(self, state: State, flags: int, episode_length: int) -> tuple:
-        """Identity of everything the in-place fast path's cached pob_state depends on: a
-        replaced field (``state.replace(done=...)``), a new metrics / info dict or another
-        any-done word gives another key, hence the full path."""
-        a = state.aux
-        return (id(state.qp), id(state.obs), id(state.reward), id(state.done), id(state.metrics),
-                id(state.info), id(a.get("any_done")), id(a.get("any_done_clear")), flags, episode_length)
+    @staticmethod
+    def _fast_refs(state: State, flags: int, episode_length: int) -> tuple:
+        """Every object the in-place fast path's cached pob_state was built from: the qp
+        tensors, obs, reward, done, each metric, each info entry (first_qp's tensors
+        included) and the any-done words.  The cache holds these objects (strong references,
+        so no id can be reused while it lives) and the fast path is taken only when each
+        current field IS the cached object -- so a replaced field (``state.replace(done=...)``)
+        or an info / metrics entry edited in place (``info['first_qp'] = qp``,
+        ``info.update(steps=...)``, wrappers.py:105-111) takes the full path."""
+        qp, a = state.qp, state.aux
+        refs = [qp.pos, qp.rot, qp.vel, qp.ang, state.obs, state.reward, state.done,
+                a.get("any_done"), a.get("any_done_clear"), flags, episode_length, len(state.metrics)]
+        refs.extend(state.metrics.values())
+        for v in state.info.values():
+            if isinstance(v, QP):
+                refs.extend((v.pos, v.rot, v.vel, v.ang))
+            else:
+                refs.append(v)
+        return tuple(refs)
+
+    @staticmethod
+    def _same_refs(a: tuple, b: tuple) -> bool:
+        return len(a) == len(b) and all(x is y or (type(x) is int and x == y) for x, y in zip(a, b))
 
     def _step_impl(self, state: State, action, flags: int, episode_length: int, inplace: bool) -> State:
         if inplace and _CAPTURE is None:
@@ -411,12 +441,13 @@ class PoBraxEnv(Env):
             # the same objects) and is returned as is -- ~3x less host time per step than
             # rebuilding the buffer map, the ctypes struct and the State (eager loops)
             fast = state.aux.get("_fast")
-            if fast is not None and fast[0] == self._fast_key(state, flags, episode_length) and \
+            if fast is not None and self._same_refs(fast[0], self._fast_refs(state, flags, episode_length)) and \
                     isinstance(action, torch.Tensor) and action.dtype == torch.float32 and action.is_cuda and \
                     (self.device.index is None or action.device.index == self.device.index) and \
                     action.is_contiguous() and \
                     action.numel() == fast[2] * self._A:
-                check(lib.pob_step(self._handle, fast[2], fast[1], action.data_ptr(), fast[1], flags,
+                cs = C.byref(fast[1])
+                check(lib.pob_step(self._handle, fast[2], cs, action.data_ptr(), cs, flags,
                                    int(episode_length), _lib.stream_handle(self.device)))
                 return state
         squeeze = state.obs.ndim == 1
@@ -458,7 +489,7 @@ class PoBraxEnv(Env):
         out = self._state_of(bout, True, squeeze)
         if inplace and not squeeze:
             # in place, the input and output buffers are the same: one struct serves both
-            out.aux["_fast"] = (self._fast_key(out, flags, episode_length), C.byref(co), B)
+            out.aux["_fast"] = (self._fast_refs(out, flags, episode_length), co, B)
         return out
 
     # helpers for the gym / randomized-autoreset wrappers

@@ -131,7 +131,19 @@ class RandomizedAutoResetWrapperCached(Wrapper):
 
 
 class EvalWrapper(Wrapper):
-    """brax EvalWrapper: per-env running episode metrics and completed-episode totals."""
+    """brax EvalWrapper [ext] (``create(..., eval_metrics=True)``, __init__.py:69-70): per-env
+    running episode metrics and completed-episode totals, restated from brax <= 0.0.12:
+
+        nstate.metrics['reward'] = nstate.reward
+        completed_episodes_steps += sum(nstate.info['steps'] * nstate.done)
+        current = tree_multimap(+, current, nstate.metrics)
+        completed_episodes += sum(nstate.done)
+        completed_metrics = tree_multimap(a + sum(b * done), completed_metrics, current)
+        current = current * (1 - nstate.done)
+
+    The step's metric keys must equal the reset's, as jax's ``tree_multimap`` requires:
+    AntHeavenHell adds ``hits`` on step (ant_heavenhell.py:122), so there the reference raises
+    and so does this wrapper (ValueError).  Device tensors, no host sync; sums are float32."""
 
     def _chain_reset(self, rng, episode, first):
         s = self.env._chain_reset(rng, episode, first)
@@ -151,8 +163,11 @@ class EvalWrapper(Wrapper):
         state.info["eval_metrics"] = em
         ns.metrics["reward"] = ns.reward
         done = ns.aux["done"] if "done" in ns.aux else ns.done.to(torch.float32)
+        if set(ns.metrics) != set(em["current_episode_metrics"]):
+            raise ValueError(f"EvalWrapper: step metrics {sorted(ns.metrics)} do not match the reset's "
+                             f"{sorted(em['current_episode_metrics'])} (jax tree_multimap structure mismatch)")
         cur = {k: em["current_episode_metrics"][k] + ns.metrics[k].to(torch.float32)
-               for k in em["current_episode_metrics"] if k in ns.metrics}
+               for k in em["current_episode_metrics"]}
         comp = {k: em["completed_episodes_metrics"][k] + (cur[k] * done).sum() for k in cur}
         steps = ns.info.get("steps")
         nem = {
@@ -344,7 +359,8 @@ class EvalGymWrapper:
     values are scattered in env order (the order of ``d.nonzero()``) to
     ``count + cumsum(d) - 1``, the other envs to a discard slot past the end.  The host reads
     the device count only when the buffer might overflow (at most ``num_envs`` entries per
-    step), i.e. once per ``capacity / num_envs`` steps.  Returns are float32 like the
+    step): the capacity starts at 64 steps' worth and grows whenever fewer than 16 steps of
+    room remain after a read, so reads stay at most one per 16 steps.  Returns are float32 like the
     reference's ``zeros_like(obs[..., -1])`` buffers; lengths are int32."""
 
     def __init__(self, env, discount: float = 1.0, capacity: int = 1 << 16):
@@ -367,7 +383,7 @@ class EvalGymWrapper:
         self.discounted_episode_returns = torch.zeros_like(like, dtype=torch.float32)
         self.episode_lengths = torch.zeros_like(like, dtype=torch.int32)
         self.current_discount = torch.ones_like(like, dtype=torch.float32)
-        cap = max(self._cap0, 4 * n)
+        cap = max(self._cap0, 64 * n)  # room for 64 steps in which every env finishes
         self._q = torch.zeros((3, cap + 1), dtype=torch.float32, device=dev)  # + discard slot
         self._lq = torch.zeros(cap + 1, dtype=torch.int32, device=dev)
         self._count = torch.zeros((), dtype=torch.int64, device=dev)
@@ -379,8 +395,8 @@ class EvalGymWrapper:
         if self._known + (self._since + 1) * n <= cap:
             return
         self._known, self._since = int(self._count), 0  # host sync (rare)
-        if self._known + n > cap:
-            new = max(2 * cap, self._known + n)
+        if self._known + 16 * n > cap:  # grow early: >= 16 steps of room after every sync
+            new = max(2 * cap, self._known + 64 * n)
             q = torch.zeros((3, new + 1), dtype=self._q.dtype, device=self._q.device)
             lq = torch.zeros(new + 1, dtype=self._lq.dtype, device=self._lq.device)
             q[:, :self._known] = self._q[:, :self._known]

@@ -14,13 +14,16 @@ from ._lib import lib, check
 
 
 def random_prngkey(seed: int, device=None) -> torch.Tensor:
-    """jax.random.PRNGKey(seed) with jax's default 32-bit mode (x64 off): the seed is
-    converted to int32 (values outside the int32 range are rejected, as jax raises
-    OverflowError) and the key is [0, seed & 0xFFFFFFFF] -- the high word is a LOGICAL
-    shift of the 32-bit seed, so PRNGKey(-1) = [0, 4294967295]."""
+    """jax.random.PRNGKey(seed) with jax's default 32-bit mode (x64 off).  jax converts a
+    Python int seed through ``np.int64`` first ("avoid overflow error in X32 mode ... supports
+    the common use-case of instantiating with Python hashes") and then to int32, which keeps
+    the low 32 bits; the key is [seed >> 32 of the 32-bit value (a LOGICAL shift, = 0),
+    seed & 0xFFFFFFFF], so PRNGKey(-1) = [0, 4294967295] and PRNGKey(2**40 + 5) = [0, 5].
+    Seeds outside int64 raise OverflowError (as np.int64 does).  [ext] jax's random.PRNGKey;
+    no reference fixture pins seeds outside int32 -- parity unpinned there."""
     seed = int(seed)
-    if not -(1 << 31) <= seed < (1 << 31):
-        raise OverflowError(f"seed {seed} does not fit in int32 (jax PRNGKey with x64 disabled)")
+    if not -(1 << 63) <= seed < (1 << 63):
+        raise OverflowError(f"seed {seed} does not fit in int64 (jax PRNGKey converts through np.int64)")
     k = torch.tensor([0, seed & 0xFFFFFFFF], dtype=torch.uint32)
     return k.to(device if device is not None else "cuda")
 

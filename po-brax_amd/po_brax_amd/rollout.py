@@ -19,9 +19,27 @@ wrappers keep their eager path.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Sequence
 
 import torch
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Keep the cyclic garbage collector off for the span of a hipGraph capture: a collection
+    there runs arbitrary finalisers, and any HIP runtime call one makes that is illegal during
+    a global-mode capture (hipFree, a synchronisation) invalidates the capture.  (The engine's
+    own handles are already safe -- no env <-> System cycle, and pob_env_destroy defers its
+    frees -- this guards the caller's objects too.)"""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _slice_state(state, lo: int, hi: int, B: int):
@@ -79,7 +97,7 @@ class GraphRollout:
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
         if groups == 1:
-            with torch.cuda.graph(self.graph):
+            with no_gc(), torch.cuda.graph(self.graph):
                 for t in range(self.steps):
                     # follow the returned State: its public typed outputs (TAG done, GA
                     # counts) are the buffers the captured kernels write
@@ -92,7 +110,7 @@ class GraphRollout:
         u._typed_outputs(self.state.aux, B, "steps" in self.state.info)
         parts = [_slice_state(self.state, lo, hi, B) for lo, hi in bounds]
         streams = [None] + [torch.cuda.Stream(dev) for _ in range(groups - 1)]
-        with torch.cuda.graph(self.graph):
+        with no_gc(), torch.cuda.graph(self.graph):
             cap = torch.cuda.current_stream(dev)
             for st in streams[1:]:
                 st.wait_stream(cap)  # fork from the capture stream
@@ -117,3 +135,40 @@ def graph_rollout(env, state, actions: Sequence[torch.Tensor] | torch.Tensor) ->
     if not isinstance(actions, torch.Tensor):
         actions = torch.stack(list(actions))
     return GraphRollout(env, state, actions)
+
+
+class GymGraphRollout:
+    """``T`` steps of a gym vector env (``create_gym_env``: ``AutoresetVmapGymWrapper``,
+    wrappers.py:240-262) captured into one hipGraph: per step the fused step kernel (which
+    also ORs the device any-done word) and the masked gym reset kernel (which reads that word,
+    re-samples the done envs from ``split(gym_key, B + 1)`` and advances the key only if
+    something was done).  The decision ``if done.any()`` lives on the device, so the whole
+    loop is capture-safe; nothing is skipped -- the same kernels run on the same buffers as
+    ``gym.step`` called T times.
+
+    The wrapper's host-side bookkeeping (the alternating any-done words and gym-key buffers)
+    is advanced by the capture itself, so ``T`` must be even: after T steps it is back where
+    it started, and every replay continues from the device state the last one left.
+    ``actions`` (T, B, A) is read at replay time (refill it between replays).  One process
+    only: the sharded wrapper's per-step RCCL all-reduce stays eager."""
+
+    def __init__(self, gym, actions: torch.Tensor):
+        if actions.dim() != 3 or actions.shape[0] % 2:
+            raise ValueError("actions must be (T, B, A) with T even")
+        sh = getattr(gym, "_shard", None)
+        if sh is not None and sh.world > 1:
+            raise NotImplementedError("a sharded gym step (RCCL any-done all-reduce) runs eagerly")
+        self.gym, self.actions = gym, actions
+        self.steps = int(actions.shape[0])
+        dev = actions.device
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with no_gc(), torch.cuda.graph(self.graph):
+            for t in range(self.steps):
+                gym.step(self.actions[t])
+
+    def replay(self):
+        """Run the captured gym steps; returns (obs, reward, done, metrics) of the last."""
+        self.graph.replay()
+        s = self.gym._state
+        return s.obs, s.reward, s.done, s.metrics

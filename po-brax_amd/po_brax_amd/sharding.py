@@ -125,3 +125,92 @@ def gather_obs_ragged(obs, total: int, group=None):
     full = gather_obs(pad, group)
     return torch.cat([full[r * m: r * m + (hi - lo)]
                       for r, (lo, hi) in enumerate(shard_range(total, world, r) for r in range(world))])
+
+
+class ObsGatherer:
+    """Double-buffered all-gather of each step's observation batch, overlapped with the
+    following steps ("overlap it with the next step via a separate stream").
+
+    ``submit(obs)`` is called on the compute stream right after step t's kernel: it copies
+    this rank's obs rows into staging slot ``p = t % depth`` (one D2D copy on the compute
+    stream, so step t + 1 may overwrite ``obs`` at once) and enqueues the all-gather of that
+    slot into ``full[p]`` on a side stream, ordered after the copy by an event.  Step t + 1's
+    kernel therefore runs concurrently with step t's gather; slot ``p`` is reused by step
+    t + depth, whose copy waits (on the device, not the host) for gather t to finish.
+    ``result(p)`` makes the caller's current stream wait for gather ``p`` and returns the
+    (B_total, D) batch in global env order; it stays valid until ``depth`` more submits.
+
+    Unequal shards (``shard_range`` of ``total``) are padded to the largest shard and the
+    padding is dropped by ``result``.  On CPU tensors (gloo) the same rotation runs
+    synchronously, which is what the world-2 tests exercise."""
+
+    def __init__(self, total: int, D: int, dtype=None, device=None, group=None, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+        self.total, self.D, self.group = int(total), int(D), group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.bounds = [shard_range(self.total, self.world, r) for r in range(self.world)]
+        self.m = max(hi - lo for lo, hi in self.bounds)
+        self.ragged = any(hi - lo != self.m for lo, hi in self.bounds)
+        self.depth = max(1, int(depth))
+        dtype = dtype or torch.float32
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.cuda = self.device.type == "cuda"
+        self.stage = [torch.zeros((self.m, self.D), dtype=dtype, device=self.device) for _ in range(self.depth)]
+        self.full = [torch.empty((self.world * self.m, self.D), dtype=dtype, device=self.device)
+                     for _ in range(self.depth)]
+        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self._done = [None] * self.depth    # event: gather of slot p finished (side stream)
+        self._t0 = [None] * self.depth      # event: gather of slot p enqueued (timing)
+        self.k = 0
+
+    def submit(self, obs) -> int:
+        """Stage ``obs`` (this rank's (B_local, D) rows) and start its all-gather; returns
+        the slot to pass to ``result``."""
+        import torch
+        import torch.distributed as dist
+        lo, hi = self.bounds[self.rank]
+        if tuple(obs.shape) != (hi - lo, self.D):
+            raise ValueError(f"obs shard {tuple(obs.shape)} != ({hi - lo}, {self.D})")
+        p = self.k % self.depth
+        self.k += 1
+        if not self.cuda:
+            self.stage[p][:hi - lo].copy_(obs)
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.full[p], self.stage[p], group=self.group)
+            else:
+                self.full[p].copy_(self.stage[p])
+            return p
+        cur = torch.cuda.current_stream(self.device)
+        if self._done[p] is not None:
+            cur.wait_event(self._done[p])  # gather t - depth has read the slot
+        self.stage[p][:hi - lo].copy_(obs)
+        staged = torch.cuda.Event()
+        staged.record(cur)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(staged)
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record(self.stream)
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.full[p], self.stage[p], group=self.group)
+            else:
+                self.full[p].copy_(self.stage[p])
+            done = torch.cuda.Event(enable_timing=True)
+            done.record(self.stream)
+        self._t0[p], self._done[p] = t0, done
+        return p
+
+    def result(self, p: int):
+        """The gathered (B_total, D) observation batch of slot ``p`` (global env order)."""
+        import torch
+        if self.cuda and self._done[p] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._done[p])
+        f = self.full[p]
+        if not self.ragged:
+            return f
+        return torch.cat([f[r * self.m: r * self.m + (hi - lo)] for r, (lo, hi) in enumerate(self.bounds)])
+
+    def gather_ms(self, p: int) -> float:
+        """Device time of slot p's last gather (side stream, from its start to its end)."""
+        return self._t0[p].elapsed_time(self._done[p]) if self.cuda and self._done[p] is not None else 0.0

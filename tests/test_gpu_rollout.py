@@ -81,3 +81,74 @@ def test_grouped_graph_rollout_equals_eager(name):
     assert torch.equal(s1.info["truncation"], s2.info["truncation"])
     for k in s1.metrics:
         assert s1.metrics[k].dtype == s2.metrics[k].dtype and torch.equal(s1.metrics[k], s2.metrics[k]), k
+
+
+def test_capture_survives_gc_of_dead_envs():
+    """Regression for the driver's round-2 GPU suite failure (hipErrorStreamCaptureInvalidated
+    in a GraphRollout capture): a cyclic-GC pass inside a global-mode capture finalises dead
+    envs, and pob_env_destroy used to hipFree their tables there.  Now (1) an env has no
+    env <-> System cycle, so dropping it frees it at once, and (2) pob_env_destroy never calls
+    the HIP runtime (the frees are deferred to the next pob_env_create).  Both are checked:
+    an env kept alive only by an explicit cycle is collected INSIDE a capture, and the captured
+    steps replay equal to eager ones."""
+    import gc
+    import weakref
+    from po_brax_amd import envs
+    e = envs.create("ant_heavenhell", batch_size=8)
+    ref = weakref.ref(e.unwrapped)
+    del e
+    assert ref() is None  # freed by reference counting: no cycle left behind
+    dead = envs.create("ant_gather", batch_size=8).unwrapped
+    dead._cycle = dead  # only the cyclic GC can free it
+    dref = weakref.ref(dead)
+    del dead
+    B = 256
+    keys = torch.from_numpy(_keys(B, 9)).cuda()
+    e1, e2 = (envs.create("ant_tag", batch_size=B, episode_length=5) for _ in range(2))
+    s1, s2 = e1.reset(keys), e2.reset(keys)
+    acts = _acts(3, B, 11)
+    s1 = e1.step_(s1, acts[0])
+    s2 = e2.step_(s2, acts[0])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s2 = e2.step_(s2, acts[1])
+        gc.collect()  # finalises the dead env (pob_env_destroy) in the middle of the capture
+        s2 = e2.step_(s2, acts[2])
+    assert dref() is None
+    g.replay()
+    for t in (1, 2):
+        s1 = e1.step_(s1, acts[t])
+    torch.cuda.synchronize()
+    for f in ("pos", "rot", "vel", "ang"):
+        assert torch.equal(getattr(s1.qp, f), getattr(s2.qp, f)), f
+    assert torch.equal(s1.obs, s2.obs) and torch.equal(s1.done, s2.done)
+    # the deferred tables are released by the next create (outside any capture)
+    envs.create("ant_tag", batch_size=8)
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag"])
+def test_gym_graph_rollout_equals_eager(name):
+    """create_gym_env steps replayed from a hipGraph (rollout.GymGraphRollout: step kernel +
+    device any-done + masked gym reset, wrappers.py:245-262) equal gym.step called eagerly,
+    bit for bit, over episodes short enough that several gym resets (and key advances) happen
+    inside the captured steps; a second replay continues from the first."""
+    from po_brax_amd import envs
+    from po_brax_amd.rollout import GymGraphRollout
+    B, T = 300, 6
+    g1, g2 = (envs.create_gym_env(name, batch_size=B, seed=5, episode_length=3) for _ in range(2))
+    o1, o2 = g1.reset(), g2.reset()
+    assert torch.equal(o1, o2)
+    acts = _acts(T, B, 13)
+    roll = GymGraphRollout(g2, acts)
+    for rep in range(2):
+        for t in range(T):
+            o1, r1, d1, m1 = g1.step(acts[t])
+        o2, r2, d2, m2 = roll.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2), rep
+        for f in ("pos", "rot", "vel", "ang"):
+            assert torch.equal(getattr(g1._state.qp, f), getattr(g2._state.qp, f)), (rep, f)
+        assert torch.equal(g1._key, g2._key), rep
+        for k in m1:
+            assert torch.equal(m1[k], m2[k]), (rep, k)

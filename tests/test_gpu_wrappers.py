@@ -154,11 +154,13 @@ def test_eval_gym_wrapper_queue_growth():
     envs = _envs()
     B = 32
     g = envs.create_gym_env("ant_heavenhell", batch_size=B, seed=2, episode_length=1, eval_metrics=True)
-    g._cap0 = 40  # tiny buffer (grown to 4 B = 128 at reset): every step finishes all B episodes
+    g._cap0 = 40  # tiny buffer (grown to 64 B = 2 048 at reset): every step finishes all B episodes
     g.reset()
-    for _ in range(10):
+    assert g._lq.shape[0] - 1 == 64 * B
+    for _ in range(80):
         g.step(torch.zeros((B, 8), device="cuda"))
-    assert len(g.l_q) == 1 + 10 * B and all(x == 1 for x in g.l_q[1:])
+    assert g._lq.shape[0] - 1 > 64 * B  # grew
+    assert len(g.l_q) == 1 + 80 * B and all(x == 1 for x in g.l_q[1:])
 
 
 @pytest.mark.parametrize("name", ["ant_tag", "ant_heavenhell"])
@@ -247,3 +249,94 @@ def test_inplace_fast_path(name):
     so = orc.OracleEnv(name).step(ref, act[8], flags=FLAGS, episode_length=L)
     s4 = e2.step_(s3, torch.from_numpy(act[8]).cuda())
     compare_states(s4, so, f"{name}: in-place after replace(done=1)")
+
+
+@pytest.mark.parametrize("name", ["ant_tag", "ant_gather"])
+def test_inplace_fast_path_sees_info_entry_edits(name):
+    """The reference's wrappers edit info entries in place (``state.info['first_qp'] = s.qp``,
+    ``info.update(steps=...)``, wrappers.py:105-111): the dict keeps its identity, so the
+    in-place fast path must compare the entries themselves.  Reassigning info['steps'] (to
+    steps one short of the time limit) and info['first_obs'] (to a new tensor) between step_
+    calls reaches the kernel: the step reads and writes the NEW tensors, equal to the oracle
+    step from the edited state."""
+    envs = _envs()
+    B, L = 64, 50
+    env = envs.create(name, batch_size=B, episode_length=L)
+    keys = _keys(B, 5)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    act = np.random.default_rng(6).uniform(-1, 1, (4, B, 8)).astype(np.float32)
+    for t in range(3):
+        s = env.step_(s, torch.from_numpy(act[t]).cuda())
+    assert "_fast" in s.aux
+    old_steps, old_first_obs = s.info["steps"], s.info["first_obs"]
+    old_steps_val = old_steps.clone()
+    new_steps = torch.full_like(old_steps, float(L - 1))
+    new_first_obs = torch.linspace(-1, 1, old_first_obs.numel(), device="cuda").reshape(old_first_obs.shape)
+    s.info["steps"] = new_steps
+    s.info.update(first_obs=new_first_obs)
+    ref = _state_np(s)
+    so = orc.OracleEnv(name).step(ref, act[3], flags=FLAGS, episode_length=L)
+    s2 = env.step_(s, torch.from_numpy(act[3]).cuda())
+    compare_states(s2, so, f"{name}: in-place after info edits")
+    assert s2.info["steps"] is new_steps and s2.info["first_obs"] is new_first_obs
+    assert bool((s2.aux["done"] == 1).all())  # every env hit the time limit -> autoreset from new_first_obs
+    assert torch.equal(s2.obs, new_first_obs)
+    assert torch.equal(old_steps, old_steps_val)  # the old buffer was not stepped
+
+
+def _eval_np(em, metrics, reward, done, steps):
+    """brax <= 0.0.12 EvalWrapper.step [ext], restated in NumPy (parity-unpinned: no reference
+    artefact holds EvalWrapper output)."""
+    m = dict(metrics, reward=reward)
+    d = done.astype(np.float32)
+    cur = {k: em["cur"][k] + m[k].astype(np.float32) for k in em["cur"]}
+    return {"steps": em["steps"] + np.sum(steps * d, dtype=np.float64),
+            "n": em["n"] + np.sum(d, dtype=np.float64),
+            "comp": {k: em["comp"][k] + np.sum(cur[k] * d, dtype=np.float64) for k in cur},
+            "cur": {k: cur[k] * (1 - d) for k in cur}}
+
+
+@pytest.mark.parametrize("name", ["ant_tag", "ant_gather"])
+def test_eval_wrapper_metrics(name):
+    """create(..., eval_metrics=True) (po_brax/envs/__init__.py:69-70, brax EvalWrapper [ext]):
+    the per-env current-episode metrics and the completed-episode totals after every step equal
+    a NumPy restatement of brax EvalWrapper driven by the ORACLE's step outputs (env fields
+    compared bit-exact first), over episodes of 3 steps so that several complete."""
+    envs = _envs()
+    B, L, T = 128, 3, 7
+    env = envs.create(name, batch_size=B, episode_length=L, eval_metrics=True)
+    u = env.unwrapped
+    keys = _keys(B, 12)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name)
+    so = o.reset(keys, first=True)
+    names = list(s.info["eval_metrics"]["current_episode_metrics"])
+    assert set(names) == set(u.reset_metrics) | {"reward"}
+    em = {"cur": {k: np.zeros(B, np.float32) for k in names}, "comp": {k: 0.0 for k in names},
+          "n": 0.0, "steps": 0.0}
+    rng = np.random.default_rng(2)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        so = o.step(so, act, flags=FLAGS, episode_length=L)
+        s = env.step(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} eval step {t}")
+        om = {n: so[f"m{u.slot_names.index(n)}"] for n in u.step_metrics}
+        em = _eval_np(em, om, so["reward"], so["done"], so["steps"])
+        g = s.info["eval_metrics"]
+        for k in names:
+            np.testing.assert_array_equal(_np(g["current_episode_metrics"][k]), em["cur"][k], err_msg=f"{t} cur {k}")
+            np.testing.assert_allclose(float(g["completed_episodes_metrics"][k]), em["comp"][k], rtol=1e-5,
+                                       atol=1e-4, err_msg=f"{t} comp {k}")
+        assert float(g["completed_episodes"]) == em["n"], t
+        np.testing.assert_allclose(float(g["completed_episodes_steps"]), em["steps"], rtol=1e-6)
+    assert em["n"] >= B  # at least one full round of episodes completed
+
+
+def test_eval_wrapper_heavenhell_metric_mismatch_raises():
+    """AntHeavenHell's step adds metrics['hits'] (ant_heavenhell.py:122) that its reset lacks:
+    brax EvalWrapper's tree_multimap over the two dicts fails there, and so does this one."""
+    envs = _envs()
+    env = envs.create("ant_heavenhell", batch_size=8, eval_metrics=True)
+    s = env.reset(torch.from_numpy(_keys(8, 1)).cuda())
+    with pytest.raises(ValueError, match="tree_multimap"):
+        env.step(s, torch.zeros((8, 8), device="cuda"))
