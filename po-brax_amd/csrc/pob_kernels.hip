@@ -1778,9 +1778,83 @@ POB_D void choice_topk_quad(uint32_t k0, uint32_t k1, int n, int K, int k, uint3
   wave_lds_sync();
 }
 
+// choice_topk for ONE env by the whole wave (all 64 lanes active; k0, k1 wave-uniform): the
+// first K of the stable argsort of random_bits(split(key)[1], (n,)), n <= 2 * 64 * POB_CW_SLOTS.
+//  1. lane l hashes pairs p = l + 64 m: one threefry2x32 call gives elements p and p + h
+//     (h = ceil(n / 2); tf_elem's pairing);
+//  2. candidates: the keys <= T0 for the smallest T0 in 2^30 - 1, 2^31 - 1, 2^32 - 1 with at
+//     least K of them (for n = 156, K = 16 the first bound holds but with probability ~1e-5:
+//     about n / 4 = 39 candidates), compacted into LDS as (key, index) pairs;
+//  3. each candidate's rank by (key, index) among the candidates -- which is its rank among
+//     all n keys, since every non-candidate is larger -- and the candidates of rank < K are
+//     written to out[rank * OS].
+// One env's choice is a short, wave-parallel chain (~2 threefry calls per lane, one ballot
+// round, ~40 broadcast LDS reads) instead of a lane quad hashing n / 4 keys in a row and
+// merging four sorted lists: an AntGather reset wave spent ~66 us in that (profiles/r3c).
+#define POB_CW_SLOTS 8
+#define GA_OBJ_F 5  // k_reset's per-object table: x, y, z, reading intensity, reading slot
+POB_D void choice_topk_wave(uint32_t k0, uint32_t k1, int n, int K, uint2 *lcand, int *out, int OS) {
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t s0, s1;
+  tf_split(k0, k1, 2u, 1u, s0, s1);
+  const int h = (n + 1) >> 1;
+  const int ns = (h + 63) >> 6;  // pair slots in use (wave-uniform)
+  uint32_t ka[POB_CW_SLOTS], kb[POB_CW_SLOTS];
+  bool va[POB_CW_SLOTS], vb[POB_CW_SLOTS];
+#pragma unroll
+  for (int m = 0; m < POB_CW_SLOTS; ++m) {
+    const int p = lane + 64 * m;
+    va[m] = m < ns && p < h;
+    vb[m] = va[m] && p + h < n;
+    ka[m] = 0u; kb[m] = 0u;
+    if (va[m]) threefry2x32(s0, s1, (uint32_t)p, vb[m] ? (uint32_t)(p + h) : 0u, ka[m], kb[m]);
+  }
+  uint32_t T = 0x3FFFFFFFu;
+  for (;;) {  // wave-uniform, at most three rounds
+    int cnt = 0;
+#pragma unroll
+    for (int m = 0; m < POB_CW_SLOTS; ++m) {
+      if (m < ns) {
+        cnt += __popcll(__ballot(va[m] && ka[m] <= T));
+        cnt += __popcll(__ballot(vb[m] && kb[m] <= T));
+      }
+    }
+    if (cnt >= K || T == 0xFFFFFFFFu) break;
+    T = (T << 1) | 1u;
+  }
+  int nc = 0;
+#pragma unroll
+  for (int m = 0; m < POB_CW_SLOTS; ++m) {
+    if (m < ns) {
+      const bool sa = va[m] && ka[m] <= T, sb = vb[m] && kb[m] <= T;
+      const uint64_t ma = __ballot(sa);
+      const uint64_t mb = __ballot(sb);
+      const int pa = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+      nc += __popcll(ma);
+      const int pb = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+      nc += __popcll(mb);
+      const int p = lane + 64 * m;
+      if (sa) lcand[pa] = make_uint2(ka[m], (uint32_t)p);
+      if (sb) lcand[pb] = make_uint2(kb[m], (uint32_t)(p + h));
+    }
+  }
+  wave_lds_sync();
+  for (int e = lane; e < nc; e += 64) {
+    const uint2 ce = lcand[e];
+    int rank = 0;
+#pragma unroll 4
+    for (int f = 0; f < nc; ++f) {
+      const uint2 cf = lcand[f];
+      rank += (cf.x < ce.x || (cf.x == ce.x && cf.y < ce.y)) ? 1 : 0;
+    }
+    if (rank < K) out[rank * OS] = (int)ce.y;
+  }
+  wave_lds_sync();
+}
+
 template <int KIND, int BS>
 POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const int k, uint32_t k0, uint32_t k1,
-                          QReset &R, uint32_t *lds_key, int *lds_idx) {
+                          QReset &R, uint32_t *lds_key, int *lds_idx, const bool wave_choice, float *ga_obj) {
   csys_t &S = *Sp;
   // random_split(rng, 5) (HH, TAG) | 4 (GA) | 3 (stock ant, brax envs/ant.py reset)
   const uint32_t ns = KIND == POB_GATHER ? 4u : (KIND == POB_ANT ? 3u : 5u);
@@ -1844,9 +1918,22 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
     R.rng0 = r[0][0]; R.rng1 = r[0][1];
   } else if (KIND == POB_GATHER) {
     // ant_gather.py:109-123: the env's chosen grid indices go to lds_idx's env row block
-    choice_topk_quad<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, k, lds_key, lds_idx,
-                         lds_idx + POB_MAXOBJ * BS + (threadIdx.x >> 2), BS / 4);
+    if (!wave_choice)  // (else k_reset ran choice_topk_wave for this env already)
+      choice_topk_quad<BS>(r[3][0], r[3][1], S.n_grid, S.n_obj, k, lds_key, lds_idx,
+                           lds_idx + POB_MAXOBJ * BS + (threadIdx.x >> 2), BS / 4);
     R.rng0 = k0; R.rng1 = k1;  // ant_gather.py:106 stores the input key
+    // the objects' positions and sensor readings (ant_gather.py:118-123, _get_readings), object
+    // o on quad lane o % 4, into the env's LDS table (GA_OBJ: x, y, z, intensity, slot)
+    float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
+    const float ori = ga_orientation(b.q[0]);
+    for (int o = k; o < S.n_obj; o += 4) {
+      const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
+      const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
+      float inten;
+      const int slot = ga_reading_slot(S, o, ox, oy, dist2d(b.x[0].x, b.x[0].y, ox, oy), ori, inten);
+      eo[o] = ox; eo[POB_MAXOBJ + o] = oy; eo[2 * POB_MAXOBJ + o] = o < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
+      eo[3 * POB_MAXOBJ + o] = inten; eo[4 * POB_MAXOBJ + o] = __int_as_float(slot);
+    }
   } else if (KIND == POB_ANT) {
     R.rng0 = r[0][0]; R.rng1 = r[0][1];  // (not part of the stock ant's State)
   } else {
@@ -1901,7 +1988,7 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
 // over the quad; lane 0 then writes the task rows (program order: after the frozen fill).
 enum { RROW_POS = 0, RROW_ROT = 1, RROW_VEL = 2, RROW_ANG = 3, RROW_OBS = 4 };
 template <int KIND, int BS>
-POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const int *lds_idx) {
+POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const float *ga_obj) {
   const int N = n_bodies<KIND>(S);
   const QBody &b = R.bd;
   if (arr == RROW_POS) {
@@ -1914,6 +2001,13 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
     for (int i = POB_NDYN + k; i < N; i += 4) {
       row[3 * i] = S.frozen_pos[i][0]; row[3 * i + 1] = S.frozen_pos[i][1]; row[3 * i + 2] = S.frozen_pos[i][2];
     }
+    if (KIND == POB_GATHER) {  // (after the frozen fill in program order) object o on quad lane o % 4
+      const float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
+      for (int o = k; o < S.n_obj; o += 4) {
+        float *d = row + 3 * (11 + o);
+        d[0] = eo[o]; d[1] = eo[POB_MAXOBJ + o]; d[2] = eo[2 * POB_MAXOBJ + o];
+      }
+    }
     if (k == 0) {
       if (KIND == POB_HEAVENHELL || KIND == POB_TAG) {  // Ground is in ant_indices
         row[27] = S.frozen_pos[9][0] + R.ax; row[28] = S.frozen_pos[9][1] + R.ay;
@@ -1921,12 +2015,6 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       if (KIND == POB_HEAVENHELL) {
         row[33] = S.hh_hhp[R.hh_first][0]; row[34] = S.hh_hhp[R.hh_first][1]; row[35] = 1.0f;
         row[36] = S.hh_hhp[1 - R.hh_first][0]; row[37] = S.hh_hhp[1 - R.hh_first][1]; row[38] = 1.0f;
-      } else if (KIND == POB_GATHER) {
-        for (int o = 0; o < S.n_obj; ++o) {
-          const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
-          float *d = row + 3 * (11 + o);
-          d[0] = S.grid[3 * g]; d[1] = S.grid[3 * g + 1]; d[2] = o < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
-        }
       } else if (KIND == POB_TAG) {
         row[30] = R.tx; row[31] = R.ty; row[32] = 0.5f;
       }
@@ -1974,13 +2062,13 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       if (KIND == POB_HEAVENHELL) {
         row[base] = 0.0f;  // priest_in_range = 0 at reset
       } else if (KIND == POB_GATHER) {
+        // the scatter readings[slot] = intensity in object order (a later object wins a slot)
         float *rd = row + base;
         ga_readings_begin(S, rd);
-        const float ori = ga_orientation(b.q[0]);
+        const float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
         for (int o = 0; o < S.n_obj; ++o) {
-          const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
-          const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
-          ga_reading_one(S, o, ox, oy, dist2d(b.x[0].x, b.x[0].y, ox, oy), ori, rd);
+          const int slot = __float_as_int(eo[4 * POB_MAXOBJ + o]);
+          if (slot >= 0) rd[slot] = eo[3 * POB_MAXOBJ + o];
         }
       } else if (KIND == POB_TAG) {
         const bool vis = dist2d(R.tx, R.ty, b.x[0].x, b.x[0].y) <= S.tag_visible_radius;
@@ -2038,10 +2126,12 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   static_assert(BS == 64, "k_reset stages one wave's rows per block");
   POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING; waves with nothing to reset exit unrecorded)
   POB_TS(0);
-  __shared__ uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_key[KIND == POB_GATHER ? POB_MAXOBJ * BS : 1];
   // per-lane sorted lists, then the merged choice per env (POB_MAXOBJ x 16 envs)
   __shared__ int lds_idx[KIND == POB_GATHER ? POB_MAXOBJ * BS + POB_MAXOBJ * (BS / 4) : 1];
   __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
+  // AntGather: each env's objects (x, y, z, reading intensity, reading slot), POB_MAXOBJ each
+  __shared__ float ga_obj[KIND == POB_GATHER ? (BS / 4) * GA_OBJ_F * POB_MAXOBJ : 1];
   extern __shared__ float stg[];  // 16 rows of WP floats
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
@@ -2099,8 +2189,21 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   __syncthreads();
   const float *LT = legtab + k * POB_LEG_FLOATS;
   const float *WT = legtab + 4 * POB_LEG_FLOATS;
+  // AntGather's object choice, one env at a time by the whole wave (ant_gather.py:118)
+  const bool wave_choice = KIND == POB_GATHER && S.n_grid <= 2 * 64 * POB_CW_SLOTS &&
+                           S.n_grid <= POB_MAXOBJ * BS / 2;  // (key, index) pairs in lds_key
+  if (wave_choice) {
+    for (uint32_t m = rows; m != 0u; m &= m - 1u) {
+      const int e = __builtin_ctz(m);
+      const uint32_t a0 = __builtin_amdgcn_readlane(k0, 4 * e), a1 = __builtin_amdgcn_readlane(k1, 4 * e);
+      uint32_t c0, c1;
+      tf_split(a0, a1, 4u, 3u, c0, c1);  // rng3 of random_split(rng, 4) (ant_gather.py:110)
+      choice_topk_wave(c0, c1, S.n_grid, S.n_obj, (uint2 *)lds_key, lds_idx + POB_MAXOBJ * BS + e, BS / 4);
+    }
+  }
   QReset R;
-  if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx);
+  if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx, wave_choice, ga_obj);
+  if (KIND == POB_GATHER) wave_lds_sync();  // the objects' table, read by other lanes of the quad
   POB_TS(2);
 #ifdef POB_EXP_TIMING
   {  // the first active lane's stamps inside the compute (stamps 4..7 of the wave's row)
@@ -2123,7 +2226,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
                                          : (arr == RROW_ROT ? s.first_rot
                                                             : (arr == RROW_VEL ? s.first_vel
                                                                                : (arr == RROW_ANG ? s.first_ang : s.first_obs))));
-    if (active) qreset_row<KIND, BS>(S, R, k, arr, myrow, lds_idx);
+    if (active) qreset_row<KIND, BS>(S, R, k, arr, myrow, ga_obj);
     wave_lds_sync();
     if (arr == RROW_OBS) reset_store_rows<float>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
     else reset_store_rows<QT>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);

@@ -15,10 +15,22 @@ from po_brax_amd import _lib, envs, jumpy  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 NAME = sys.argv[2] if len(sys.argv) > 2 else "ant_heavenhell"
-GYM = len(sys.argv) > 3 and sys.argv[3] == "gym"  # time the gym path's masked reset kernel instead
+# "gym": time the gym path's masked reset kernel instead; "masked": a masked reset (RESET_OWN)
+# of a few done envs (argv[4]: how many, default 8), as a gym step with done envs runs it
+GYM = len(sys.argv) > 3 and sys.argv[3] in ("gym", "masked")
+MASKED = len(sys.argv) > 3 and sys.argv[3] == "masked"
 key = jumpy.random_prngkey(0)
 act = torch.empty((B, 8), device="cuda")
-if GYM:
+if MASKED:
+    env = envs.create(NAME, batch_size=B, episode_length=1000)
+    s = env.reset(jumpy.random_split(key, B + 1)[1:].contiguous())
+    nd = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    done = torch.zeros(B, device="cuda")
+    done[torch.randperm(B, generator=torch.Generator().manual_seed(0))[:nd].cuda()] = 1.0
+    for _ in range(3):
+        s.aux["done"].copy_(done)
+        env.unwrapped._reset_where_done(s, _lib.RESET_OWN)
+elif GYM:
     gym = envs.create_gym_env(NAME, batch_size=B, seed=0, episode_length=1000)
     gym.reset()
     for _ in range(30):
