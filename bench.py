@@ -82,8 +82,10 @@ def main() -> int:
                     help="envs PER GPU (weak scaling, opt-in); overrides --global-batch")
     ap.add_argument("--episode-length", type=int, default=1000)
     ap.add_argument("--gym", action="store_true", help="create_gym_env path (gym-side autoreset)")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU-baseline budget per leg")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (default: OMP_NUM_THREADS, the pool's per-GPU share)")
     ap.add_argument("--gather-obs", action="store_true",
                     help="RCCL all-gather of every timed step's obs batch, overlapped with the next step (N>1)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -300,7 +302,8 @@ def main() -> int:
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and gym is None:
-        cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, B, args.cpu_seconds)
+        cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, B, args.cpu_seconds,
+                           args.cpu_threads)
 
     par = f"env-shard x{world}" + (" (strong: global batch split)" if strong else " (weak: batch per GPU)")
     line = {
@@ -361,12 +364,17 @@ def committed_profile(env: str, B: int, qp: str):
     return best
 
 
-def cpu_baseline(name: str, B: int, seconds: float) -> dict:
+def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0) -> dict:
     """The C restatement (kind "port": same algorithm, oracle/pob_oracle.c) compiled
-    -O3 -march=native on this host, timed on the same workload (this GPU's batch B), on
-    every core this process may run on (``sched_getaffinity``, SURVEY.md §8(d) "all cores";
-    the reported ``value``), on the launcher's per-process share (``OMP_NUM_THREADS``, 16 on
-    the GPU box) and on one thread (OpenMP over envs, static schedule).  Time-boxed samples."""
+    -O3 -march=native on this host, timed on the same workload (this GPU's batch B): on the
+    process's CPU share and on one thread (OpenMP over envs, static schedule; time-boxed).
+
+    The share is ``OMP_NUM_THREADS`` (the GPU pool sets 16 per GPU and asks jobs to size their
+    thread pools to it: ``sched_getaffinity`` there lists the whole shared host, 256 cores,
+    most of them other tenants'), or every affinity core when it is unset; ``threads`` (bench
+    ``--cpu-threads``, e.g. all cores of a dedicated host) overrides it.  The reported
+    ``value`` is the multi-threaded leg; ``all_cores_linear_bound`` = single-thread rate x
+    affinity cores is an upper bound for the whole host, not a measurement."""
     import numpy as np
     import orc
     import pob_np as P
@@ -375,12 +383,12 @@ def cpu_baseline(name: str, B: int, seconds: float) -> dict:
     except AttributeError:  # pragma: no cover
         aff = os.cpu_count() or 1
     share = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff)))
+    nt_multi = max(1, min(aff, threads)) if threads > 0 else share
     e = orc.OracleEnv(name, native=True)
-    s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=aff)
+    s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=nt_multi)
     acts = np.random.default_rng(0).uniform(-1, 1, (2, B, 8)).astype(np.float32)
-    legs = [("all", aff)] + ([("share", share)] if share not in (aff, 1) else []) + [("single", 1)]
     out = {}
-    for leg, nt in legs:
+    for leg, nt in (("multi", nt_multi), ("single", 1)):
         e.step(s, acts[0], flags=3, nthreads=nt, inplace=True)  # warm caches / the thread pool
         n, t0 = 0, time.perf_counter()
         while True:
@@ -390,17 +398,17 @@ def cpu_baseline(name: str, B: int, seconds: float) -> dict:
                 break
         dt = time.perf_counter() - t0
         out[leg] = (B * n / dt, n, dt, nt)
-    v, n, dt, _ = out["all"]
-    res = {"value": round(v, 1), "unit": "env-steps/s", "cores": aff, "kind": "port",
-           "single_thread_value": round(out["single"][0], 1)}
-    if "share" in out:
-        res["share_threads"] = share
-        res["share_threads_value"] = round(out["share"][0], 1)
-    res["sample"] = (f"{name} B={B} (the GPU workload's batch), the same fused step (oracle/pob_oracle.c, "
-                     "gcc -O3 -march=native, OpenMP over envs): "
-                     + "; ".join(f"{o[1]} steps in {o[2]:.1f} s on {o[3]} thread(s)" for o in out.values()))
-    res.update(cpu=orc.cpu_model(), nproc=os.cpu_count(), affinity_cores=aff)
-    return res
+    v, n, dt, _ = out["multi"]
+    v1 = out["single"][0]
+    return {"value": round(v, 1), "unit": "env-steps/s", "cores": nt_multi, "kind": "port",
+            "single_thread_value": round(v1, 1),
+            "all_cores_linear_bound": round(v1 * aff, 1),
+            "sample": f"{name} B={B} (the GPU workload's batch), the same fused step (oracle/pob_oracle.c, "
+                      "gcc -O3 -march=native, OpenMP over envs): "
+                      + "; ".join(f"{o[1]} steps in {o[2]:.1f} s on {o[3]} thread(s)" for o in out.values()),
+            "threads_basis": ("--cpu-threads" if threads > 0 else
+                              "OMP_NUM_THREADS (the pool's per-GPU CPU share)" if share < aff else "all affinity cores"),
+            "cpu": orc.cpu_model(), "nproc": os.cpu_count(), "affinity_cores": aff}
 
 
 if __name__ == "__main__":
