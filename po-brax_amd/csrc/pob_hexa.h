@@ -66,6 +66,24 @@ __host__ __device__ constexpr int hex_max_walls(int kind) {
   return kind == POB_ANT ? 0 : (kind == POB_HEAVENHELL ? POB_MAXW : 4);
 }
 
+// The walls in registers (POB_HEX_VWALLS, default on): every wall's broadphase box (xy) and
+// row, and the common z extent, loaded once per launch from the LDS table into VGPRs.  Read
+// from the system table instead, they were ~80 scalar values per collide substep -- more than
+// the SGPR budget holds across the substep loop -- so each collide substep re-issued ~20
+// scalar loads and waited for them (SQ_WAIT_ANY was 42 % of a wave's cycles at HH B = 4 096).
+#ifndef POB_HEX_VWALLS
+#define POB_HEX_VWALLS 1
+#endif
+#define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
+#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz
+#define HW_FLOATS (4 * POB_MAXW + 2)
+template <int MW>
+struct HWalls {
+  float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
+  float row[MW > 0 ? MW : 1][POB_WALL_FLOATS];
+  float cz, hz;
+};
+
 struct HBody {
   v3 x, v, w;
   q4 q;
@@ -86,7 +104,8 @@ struct HContacts {
 // (wall, end) order.  (Per-body boxes would not shorten the walk: the wave iterates over the
 // most walls any of its lanes is near, a lower leg's.)
 template <int MW, class G>
-POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBody &b, HContacts &ct) {
+POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, const HBody &b,
+                   HContacts &ct) {
   ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
   // (both wall loops are unrolled over POB_MAXW with wave-uniform guards, so the walls' boxes
@@ -104,7 +123,11 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
     for (int w = 0; w < MW; ++w) {
       // every wall's box is loaded (the table always holds POB_MAXW rows) and w < nw is a
       // predicate: loads behind a per-wall branch were one scalar round trip per wall
+#if POB_HEX_VWALLS
+      const float lx = HW.lx[w], ly = HW.ly[w], hx = HW.hx[w], hy = HW.hy[w];
+#else
       const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
+#endif
       const bool near = (b.x.x <= hx) & (b.x.x >= lx) & (b.x.y <= hy) & (b.x.y >= ly);
       m |= (near & (w < nw)) ? 1u << w : 0u;
     }
@@ -117,18 +140,24 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
     const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
     const float r = HT[HT_R];
     const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
+#if POB_HEX_VWALLS
+    const float (&R)[MW > 0 ? MW : 1][POB_WALL_FLOATS] = HW.row;
+    const float hz = HW.hz, cz = HW.cz;
+#else
     // every wall row in one scalar round trip (not one per near wall inside its branch)
     float R[MW > 0 ? MW : 1][POB_WALL_FLOATS];
 #pragma unroll
     for (int w = 0; w < MW; ++w)
 #pragma unroll
       for (int k = 0; k < POB_WALL_FLOATS; ++k) R[w][k] = S.wall_row[w][k];
+    const float hz = S.wall_hz, cz = S.wall_cz;
+#endif
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
       const bool on = ((m >> w) & 1u) != 0u;
       if (__any(on)) {
-        qwall_end_v(g, S, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
-        qwall_end_v(g, S, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
+        qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
+        qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
       }
     }
   }
@@ -141,8 +170,8 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HBod
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
 template <int MW, class G>
-POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, HBody &b, const float act, v3 &cv,
-                        v3 &ca, const bool COLLIDE) {
+POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, HBody &b,
+                        const float act, v3 &cv, v3 &ca, const bool COLLIDE) {
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
   const bool torso = isP && hip, leg = !isP && !hip;
   const v3 px = b.x;
@@ -232,7 +261,11 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, HBody
       DA = torso ? dat : (leg ? dal : daa);
     }
     if (COLLIDE) {
-      hdetect<MW>(g, S, HT, WT, b, ct);
+      hdetect<MW>(g, S, HT, WT, HW, b, ct);
+#ifdef POB_EXP_NO_WALL_RESPONSE  // timing experiment only: detection kept, no wall response
+      asm volatile("" ::"v"(ct.pen), "v"(ct.n.x), "v"(ct.n.y), "v"(ct.n.z), "v"(ct.pe.x), "v"(ct.pe.y), "v"(ct.pe.z));
+      ct.pen = -1.0f;
+#endif
       const float im = HT[HT_IM];
       if (ct.gpen > 0.0f) oground_position(g, S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
       if (ct.pen > 0.0f) owall_position(g, S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);

@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
   POB_TS(0);
   __shared__ float stg[POB_HSTAGE_FLOATS];
-  __shared__ __attribute__((aligned(16))) float htab[HT_TAB_FLOATS];
+  __shared__ __attribute__((aligned(16))) float htab[HT_TAB_FLOATS + HW_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
@@ -1465,12 +1465,27 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     stage_table<16 * HT_FLOATS>(htab, src, (int)threadIdx.x, 64);
     const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
     stage_table<POB_MAXW * POB_WALL_FLOATS>(htab + 16 * HT_FLOATS, wsrc, (int)threadIdx.x, 64);
+    if (lane < HW_FLOATS) {  // the walls' broadphase boxes (xy) and common z extent
+      const int w = lane >> 2, c = lane & 3;
+      htab[HT_TAB_FLOATS + lane] = lane >= HW_CZ ? (lane == HW_CZ ? S.wall_cz : S.wall_hz)
+                                                 : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
+    }
     wave_lds_sync();
   }
   float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
 #pragma unroll
   for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
   const float *WT = htab + 16 * HT_FLOATS;
+  constexpr int HMW = hex_max_walls(KIND);
+  HWalls<HMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
+#pragma unroll
+  for (int w = 0; w < HMW; ++w) {
+    const float *bx = htab + HT_TAB_FLOATS + HW_BOX + 4 * w;
+    HW.lx[w] = bx[0]; HW.ly[w] = bx[1]; HW.hx[w] = bx[2]; HW.hy[w] = bx[3];
+#pragma unroll
+    for (int k = 0; k < POB_WALL_FLOATS; ++k) HW.row[w][k] = WT[POB_WALL_FLOATS * w + k];
+  }
+  HW.cz = htab[HT_TAB_FLOATS + HW_CZ]; HW.hz = htab[HT_TAB_FLOATS + HW_CZ + 1];
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
@@ -1483,29 +1498,37 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
     GuardBranch gb;
-    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false);  // timing experiment only
 #else
+#ifdef POB_HEX_UNROLL2
+#define HEX_SUBSTEPS(G)                                                                       \
+  _Pragma("nounroll") for (int it = 0; it < iters; ++it) {                                   \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, false);                  \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, true);                   \
+  }
+#else
+#define HEX_SUBSTEPS(G)                                                                       \
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0);
+#endif
     if constexpr (!GACC) {
       GuardBranch gb;
-#pragma nounroll
-      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+      HEX_SUBSTEPS(gb)
     } else {
     // one wave per SIMD (GACC): the substeps without guard branches (GuardAcc, pob_math.h); a wave any of whose lanes
     // met an operand outside the fast forms' range reruns them from the loaded state with
     // the branch guards (bit-identical for every lane that stayed in range)
     const HBody b0 = bd;
     GuardAcc ga;
-#pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(ga, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+    HEX_SUBSTEPS(ga)
     if (__builtin_expect(__any(ga.bad()), 0)) {
       bd = b0;
       cvl = V(0.0f, 0.0f, 0.0f); cal = cvl;
       GuardBranch gb;
-#pragma nounroll
-      for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, bd, a, cvl, cal, (it & 1) != 0);
+      HEX_SUBSTEPS(gb)
     }
     }
 #endif

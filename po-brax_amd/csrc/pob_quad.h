@@ -113,12 +113,13 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 // sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
 // (the row's six floats given as values: LDS rows for a per-lane wall walk, the system
 // table's scalars for a wave-uniform one)
+// (wall_hz / wall_cz given as values: the sixteen-lane kernel keeps them in registers)
 template <class G = GuardBranch>
-POB_D void qwall_end_v(G &g, csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
-                       const float hy, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn, bool &bsel,
-                       v3 &bpe) {
-  const v3 h = V(hx, hy, S.wall_hz);
-  v3 d = vsub(p, V(cx, cy, S.wall_cz));
+POB_D void qwall_end_vz(G &g, const float wall_hz, const float wall_cz, const float cx, const float cy, const float c,
+                        const float s, const float hx, const float hy, v3 p, float r, float T, bool on, bool q1,
+                        float &best, v3 &bn, bool &bsel, v3 &bpe) {
+  const v3 h = V(hx, hy, wall_hz);
+  v3 d = vsub(p, V(cx, cy, wall_cz));
   float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
   float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
   float ex = lx - qx, ey = ly - qy, ez = lz - qz;
@@ -143,6 +144,12 @@ POB_D void qwall_end_v(G &g, csys_t &S, const float cx, const float cy, const fl
       bpe = p;
     }
   }
+}
+template <class G = GuardBranch>
+POB_D void qwall_end_v(G &g, csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
+                       const float hy, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn, bool &bsel,
+                       v3 &bpe) {
+  qwall_end_vz(g, S.wall_hz, S.wall_cz, cx, cy, c, s, hx, hy, p, r, T, on, q1, best, bn, bsel, bpe);
 }
 POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
                      bool &bsel, v3 &bpe) {
