@@ -75,13 +75,22 @@ __host__ __device__ constexpr int hex_max_walls(int kind) {
 #define POB_HEX_VWALLS 1
 #endif
 #define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
-#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz
-#define HW_FLOATS (4 * POB_MAXW + 2)
+#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls
+#define HW_FLOATS (4 * POB_MAXW + 5)
 template <int MW>
 struct HWalls {
   float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
   float row[MW > 0 ? MW : 1][POB_WALL_FLOATS];
   float cz, hz;
+  // the table scalars the compiler re-loaded inside the substep loop for want of SGPRs (one
+  // waited scalar load per joint projection and per contact): kept in VGPRs as well
+  float s_pos, friction;
+  int n_walls;
+};
+// the contact functions' view of the table (oground_position / owall_position /
+// ocontact_vel_one read S.friction and S.inv_h only)
+struct HCon {
+  float friction, inv_h;
 };
 
 struct HBody {
@@ -116,6 +125,8 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWal
   if (MW > 0) {
 #ifdef POB_EXP_NO_WALLS
     const int nw = 0;  // timing experiment only
+#elif POB_HEX_VWALLS
+    const int nw = HW.n_walls;
 #else
     const int nw = S.n_walls;
 #endif
@@ -174,6 +185,11 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
                         const float act, v3 &cv, v3 &ca, const bool COLLIDE) {
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
   const bool torso = isP && hip, leg = !isP && !hip;
+#if POB_HEX_VWALLS
+  const HCon SC{HW.friction, S.inv_h};
+#else
+  const csys_t &SC = S;
+#endif
   const v3 px = b.x;
   const q4 pq = b.q;
   // 1. acceleration level: the joint's torque tt (actuator + damping) on both of its lanes
@@ -229,7 +245,11 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
       if (L2 > 0.0f) {
         const v3 ep = vcross(rp, d), ec = vcross(rc, d);
         const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
+#if POB_HEX_VWALLS
+        const float k = (L2 * HW.s_pos) * g.rcp(den);
+#else
         const float k = (L2 * S.s_pos) * g.rcp(den);
+#endif
         P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
       }
       const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
@@ -267,8 +287,8 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
       ct.pen = -1.0f;
 #endif
       const float im = HT[HT_IM];
-      if (ct.gpen > 0.0f) oground_position(g, S, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
-      if (ct.pen > 0.0f) owall_position(g, S, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+      if (ct.gpen > 0.0f) oground_position(g, SC, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
+      if (ct.pen > 0.0f) owall_position(g, SC, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
     }
     b.x = vadd(b.x, DX);
     qadd_half(b.q, qmul_vq(DA, b.q), 1.0f);
@@ -287,11 +307,11 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
     const float im = HT[HT_IM];
     if (ct.gpen > 0.0f)
-      ocontact_vel_one(g, S, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+      ocontact_vel_one(g, SC, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
     if (ct.pen > 0.0f) {
       const v3 e0 = HTV(HT, HT_E0);
       const v3 e = ct.sel ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(g, S, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
+      ocontact_vel_one(g, SC, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
     }
     b.v = vadd(b.v, dV); b.w = vadd(b.w, dW);
     cv = vadd(cv, dV);

@@ -272,7 +272,27 @@ struct TaskOut {
   // AntGather objects already handled by the env's four lanes (ga_quad_objects)
   bool ga_done_quad, ga_any_a, ga_any_b, ga_all_wait;
   int ga_na, ga_nb;
+  // task bodies' input xy loaded before the physics (tp_ok): HH priest, target, hell
+  // (rows 10, 11, 12) and TAG target (row 10) -- their loads would otherwise be a memory
+  // round trip after the substeps, on the wave's critical path
+  bool tp_ok;
+  float tp[6];
 };
+
+// the task bodies' xy (TaskOut::tp) of env row r3
+template <int KIND, typename QT>
+POB_D void task_prefetch(const StatePtrs &in, const size_t r3, TaskOut &t) {
+  using QQ = Q<QT>;
+  t.tp_ok = KIND == POB_HEAVENHELL || KIND == POB_TAG;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) t.tp[i] = 0.0f;
+  if (KIND == POB_HEAVENHELL) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { t.tp[2 * i] = QQ::ld(in.pos, r3 + 30 + 3 * i); t.tp[2 * i + 1] = QQ::ld(in.pos, r3 + 31 + 3 * i); }
+  } else if (KIND == POB_TAG) {
+    t.tp[0] = QQ::ld(in.pos, r3 + 30); t.tp[1] = QQ::ld(in.pos, r3 + 31);
+  }
+}
 
 // Per-env POMDP logic after the physics (env.step minus System.step) + EpisodeWrapper:
 // reward / done / metrics / rng, the task part of the obs, and the task bodies' rows.
@@ -294,13 +314,15 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     // ant_heavenhell.py:106-123
     reward = dead > 0.0f ? S.hh_dying_cost : 0.0f;
     const float *ip = in.pos;
-    bool in0 = dist2d(QQ::ld(ip, r3 + 33), QQ::ld(ip, r3 + 34), x0.x, x0.y) <= S.hh_visible_radius;  // Target
-    bool in1 = dist2d(QQ::ld(ip, r3 + 36), QQ::ld(ip, r3 + 37), x0.x, x0.y) <= S.hh_visible_radius;  // Hell
-    bool in2 = dist2d(QQ::ld(ip, r3 + 30), QQ::ld(ip, r3 + 31), x0.x, x0.y) <= S.hh_visible_radius;  // Priest
+    const float px_ = t.tp_ok ? t.tp[0] : QQ::ld(ip, r3 + 30), py_ = t.tp_ok ? t.tp[1] : QQ::ld(ip, r3 + 31);
+    const float tx = t.tp_ok ? t.tp[2] : QQ::ld(ip, r3 + 33), ty = t.tp_ok ? t.tp[3] : QQ::ld(ip, r3 + 34);
+    const float hx_ = t.tp_ok ? t.tp[4] : QQ::ld(ip, r3 + 36), hy_ = t.tp_ok ? t.tp[5] : QQ::ld(ip, r3 + 37);
+    bool in0 = dist2d(tx, ty, x0.x, x0.y) <= S.hh_visible_radius;    // Target
+    bool in1 = dist2d(hx_, hy_, x0.x, x0.y) <= S.hh_visible_radius;  // Hell
+    bool in2 = dist2d(px_, py_, x0.x, x0.y) <= S.hh_visible_radius;  // Priest
     if (in0) reward = 1.0f;
     if (in1) reward = -1.0f;
     done = reward != 0.0f ? 1.0f : 0.0f;
-    const float tx = QQ::ld(ip, r3 + 33);
     const float sgn = tx > 0.0f ? 1.0f : (tx < 0.0f ? -1.0f : 0.0f);
     t.ob0 = in2 ? sgn : 0.0f;
     m2 = done;  // metrics['hits']
@@ -347,7 +369,8 @@ POB_D void task_step(csys_t &S, const StatePtrs &in, const int b, const size_t r
     uint32_t k20, k21;  // randint(rng1, (), 0, 4) = bits(split(rng1)[1]) % 4
     tf_split(c0, c1, 2u, 1u, k20, k21);
     const int ch = (int)(tf_elem(k20, k21, 1u, 0u) % 4u);
-    const float ax = x0.x, ay = x0.y, tx = QQ::ld(in.pos, r3 + 30), ty = QQ::ld(in.pos, r3 + 31);
+    const float ax = x0.x, ay = x0.y;
+    const float tx = t.tp_ok ? t.tp[0] : QQ::ld(in.pos, r3 + 30), ty = t.tp_ok ? t.tp[1] : QQ::ld(in.pos, r3 + 31);
     float vx = ax - tx, vy = ay - ty;
     const float nrm = sqrtf(vx * vx + vy * vy);
     vx = vx / nrm; vy = vy / nrm;
@@ -794,6 +817,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   float jang[QNJ], jvel[QNJ];
   v3 cvl[QNB], cal[QNB];
   TaskOut t;
+  t.tp_ok = false;
   if (act_lane) {
     const float xb = bd.x[0].x;
     float a[QNJ];
@@ -1206,6 +1230,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   float jang = 0.0f, jvel = 0.0f;
   v3 cvl[ONB], cal[ONB];
   TaskOut t;
+  t.tp_ok = false;
   if (act_lane) {
     const float xb = bd.x[0].x;
     const float a = act[(size_t)b * POB_NJ + jown];
@@ -1467,8 +1492,11 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     stage_table<POB_MAXW * POB_WALL_FLOATS>(htab + 16 * HT_FLOATS, wsrc, (int)threadIdx.x, 64);
     if (lane < HW_FLOATS) {  // the walls' broadphase boxes (xy) and common z extent
       const int w = lane >> 2, c = lane & 3;
-      htab[HT_TAB_FLOATS + lane] = lane >= HW_CZ ? (lane == HW_CZ ? S.wall_cz : S.wall_hz)
-                                                 : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
+      const int e = lane - HW_CZ;
+      htab[HT_TAB_FLOATS + lane] =
+          e >= 0 ? (e == 0 ? S.wall_cz : e == 1 ? S.wall_hz : e == 2 ? S.s_pos : e == 3 ? S.friction
+                                                                                : __int_as_float(S.n_walls))
+                 : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
     }
     wave_lds_sync();
   }
@@ -1486,12 +1514,24 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     for (int k = 0; k < POB_WALL_FLOATS; ++k) HW.row[w][k] = WT[POB_WALL_FLOATS * w + k];
   }
   HW.cz = htab[HT_TAB_FLOATS + HW_CZ]; HW.hz = htab[HT_TAB_FLOATS + HW_CZ + 1];
+  HW.s_pos = htab[HT_TAB_FLOATS + HW_CZ + 2]; HW.friction = htab[HT_TAB_FLOATS + HW_CZ + 3];
+  HW.n_walls = __float_as_int(htab[HT_TAB_FLOATS + HW_CZ + 4]);
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
   float jang = 0.0f, jvel = 0.0f;
   v3 cvl = V(0.0f, 0.0f, 0.0f), cal = cvl;
   TaskOut t;
+  t.tp_ok = false;
+  if (act_lane && lane0) {
+    // the task inputs, loaded before the physics so that their round trip overlaps it
+    float steps = in.steps ? in.steps[b] : 0.0f;
+    if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
+    t.steps = steps;
+    t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+    t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+    task_prefetch<KIND, QT>(in, r3, t);
+  }
   if (act_lane) {
     const float xb = bd.x.x;
     const float a = act[(size_t)b * POB_NJ + jown];
@@ -1547,11 +1587,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     Ls.set3(0, cvl);
     wave_lds_sync();
     if (lane0) {
-      float steps = in.steps ? in.steps[b] : 0.0f;
-      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
-      t.steps = steps;
-      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
-      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
       t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
       if (KIND == POB_ANT) {
         // contact rows 0..8 = torso, then Aux k (lane 7 - k) and lower leg k (lane 15 - k)

@@ -142,8 +142,8 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
 }
 
 // position-level ground contact (n = +z; qcontact_position's ground branch) on body (x, q)
-template <class G = GuardBranch>
-POB_D void oground_position(G &g, csys_t &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
+template <class G = GuardBranch, class SS = csys_t>
+POB_D void oground_position(G &g, const SS &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
                             const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
   const v3 cp = V(pe.x, pe.y, pe.z - rad);
   const v3 rr = vsub(cp, x);
@@ -170,8 +170,8 @@ POB_D void oground_position(G &g, csys_t &S, const float pen, const v3 pe, const
 }
 
 // position-level wall contact (qcontact_position's general branch)
-template <class G = GuardBranch>
-POB_D void owall_position(G &g, csys_t &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
+template <class G = GuardBranch, class SS = csys_t>
+POB_D void owall_position(G &g, const SS &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
                           const v3 x, const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
   v3 cp = vfma(n, -rad, pe);
   v3 rr = vsub(cp, x);
@@ -218,8 +218,8 @@ POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, con
 }
 
 // velocity-level contact (qcontact_velocity's body of one contact); e = the body-frame end
-template <class G = GuardBranch>
-POB_D void ocontact_vel_one(G &g, csys_t &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
+template <class G = GuardBranch, class SS = csys_t>
+POB_D void ocontact_vel_one(G &g, const SS &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
                             const float im, const v3 x, const q4 q, const v3 v, const v3 w, v3 &dV, v3 &dW) {
   v3 pe = vadd(x, qrot_xy(e, q));
   v3 cp = vfma(n, -rad, pe);

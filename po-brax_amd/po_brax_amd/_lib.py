@@ -2,7 +2,8 @@
 
 The product path is HIP-only: importing this module loads the in-tree ``libpob.so``
 built by ``__graft_entry__.build()`` and raises ImportError if it is missing -- there is
-no CPU fallback.  ``torch`` is imported first so that libpob.so binds to the HIP runtime
+no CPU fallback.  The per-step entry points (pob_step, pob_reset, pob_reset_where_done_shard)
+are called through the pybind11 module ``_pob`` (``pob`` below); the rest through ctypes.  ``torch`` is imported first so that libpob.so binds to the HIP runtime
 torch already loaded (same SONAME, libamdhip64.so.7).
 """
 from __future__ import annotations
@@ -100,6 +101,23 @@ def _load():
 
 
 lib = _load()
+
+
+def _load_pyext():
+    """The pybind11 binding of the per-step entry points (csrc/pob_py.cpp), bound to the
+    functions of the libpob.so loaded above (so a POB_LIB build is used by both bindings)."""
+    try:
+        from . import _pob
+    except ImportError as e:
+        raise ImportError(f"po_brax_amd._pob (pybind11 binding) is not built: {e}; build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'`") from e
+    addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+    _pob.bind(addr(lib.pob_step), addr(lib.pob_reset), addr(lib.pob_reset_where_done_shard),
+              addr(lib.pob_last_error))
+    return _pob
+
+
+pob = _load_pyext()
 
 
 def check(rc: int) -> None:

@@ -23,7 +23,7 @@ from typing import Any, Dict, Optional
 import torch
 
 from .. import _lib
-from .._lib import lib, check
+from .._lib import lib, check, pob
 
 F_EPISODE, F_AUTORESET, F_ZERO = _lib.F_EPISODE, _lib.F_AUTORESET, _lib.F_ZERO_STEPS_ON_DONE
 
@@ -406,8 +406,7 @@ class PoBraxEnv(Env):
         B = keys.shape[0]
         b = self._empty(B, episode, first)
         cs = self._cstate(b)
-        check(lib.pob_reset(self._handle, B, keys.data_ptr(), C.byref(cs),
-                            _lib.stream_handle(self.device)))
+        pob.reset(self._handle.value, B, keys.data_ptr(), C.addressof(cs), _lib.stream_handle(self.device))
         return self._state_of(b, False, squeeze)
 
     @staticmethod
@@ -446,9 +445,9 @@ class PoBraxEnv(Env):
                     (self.device.index is None or action.device.index == self.device.index) and \
                     action.is_contiguous() and \
                     action.numel() == fast[2] * self._A:
-                cs = C.byref(fast[1])
-                check(lib.pob_step(self._handle, fast[2], cs, action.data_ptr(), cs, flags,
-                                   int(episode_length), _lib.stream_handle(self.device)))
+                cs = fast[3]  # the cached struct's address (fast[1] keeps it alive)
+                pob.step(self._handle.value, fast[2], cs, action.data_ptr(), cs, flags, int(episode_length),
+                         _lib.stream_handle(self.device))
                 return state
         squeeze = state.obs.ndim == 1
         if squeeze:
@@ -484,12 +483,12 @@ class PoBraxEnv(Env):
                                  episode_length=int(episode_length), bin=bin_, bout=bout, squeeze=squeeze))
             return None
         else:
-            check(lib.pob_step(self._handle, B, C.byref(ci), act.data_ptr(), C.byref(co), flags,
-                               int(episode_length), _lib.stream_handle(self.device)))
+            pob.step(self._handle.value, B, C.addressof(ci), act.data_ptr(), C.addressof(co), flags,
+                     int(episode_length), _lib.stream_handle(self.device))
         out = self._state_of(bout, True, squeeze)
         if inplace and not squeeze:
             # in place, the input and output buffers are the same: one struct serves both
-            out.aux["_fast"] = (self._fast_refs(out, flags, episode_length), co, B)
+            out.aux["_fast"] = (self._fast_refs(out, flags, episode_length), co, B, C.addressof(co))
         return out
 
     # helpers for the gym / randomized-autoreset wrappers
@@ -500,9 +499,9 @@ class PoBraxEnv(Env):
         b = self._bufs_of(state)
         cs = self._cstate(b)
         B = b["pos"].shape[0]
-        check(lib.pob_reset_where_done_shard(self._handle, B, int(total) if total else B, int(first), mode,
-                                             _lib.ptr(gym_in), _lib.ptr(gym_out), C.byref(cs),
-                                             _lib.stream_handle(self.device)))
+        pob.reset_where_done_shard(self._handle.value, B, int(total) if total else B, int(first), mode,
+                                   _lib.ptr(gym_in) or 0, _lib.ptr(gym_out) or 0, C.addressof(cs),
+                                   _lib.stream_handle(self.device))
 
 
 # set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here

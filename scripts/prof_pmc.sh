@@ -15,7 +15,7 @@ i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
            "SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SMEM SQ_IFETCH SQ_INSTS_VSKIPPED SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-           ${EXTRA_SETS:-"FETCH_SIZE WRITE_SIZE"}; do
+           ${EXTRA_SETS:-FETCH_SIZE WRITE_SIZE}; do
   i=$((i + 1))
   timeout -s KILL 90 rocprofv3 --pmc $set -d $OUT/pmc$i -o pmc$i --output-format csv -- $B > $OUT/bench_pmc$i.json 2> $OUT/pmc$i.err || { tail -5 $OUT/pmc$i.err; exit 1; }
 done

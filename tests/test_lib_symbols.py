@@ -72,3 +72,21 @@ def test_ctypes_state_layout_matches_header():
     field is a pointer, so equal order means equal layout)."""
     from po_brax_amd import _lib
     assert [n for n, _ in _lib.pob_state._fields_] == _struct_fields("pob_state")
+
+
+def test_pybind_module_binds_the_loaded_library():
+    """po_brax_amd._pob (pybind11, csrc/pob_py.cpp) is built, bound to the entry points of the
+    libpob.so the ctypes layer loaded, and maps C status codes to ValueError / RuntimeError
+    (no GPU needed: a NULL env is rejected before any HIP call)."""
+    import __graft_entry__ as g
+    g.build_pyext()
+    import pytest
+    from po_brax_amd import _lib
+    assert _lib.pob.ENTRY_POINTS == ("pob_step", "pob_reset", "pob_reset_where_done_shard")
+    assert set(_lib.pob.ENTRY_POINTS) <= set(_declared())
+    with pytest.raises(ValueError, match="env is NULL"):
+        _lib.pob.step(0, 4, 0, 0, 0, 0, 0, 0)
+    with pytest.raises(ValueError, match="env is NULL"):
+        _lib.pob.reset(0, 4, 0, 0, 0)
+    with pytest.raises(ValueError, match="env is NULL"):
+        _lib.pob.reset_where_done_shard(0, 4, 4, 0, 0, 0, 0, 0, 0)
