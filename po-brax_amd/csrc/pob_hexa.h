@@ -74,6 +74,9 @@ __host__ __device__ constexpr int hex_max_walls(int kind) {
 #ifndef POB_HEX_VWALLS
 #define POB_HEX_VWALLS 1
 #endif
+#ifndef POB_HEX_BF_WALL  // branch-free wall-end search step (qwall_end_bf)
+#define POB_HEX_BF_WALL 0
+#endif
 #define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
 #define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls
 #define HW_FLOATS (4 * POB_MAXW + 5)
@@ -166,9 +169,18 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWal
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
       const bool on = ((m >> w) & 1u) != 0u;
+#ifdef POB_EXP_NO_ANY_WALL  // experiment: every wall row evaluated, no per-wall wave branch
+      if (true) {
+#else
       if (__any(on)) {
+#endif
+#if POB_HEX_BF_WALL
+        qwall_end_bf(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
+        qwall_end_bf(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
+#else
         qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
         qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
+#endif
       }
     }
   }
@@ -180,9 +192,26 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWal
 }
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
+// timing experiment only (POB_EXP_TIMING_SUB): shader-clock durations of the substep's
+// phases summed into tacc[0..3] (accel + kinetic, joint, contact detect + position, velocity)
+#ifdef POB_EXP_TIMING_SUB
+#define HSUB_T(i)                                                  \
+  {                                                                \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();   \
+    if (tacc) tacc[i] += _t - _tl;                                 \
+    _tl = _t;                                                      \
+  }
+#else
+#define HSUB_T(i)
+#endif
 template <int MW, class G>
 POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, HBody &b,
-                        const float act, v3 &cv, v3 &ca, const bool COLLIDE) {
+                        const float act, v3 &cv, v3 &ca, const bool COLLIDE, unsigned long long *tacc = nullptr) {
+#ifdef POB_EXP_TIMING_SUB
+  unsigned long long _tl = __builtin_amdgcn_s_memtime();
+#else
+  (void)tacc;
+#endif
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
   const bool torso = isP && hip, leg = !isP && !hip;
 #if POB_HEX_VWALLS
@@ -223,6 +252,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
     b.q = g.qnorm(q);
   }
+  HSUB_T(0)
   // 3. position projection
   HContacts ct;
   {
@@ -280,6 +310,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
       DX = torso ? dxt : (leg ? dxl : dxa);
       DA = torso ? dat : (leg ? dal : daa);
     }
+    HSUB_T(1)
     if (COLLIDE) {
       hdetect<MW>(g, S, HT, WT, HW, b, ct);
 #ifdef POB_EXP_NO_WALL_RESPONSE  // timing experiment only: detection kept, no wall response
@@ -293,6 +324,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     b.x = vadd(b.x, DX);
     qadd_half(b.q, qmul_vq(DA, b.q), 1.0f);
   }
+  HSUB_T(2)
   // 4. velocity projection
   b.q = g.qnorm(b.q);
   b.v = vscl(vsub(b.x, px), S.inv_h);
@@ -317,4 +349,5 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     cv = vadd(cv, dV);
     ca = vadd(ca, dW);
   }
+  HSUB_T(3)
 }

@@ -1549,6 +1549,10 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, false);                  \
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, true);                   \
   }
+#elif defined(POB_EXP_TIMING_SUB)  // timing experiment only: phase durations into stamps 5..8
+#define HEX_SUBSTEPS(G)                                                                       \
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
 #else
 #define HEX_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
