@@ -91,6 +91,9 @@ def main() -> int:
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 ('nccl' = RCCL; 'gloo' lets several ranks share "
                          "one GPU for a functional rehearsal, not a measurement)")
+    ap.add_argument("--policy-mlp", type=int, default=0, metavar="H",
+                    help="time the RL unroll instead: a 2-layer tanh MLP (hidden H) policy and the step, "
+                         "captured together per step (rollout.PolicyRollout); not the headline workload")
     ap.add_argument("--groups", type=int, default=1,
                     help="graph rollout: env groups stepped on their own streams (rollout.GraphRollout)")
     ap.add_argument("--no-graph", action="store_true",
@@ -181,7 +184,20 @@ def main() -> int:
     use_graph = not args.no_graph and not do_gather and pre and (gym is None or world == 1) and \
         (gym is None or args.steps % 2 == 0)
     roll = None
-    if use_graph:  # capture the K timed steps (capture does not run them)
+    if args.policy_mlp:
+        if gym is not None or args.env == "mixed" or do_gather:
+            ap.error("--policy-mlp runs the create() chain of one env kind")
+        from po_brax_amd.rollout import PolicyRollout
+        gen = torch.Generator(device=dev).manual_seed(0)
+        D, H = state.obs.shape[1], args.policy_mlp
+        W1 = torch.randn((D, H), generator=gen, device=dev) * D ** -0.5
+        W2 = torch.randn((H, 8), generator=gen, device=dev) * H ** -0.5
+
+        def policy(obs):
+            return torch.tanh(torch.tanh(obs @ W1) @ W2)
+
+        roll = PolicyRollout(env, state, policy, args.steps)
+    elif use_graph:  # capture the K timed steps (capture does not run them)
         from po_brax_amd.rollout import GraphRollout, GymGraphRollout
         if gym is not None:
             roll = GymGraphRollout(gym, acts[args.warmup:args.warmup + args.steps])
@@ -220,13 +236,14 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    if roll is not None and gym is None:  # untimed: per-step kernel durations for the roofline
+    if roll is not None and gym is None and not args.policy_mlp:  # untimed: per-step kernel durations
         for k in range(args.steps):
             ev_a[k].record()
             one_step(args.warmup + k)
             ev_b[k].record()
         torch.cuda.synchronize()
-    per = [ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)] if roll is None or gym is None else []
+    per = ([ev_a[k].elapsed_time(ev_b[k]) for k in range(args.steps)]
+           if roll is None or (gym is None and not args.policy_mlp) else [])
     eager_ms = sum(per) / len(per) if per else float("nan")
     # the dominant kernel's time per launch: from the graph replay (back-to-back launches, no
     # host gaps) when there is one -- an eager step's event pair also holds the host's launch
@@ -268,7 +285,8 @@ def main() -> int:
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TF, "unit": "TFLOP/s",
         "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
-        "kernel": kname + (" + gym any-done + k_reset(where done)" if gym is not None else ""),
+        "kernel": kname + (" + gym any-done + k_reset(where done)" if gym is not None else "")
+                  + (" + policy MLP GEMMs (per-step replay time, not the step kernel alone)" if args.policy_mlp else ""),
         "kernel_ms": round(kern_ms, 4), "units_per_launch": B,
         "kernel_ms_source": "hipGraph replay of the K timed steps / K" if roll is not None
                             else "HIP events around each eager step",
@@ -307,8 +325,10 @@ def main() -> int:
 
     par = f"env-shard x{world}" + (" (strong: global batch split)" if strong else " (weak: batch per GPU)")
     line = {
-        "metric": HEADLINE_METRIC if (args.env == "ant_heavenhell" and strong and total == 65536 and gym is None)
-                  else f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU"),
+        "metric": HEADLINE_METRIC if (args.env == "ant_heavenhell" and strong and total == 65536 and gym is None
+                                      and not args.policy_mlp)
+                  else f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU")
+                  + (f" with a {args.policy_mlp}-hidden MLP policy in the loop" if args.policy_mlp else ""),
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -318,7 +338,9 @@ def main() -> int:
                                + f", episode_length {args.episode_length}, PBD 10 substeps, random "
                                "uniform(-1,1) actions (threefry)"
                                + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else "")
-                               + (", RCCL obs all-gather per step" if do_gather else ""),
+                               + (", RCCL obs all-gather per step" if do_gather else "")
+                               + (f", MLP policy (D x {args.policy_mlp} x 8, tanh) per step in the same graph"
+                                  if args.policy_mlp else ""),
                    "env": args.env, "global_batch": total, "batch_per_gpu": B,
                    "episode_length": args.episode_length, "qp_storage": args.qp_dtype, "parallelism": par,
                    "path": "gym" if gym is not None else "brax",

@@ -172,3 +172,56 @@ class GymGraphRollout:
         self.graph.replay()
         s = self.gym._state
         return s.obs, s.reward, s.done, s.metrics
+
+
+class PolicyRollout:
+    """``T`` env-steps with the policy in the loop, replayed from ONE hipGraph: per step
+    ``action = policy(obs)`` (any torch ops -- an MLP on hipBLASLt, sampling with a device
+    generator -- static shapes, no host sync) then the fused step kernel, and the trajectory
+    written to device buffers.  This is the MI355X counterpart of the reference's training-side
+    ``jax.lax.scan`` over (policy, ``env.step``): one replay runs the whole unroll with no
+    per-step host work.
+
+        roll = PolicyRollout(env, state, policy, steps=T)
+        roll.replay()        # T steps, in place on ``state``
+        roll.obs[t]          # (B, D) observation the policy acted on at step t
+        roll.actions[t], roll.reward[t], roll.done[t]   # its action, then the step's reward / done
+
+    ``done`` is float32 (the engine's done; AntTag's public bool done is ``done != 0``).  The
+    capture is preceded by ``warmup`` eager policy calls on a side stream (library handles and
+    workspaces must exist before a capture); they do not step the env."""
+
+    def __init__(self, env, state, policy, steps: int, warmup: int = 2):
+        if steps <= 0:
+            raise ValueError("steps must be positive")
+        self.env, self.state, self.policy, self.steps = env, state, policy, int(steps)
+        obs = state.obs
+        dev = obs.device
+        B, D = int(obs.shape[0]), int(obs.shape[1])
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, int(warmup))):
+                a = policy(obs)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        if not (isinstance(a, torch.Tensor) and a.shape == (B, env.action_size) and a.is_cuda):
+            raise ValueError(f"policy must map obs (B, D) to a (B, {env.action_size}) device tensor")
+        T = self.steps
+        self.obs = torch.empty((T, B, D), dtype=obs.dtype, device=dev)
+        self.actions = torch.empty((T, B, env.action_size), dtype=torch.float32, device=dev)
+        self.reward = torch.empty((T, B), dtype=torch.float32, device=dev)
+        self.done = torch.empty((T, B), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with no_gc(), torch.cuda.graph(self.graph):
+            for t in range(T):
+                self.obs[t].copy_(self.state.obs)
+                self.actions[t].copy_(policy(self.state.obs))
+                self.state = env.step_(self.state, self.actions[t])
+                self.reward[t].copy_(self.state.reward)
+                self.done[t].copy_(self.state.aux["done"] if "done" in self.state.aux else self.state.done)
+
+    def replay(self):
+        """Run the captured unroll (stream-ordered on torch's current stream)."""
+        self.graph.replay()
+        return self.state

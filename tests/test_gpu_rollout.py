@@ -152,3 +152,43 @@ def test_gym_graph_rollout_equals_eager(name):
         assert torch.equal(g1._key, g2._key), rep
         for k in m1:
             assert torch.equal(m1[k], m2[k]), (rep, k)
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_tag"])
+def test_policy_rollout_equals_eager(name):
+    """rollout.PolicyRollout: an MLP policy (hipBLASLt GEMMs + tanh) and the fused step
+    captured together per step, replayed from one graph, equal the same loop run eagerly --
+    observations, actions, rewards, dones and the final state, bit for bit, over episodes
+    short enough to autoreset inside the unroll; a second replay continues from the first."""
+    from po_brax_amd import envs
+    from po_brax_amd.rollout import PolicyRollout
+    B, T = 512, 7
+    keys = torch.from_numpy(_keys(B, 21)).cuda()
+    e1, e2 = (envs.create(name, batch_size=B, episode_length=4) for _ in range(2))
+    s1, s2 = e1.reset(keys), e2.reset(keys)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    D = e1.observation_size
+    W1 = torch.randn((D, 64), generator=g, device="cuda") * 0.1
+    W2 = torch.randn((64, 8), generator=g, device="cuda") * 0.3
+
+    def policy(obs):
+        return torch.tanh(torch.tanh(obs @ W1) @ W2)
+
+    roll = PolicyRollout(e2, s2, policy, T)
+    for rep in range(2):
+        obs_l, act_l, rew_l, done_l = [], [], [], []
+        for t in range(T):
+            obs_l.append(s1.obs.clone())
+            a = policy(s1.obs)
+            act_l.append(a)
+            s1 = e1.step_(s1, a)
+            rew_l.append(s1.reward.clone())
+            done_l.append(s1.aux["done"].clone())
+        s2 = roll.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(torch.stack(obs_l), roll.obs), rep
+        assert torch.equal(torch.stack(act_l), roll.actions), rep
+        assert torch.equal(torch.stack(rew_l), roll.reward) and torch.equal(torch.stack(done_l), roll.done), rep
+        for f in ("pos", "rot", "vel", "ang"):
+            assert torch.equal(getattr(s1.qp, f), getattr(s2.qp, f)), (rep, f)
+    assert float(roll.done.sum()) > 0  # autoresets happened inside the unroll
