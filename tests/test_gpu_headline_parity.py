@@ -216,3 +216,65 @@ def test_out_of_range_inputs_take_exact_fallbacks(monkeypatch, lanes, B, gacc):
             so = o.step(_state_np(s), act, flags=FLAGS, episode_length=1000, nthreads=NT)
             s = env.step(s, torch.from_numpy(act).cuda())
             compare_states(s, so, f"{name} B={B} lanes={lanes} step {t}")
+
+
+def test_config4_tag_shard_equals_slice_of_full_batch():
+    """BASELINE config 4 at full size: AntTag, global batch 65 536 over 8 ranks.  Rank 5's
+    shard (8 192 envs: the sixteen-lane kernel) stepped from its own rows of the global reset
+    keys and actions equals rows [40 960, 49 152) of the whole batch stepped on one GPU (the
+    four-lane kernel), bit for bit -- the index-sharding property bench.py's strong-scaling
+    runs rely on, across the kernel switch."""
+    from po_brax_amd import envs, jumpy
+    from po_brax_amd.sharding import shard_keys, shard_range
+    total, world, rank, T = 65536, 8, 5, 8
+    lo, hi = shard_range(total, world, rank)
+    key = jumpy.random_prngkey(0)
+    full = envs.create("ant_tag", batch_size=total, episode_length=4)
+    part = envs.create("ant_tag", batch_size=hi - lo, episode_length=4)
+    sf = full.reset(shard_keys(key, total, 1, 0))
+    sp = part.reset(shard_keys(key, total, world, rank))
+    k1, k2 = key.clone(), key.clone()
+    af = torch.empty((total, 8), device="cuda")
+    ap = torch.empty((hi - lo, 8), device="cuda")
+    for t in range(T):
+        jumpy.random_actions_(k1, total, 0, af)
+        jumpy.random_actions_(k2, total, lo, ap)
+        sf = full.step_(sf, af)
+        sp = part.step_(sp, ap)
+    torch.cuda.synchronize()
+    for f in ("pos", "rot", "vel", "ang"):
+        assert torch.equal(getattr(sf.qp, f)[lo:hi], getattr(sp.qp, f)), f
+    assert torch.equal(sf.obs[lo:hi], sp.obs) and torch.equal(sf.done[lo:hi], sp.done)
+    assert torch.equal(sf.info["rng"][lo:hi], sp.info["rng"])
+    assert bool(sf.done.all())  # step 8 of 4-step episodes: the time limit (after one autoreset)
+
+
+def test_config5_mixed_fp16_full_global_batch_properties():
+    """BASELINE config 5 at its full global batch on one GPU: HH + GA + TAG mixed in one
+    launch per step, 262 144 envs, binary16 qp storage, autoreset: every output finite, the
+    dynamic bodies' quaternions unit within binary16 rounding, the reference's dtypes (TAG
+    bool done, GA int32 counts), rewards from each task's set, and episodes ending at the
+    run's last step (every env reaches the time limit)."""
+    from po_brax_amd import envs, jumpy
+    total, T = 262144, 5
+    names = ["ant_heavenhell", "ant_gather", "ant_tag"]
+    sizes = [total // 3 + (1 if i < total % 3 else 0) for i in range(3)]
+    m = envs.create_mixed(names, episode_length=5, qp_dtype=torch.float16)
+    key = jumpy.random_prngkey(3)
+    s = m.reset(key, sizes)
+    act = torch.empty((total, 8), device="cuda")
+    for t in range(T):
+        jumpy.random_actions_(key, total, 0, act)
+        s = m.step_(s, act)
+    torch.cuda.synchronize()
+    rsets = {"ant_heavenhell": {-2.0, -1.0, 0.0, 1.0}, "ant_gather": {-10.0, -1.0, 0.0, 1.0},
+             "ant_tag": {-1.0, 0.0, 1.0}}
+    for name, st in zip(names, s):
+        assert st.qp.pos.dtype == torch.float16
+        assert torch.isfinite(st.obs).all() and torch.isfinite(st.qp.pos.float()).all(), name
+        qn = st.qp.rot[:, :9].float().norm(dim=-1)
+        assert torch.allclose(qn, torch.ones_like(qn), atol=2e-3), name
+        assert set(torch.unique(st.reward).tolist()) <= rsets[name], name
+        assert bool((st.info["steps"] <= 5).all()), name
+    assert s[2].done.dtype == torch.bool and s[1].metrics["apples"].dtype == torch.int32
+    assert all(bool((st.aux["done"] != 0).all()) for st in s)  # step 5 of 5: the time limit
