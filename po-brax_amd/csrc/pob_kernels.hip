@@ -826,6 +826,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
+    const float fric = quad_friction(S);
     if (LEG) {
       // legacy spring dynamics: every substep kinetic + springs + contact impulses
 #pragma nounroll
@@ -833,9 +834,9 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     } else {
 #pragma nounroll
 #if defined(POB_EXP_NO_COLLIDE)
-    for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false, S.friction);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
-    for (int it = 0; it < 0 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false, S.friction);  // timing experiment only
 #else
     for (int it = 0; it < 2 * iters; ++it) {
       // Issue priority falls with progress, so a SIMD's four waves (one per block) advance
@@ -848,7 +849,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
       else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
-      qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0);
+      qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);
     }
 #endif
     }
@@ -2029,7 +2030,7 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { R.cv[l] = V(0.0f, 0.0f, 0.0f); R.ca[l] = V(0.0f, 0.0f, 0.0f); }
   if (S.legacy) qlegacy_contacts(Sp, LT, b, ct, R.cv, R.ca);  // legacy sys.info: the colliders' impulses
-  else qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca);
+  else qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca, S.friction);
 #ifdef POB_EXP_TIMING
   R.ts[3] = __builtin_amdgcn_s_memtime();
 #endif

@@ -296,7 +296,7 @@ POB_D void qcontact_geom(csys_t &S, const float *LT, const QContacts &ct, int c,
 
 // contact processing order of one body = oracle order (ground contact first, then wall)
 POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const Lds &L, const QContacts &ct,
-                             v3 (&DX)[QNB], v3 (&DA)[QNB]) {
+                             v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
 #pragma unroll
   for (int c = 0; c < 2 + QNB; ++c) {
     POB_FENCE();
@@ -327,7 +327,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
           const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
           const float wt = im + vdot(ctn, ctn);
           const float lamt = POB_DIV(lt, wt);
-          if (lamt < S.friction * lam) {
+          if (lamt < fric * lam) {
             const float px = tx * -lamt, py = ty * -lamt;
             DX[l].x = FMA(px, im, DX[l].x);
             DX[l].y = FMA(py, im, DX[l].y);
@@ -354,7 +354,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
         v3 ctn = vcross(rr, t);
         float wt = im + vdot(ctn, ctn);
         float lamt = POB_DIV(lt, wt);
-        if (lamt < S.friction * lam) {
+        if (lamt < fric * lam) {
           v3 Pt = vscl(t, -lamt);
           DX[l] = vfma(Pt, im, DX[l]);
           DA[l] = vadd(DA[l], vcross(rr, Pt));
@@ -365,7 +365,7 @@ POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const 
 }
 
 POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const QContacts &ct, v3 (&dV)[QNB],
-                             v3 (&dW)[QNB]) {
+                             v3 (&dW)[QNB], const float fric) {
 #pragma unroll
   for (int c = 0; c < 2 + QNB; ++c) {
     POB_FENCE();
@@ -388,7 +388,7 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
         float lt, ilt;
         pob_sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
         if (lt > 0.0f) {
-          const float fr = fminf(S.friction * pen * S.inv_h, lt);
+          const float fr = fminf(fric * pen * S.inv_h, lt);
           const float k = -(fr * ilt);
           dv = V(vr.x * k, vr.y * k, 0.0f);
         }
@@ -399,7 +399,7 @@ POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const 
         float lt, ilt;
         pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
         if (lt > 0.0f) {
-          float fr = fminf(S.friction * pen * S.inv_h, lt);
+          float fr = fminf(fric * pen * S.inv_h, lt);
           dv = vscl(vt, -(fr * ilt));
         }
         if (vn < 0.0f) dv = vfma(n, -vn, dv);
@@ -495,10 +495,25 @@ POB_D void qtorso_add(v3 &dx, v3 &da, const QTorso &t, const float imp0) {
   da = vadd(da, quad_bcast3<J>(t.t));
 }
 
+// The friction coefficient for the substep loop (POB_QFRIC_REG, default on): read once and
+// passed through an empty asm, so the compiler holds it in a register instead of
+// re-issuing a scalar load of pob_sys::friction at each of the ten contact sites of every
+// collide substep (and waiting for it).
+#ifndef POB_QFRIC_REG
+#define POB_QFRIC_REG 1
+#endif
+POB_D float quad_friction(const csys_t &S) {
+  float f = S.friction;
+#if POB_QFRIC_REG
+  asm volatile("" : "+s"(f));
+#endif
+  return f;
+}
+
 // One XPBD substep on a lane quad (see the header comment for the split).
 template <bool WALLS>
 POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const Lds &L,
-                        const bool COLLIDE) {
+                        const bool COLLIDE, const float fric) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
   // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
@@ -571,7 +586,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     }
     if (COLLIDE) {
       qdetect<WALLS>(Sp, LT, WT, b, ct);
-      qcontact_position(Sp, LT, b, L, ct, DX, DA);
+      qcontact_position(Sp, LT, b, L, ct, DX, DA, fric);
     }
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
@@ -596,7 +611,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontact_velocity(Sp, LT, b, ct, dV, dW);
+    qcontact_velocity(Sp, LT, b, ct, dV, dW, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
