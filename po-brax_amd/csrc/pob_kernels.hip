@@ -277,6 +277,7 @@ struct TaskOut {
   // round trip after the substeps, on the wave's critical path
   bool tp_ok;
   float tp[6];
+  float pdone;  // the input done (sixteen-lane kernel: loaded before the physics)
 };
 
 // the task bodies' xy (TaskOut::tp) of env row r3
@@ -1485,6 +1486,9 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
       gop_ok = true;
     }
   }
+  // the action, loaded with the state (its round trip overlaps the table loads)
+  const float a_in = act_lane ? act[(size_t)b * POB_NJ + jown] : 0.0f;
+  constexpr int HMW = hex_max_walls(KIND);
   // the role table, staged after the state loads are issued (as in the eight-lane kernel)
   {
     const __attribute__((address_space(4))) float *src = &Sp->hex[0][0];
@@ -1505,7 +1509,6 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
 #pragma unroll
   for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
   const float *WT = htab + 16 * HT_FLOATS;
-  constexpr int HMW = hex_max_walls(KIND);
   HWalls<HMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
 #pragma unroll
   for (int w = 0; w < HMW; ++w) {
@@ -1525,17 +1528,17 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   TaskOut t;
   t.tp_ok = false;
   if (act_lane && lane0) {
-    // the task inputs, loaded before the physics so that their round trip overlaps it
-    float steps = in.steps ? in.steps[b] : 0.0f;
-    if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
-    t.steps = steps;
+    // the task inputs, loaded before the physics so that their round trip overlaps it (the
+    // done test that zeroes steps waits for its load, so it runs after the physics)
+    t.steps = in.steps ? in.steps[b] : 0.0f;
+    t.pdone = in.done[b];
     t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
     t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
     task_prefetch<KIND, QT>(in, r3, t);
   }
   if (act_lane) {
     const float xb = bd.x.x;
-    const float a = act[(size_t)b * POB_NJ + jown];
+    const float a = a_in;
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
@@ -1592,6 +1595,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     Ls.set3(0, cvl);
     wave_lds_sync();
     if (lane0) {
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && t.pdone != 0.0f) t.steps = 0.0f;
       t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
       if (KIND == POB_ANT) {
         // contact rows 0..8 = torso, then Aux k (lane 7 - k) and lower leg k (lane 15 - k)
