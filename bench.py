@@ -360,9 +360,10 @@ def main() -> int:
 
 def step_kernel(B: int) -> str:
     """The step kernel pob_step launches for a batch of B envs (pob_kernels.hip pob_step:
-    sixteen lanes per env up to POB_HEXA_MAX_B (8 192), eight up to POB_OCTET_MAX_B (16 384),
-    four above)."""
-    if B <= int(os.environ.get("POB_HEXA_MAX_B", "8192")):
+    sixteen lanes per env up to POB_HEXA_MAX_B (16 x the CU count: 4 096 on MI355X), eight up
+    to POB_OCTET_MAX_B (16 384), four above)."""
+    n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    if B <= int(os.environ.get("POB_HEXA_MAX_B", str(16 * n_cu))):
         return "k_step_hex"
     if B <= int(os.environ.get("POB_OCTET_MAX_B", "16384")):
         return "k_step_oct"

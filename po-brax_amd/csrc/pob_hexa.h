@@ -193,7 +193,8 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWal
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
 // timing experiment only (POB_EXP_TIMING_SUB): shader-clock durations of the substep's
-// phases summed into tacc[0..3] (accel + kinetic, joint, contact detect + position, velocity)
+// phases summed into tacc[0..7] (accel + kinetic, joint, contact position (wall response), velocity
+// contacts (wall), contact detection, ground position, velocity projection, ground velocity)
 #ifdef POB_EXP_TIMING_SUB
 #define HSUB_T(i)                                                  \
   {                                                                \
@@ -313,12 +314,14 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     HSUB_T(1)
     if (COLLIDE) {
       hdetect<MW>(g, S, HT, WT, HW, b, ct);
+      HSUB_T(4)
 #ifdef POB_EXP_NO_WALL_RESPONSE  // timing experiment only: detection kept, no wall response
       asm volatile("" ::"v"(ct.pen), "v"(ct.n.x), "v"(ct.n.y), "v"(ct.n.z), "v"(ct.pe.x), "v"(ct.pe.y), "v"(ct.pe.z));
       ct.pen = -1.0f;
 #endif
       const float im = HT[HT_IM];
       if (ct.gpen > 0.0f) oground_position(g, SC, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
+      HSUB_T(5)
       if (ct.pen > 0.0f) owall_position(g, SC, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
     }
     b.x = vadd(b.x, DX);
@@ -334,12 +337,14 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     const float kw = dq.w >= 0.0f ? k2 : -k2;
     b.w = V(dq.x * kw, dq.y * kw, dq.z * kw);
   }
+  HSUB_T(6)
   // 5. velocity-level contacts (ground first, then wall: the oracle's per-body order)
   if (COLLIDE) {
     v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
     const float im = HT[HT_IM];
     if (ct.gpen > 0.0f)
       ocontact_vel_one(g, SC, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+    HSUB_T(7)
     if (ct.pen > 0.0f) {
       const v3 e0 = HTV(HT, HT_E0);
       const v3 e = ct.sel ? V(-e0.x, -e0.y, -e0.z) : e0;

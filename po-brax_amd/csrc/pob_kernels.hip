@@ -660,7 +660,11 @@ POB_D void stage_leg_table(csys_t *Sp, float *legtab) {
 #ifdef POB_EXP_TIMING
 #define POB_TS_WAVES 65536
 // per wave: hw id, xcc id, then POB_TS_N stamps (unset stamps are 0)
+#ifdef POB_EXP_TIMING_SUB
+#define POB_TS_N 16  // + the substep phase sums in stamps 5..12
+#else
 #define POB_TS_N 10
+#endif
 #define POB_TS_ROW (POB_TS_N + 4)  // + the wave's start / end on the device-wide 100 MHz clock
 __device__ unsigned long long pob_ts_buf[POB_TS_WAVES * POB_TS_ROW];  // timing experiment only
 #define POB_TS_DECL() \
@@ -1553,7 +1557,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, false);                  \
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, true);                   \
   }
-#elif defined(POB_EXP_TIMING_SUB)  // timing experiment only: phase durations into stamps 5..8
+#elif defined(POB_EXP_TIMING_SUB)  // timing experiment only: phase durations into stamps 5..12
 #define HEX_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
@@ -2427,10 +2431,17 @@ static int octet_max_batch() {
   const char *e = getenv("POB_OCTET_MAX_B");
   return e ? atoi(e) : 16384;
 }
-// sixteen lanes per env up to this batch (POB_HEXA_MAX_B overrides; 0 disables)
-static int hexa_max_batch() {
+// sixteen lanes per env while its waves fit one per SIMD: B <= 4 envs x 4 SIMDs x n_cu (4 096
+// on 256 CUs; POB_HEXA_MAX_B overrides; 0 disables).  At two waves per SIMD the eight-lane
+// kernel (one wave per SIMD up to B = 8 192) is faster: interleaved A/B, kernel ms
+// (profiles/r3k/kernel_select.txt)
+//                B:  5 120           6 144           7 168           8 192
+//   HH  hex / oct:   0.0371/0.0366   0.0379/0.0365   0.0384/0.0372   0.0388/0.0373
+//   TAG hex / oct:   0.0358/0.0346   0.0376/0.0348   0.0369/0.0350   0.0372/0.0354
+// while at B = 4 096 the sixteen-lane kernel is 19 % faster (HH 0.0295 / 0.0363).
+static int hexa_max_batch(int n_cu) {
   const char *e = getenv("POB_HEXA_MAX_B");
-  return e ? atoi(e) : 8192;
+  return e ? atoi(e) : 16 * n_cu;
 }
 template <typename QT, bool GACC>
 static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
@@ -2443,10 +2454,11 @@ static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, c
     default: hipLaunchKernelGGL((k_step_hex<POB_ANT, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
 }
-// Up to one wave per SIMD (B <= the SIMD count x 4 envs) the wave's dependency chain is the
-// step time and the guard branches split it (GuardAcc, measured HH B=4 096 -3.5 %); with two
-// or more waves per SIMD the other wave hides them and the accumulator's VALU operations cost
-// (B = 8 192: TAG / GA +1 %), so the branch guards stay.  POB_HEX_GACC=0/1 forces either.
+// Up to one wave per SIMD (B <= the SIMD count x 4 envs: the default batch range of this
+// kernel) the wave's dependency chain is the step time and the guard branches split it
+// (GuardAcc, measured HH B=4 096 -3.5 %); with two or more waves per SIMD (a POB_HEXA_MAX_B
+// override) the other wave hides them and the accumulator's VALU operations cost (B = 8 192:
+// TAG / GA +1 %), so the branch guards stay.  POB_HEX_GACC=0/1 forces either.
 template <typename QT>
 static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
@@ -2638,7 +2650,7 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch() &&  // legacy: lane quads only
+  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch(e->n_cu) &&  // legacy: lane quads only
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);
   const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch() &&
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);

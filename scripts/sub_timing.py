@@ -1,9 +1,10 @@
 """Per-phase substep durations of the sixteen-lane kernel (timing experiment, not a test).
 
-Needs a library built with -DPOB_EXP_TIMING -DPOB_EXP_TIMING_SUB (POB_LIB=...): stamps 5..8 of
+Needs a library built with -DPOB_EXP_TIMING -DPOB_EXP_TIMING_SUB (POB_LIB=...): stamps 5..12 of
 each wave's row hold the shader-clock durations of the step's substep phases summed over its
-ten substeps (accel + kinetic, joint projection, contact detection + position, velocity
-projection + velocity-level contacts).  argv: B (<= 8192), env name."""
+ten substeps (accel + kinetic, joint projection, wall-contact position + the state update,
+wall-contact velocity, contact detection, ground-contact position, velocity projection,
+ground-contact velocity).  argv: B (<= 8192), env name."""
 import ctypes as C
 import os
 import sys
@@ -25,15 +26,17 @@ for _ in range(20):
     s = env.step_(s, act)
 torch.cuda.synchronize()
 W = (B * 16 + 63) // 64
-NTS = 10
+NTS = 16  # POB_TS_N of a POB_EXP_TIMING_SUB build
 buf = np.zeros((W, NTS + 4), np.uint64)
 f = _lib.lib.pob_debug_timing
 f.argtypes = [C.c_void_p, C.c_int]
 assert f(buf.ctypes.data, W) == 0
 t = buf[:, 2:2 + NTS].astype(np.int64)
-tot = t[:, 9] - t[:, 0]
+tot = t[:, NTS - 1] - t[:, 0]
 print(f"{NAME} B={B} waves={W}: wave ticks p50 {np.median(tot):.0f} max {tot.max()}")
 phys = t[:, 2] - t[:, 1]
 print(f"physics (stamp 1->2) p50 {np.median(phys):.0f}")
-for i, n in zip(range(5, 9), ("accel+kinetic", "joint", "contact detect+position", "velocity+contact vel")):
+names = ("accel+kinetic", "joint", "wall position+update", "wall contact vel", "contact detect",
+         "ground position", "velocity projection", "ground contact vel")
+for i, n in zip(range(5, 13), names):
     print(f"{n:26s} p50 {np.median(t[:, i]):8.0f}  p90 {np.percentile(t[:, i], 90):8.0f}  max {t[:, i].max():8.0f}")

@@ -1,6 +1,7 @@
 """GPU parity at the BASELINE.json batch sizes, on the launch paths the bench takes.
 
-``pob_step`` runs the sixteen-lanes-per-env kernel (``k_step_hex``) for B <= 8 192, the
+``pob_step`` runs the sixteen-lanes-per-env kernel (``k_step_hex``) while its waves fit one
+per SIMD (B <= 16 x the CU count: 4 096 on MI355X; ``POB_HEXA_MAX_B`` overrides), the
 eight-lane kernel (``k_step_oct``) for B <= 16 384 and the four-lane kernel (``k_step_quad``)
 above -- with one-wave (64-thread) blocks when the smaller-batch kernels are disabled
 (``POB_HEXA_MAX_B=0``, ``POB_OCTET_MAX_B=0``) and B <= 4 096, 256-thread blocks otherwise; the
@@ -89,9 +90,17 @@ def test_per_step_parity_eight_lane_small(monkeypatch, B):
 
 
 @pytest.mark.parametrize("name,B", [("ant_heavenhell", 8192), ("ant_tag", 8192), ("ant_gather", 8191), ("ant", 8190)])
-def test_per_step_parity_sixteen_lane(name, B):
-    """The sixteen-lane kernel at its largest batches (config 4's per-GPU TAG batch)."""
+def test_per_step_parity_sixteen_lane(monkeypatch, name, B):
+    """The sixteen-lane kernel at two waves per SIMD (config 4's per-GPU TAG batch; selected
+    by POB_HEXA_MAX_B, the default launches the eight-lane kernel there)."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "8192")
     _per_step(name, B, seed=5)
+
+
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 8192), ("ant_tag", 8192), ("ant_gather", 8191)])
+def test_per_step_parity_eight_lane_default(name, B):
+    """The eight-lane kernel at config 4's per-GPU batch (the default launch there)."""
+    _per_step(name, B, seed=6)
 
 
 def _prefix_identical(Ba, Bb, env_a=None, env_b=None):
@@ -120,8 +129,17 @@ def test_octet_quad_switch_prefix_identical():
 
 
 def test_hexa_octet_switch_prefix_identical():
-    """The first 8 192 envs of a B = 8 193 run (eight-lane kernel) equal a B = 8 192 run
-    (sixteen-lane kernel) bit for bit, fp32 and fp16 storage, for every kind."""
+    """At the default switch (16 x the CU count): the first n envs of a B = n + 1 run
+    (eight-lane kernel) equal a B = n run (sixteen-lane kernel) bit for bit, fp32 and fp16
+    storage, for every kind."""
+    n = 16 * torch.cuda.get_device_properties(0).multi_processor_count
+    _prefix_identical(n, n + 1)
+
+
+def test_hexa_octet_switch_prefix_identical_8192(monkeypatch):
+    """The same across an overridden switch (POB_HEXA_MAX_B = 8 192: the sixteen-lane kernel
+    at two waves per SIMD against the eight-lane kernel at B = 8 193)."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "8192")
     _prefix_identical(8192, 8193)
 
 
@@ -163,9 +181,14 @@ def test_mixed_fp16_config5_parity():
 
 
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_tag"])
-def test_wall_stress_256_thread_blocks(name):
-    """test_gpu_parity.test_step_parity_against_walls at B = 8 192 (256-thread blocks, four
-    waves sharing the block's LDS wall rows): ants teleported onto the walls."""
+@pytest.mark.parametrize("kernel", ["default", "four_lane"])
+def test_wall_stress_256_thread_blocks(monkeypatch, name, kernel):
+    """test_gpu_parity.test_step_parity_against_walls at B = 8 192: ants teleported onto the
+    walls, on the default launch (the eight-lane kernel) and on the four-lane kernel in
+    256-thread blocks (four waves sharing the block's LDS wall rows)."""
+    if kernel == "four_lane":
+        monkeypatch.setenv("POB_HEXA_MAX_B", "0")
+        monkeypatch.setenv("POB_OCTET_MAX_B", "0")
     B, T = 8192, 4
     env = _envs().create(name, batch_size=B, episode_length=1000)
     s = env.reset(torch.from_numpy(_keys(B, 5)).cuda())
@@ -220,7 +243,7 @@ def test_out_of_range_inputs_take_exact_fallbacks(monkeypatch, lanes, B, gacc):
 
 def test_config4_tag_shard_equals_slice_of_full_batch():
     """BASELINE config 4 at full size: AntTag, global batch 65 536 over 8 ranks.  Rank 5's
-    shard (8 192 envs: the sixteen-lane kernel) stepped from its own rows of the global reset
+    shard (8 192 envs: the eight-lane kernel) stepped from its own rows of the global reset
     keys and actions equals rows [40 960, 49 152) of the whole batch stepped on one GPU (the
     four-lane kernel), bit for bit -- the index-sharding property bench.py's strong-scaling
     runs rely on, across the kernel switch."""
