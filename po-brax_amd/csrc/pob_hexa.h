@@ -66,36 +66,13 @@ __host__ __device__ constexpr int hex_max_walls(int kind) {
   return kind == POB_ANT ? 0 : (kind == POB_HEAVENHELL ? POB_MAXW : 4);
 }
 
-// The walls in registers (POB_HEX_VWALLS, default on): every wall's broadphase box (xy) and
-// row, and the common z extent, loaded once per launch from the LDS table into VGPRs.  Read
-// from the system table instead, they were ~80 scalar values per collide substep -- more than
-// the SGPR budget holds across the substep loop -- so each collide substep re-issued ~20
-// scalar loads and waited for them (SQ_WAIT_ANY was 42 % of a wave's cycles at HH B = 4 096).
+// The walls in registers (POB_HEX_VWALLS, default on; HWalls, pob_octet.h).
 #ifndef POB_HEX_VWALLS
 #define POB_HEX_VWALLS 1
 #endif
 #ifndef POB_HEX_BF_WALL  // branch-free wall-end search step (qwall_end_bf)
 #define POB_HEX_BF_WALL 0
 #endif
-#define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
-#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls
-#define HW_FLOATS (4 * POB_MAXW + 5)
-template <int MW>
-struct HWalls {
-  float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
-  float row[MW > 0 ? MW : 1][POB_WALL_FLOATS];
-  float cz, hz;
-  // the table scalars the compiler re-loaded inside the substep loop for want of SGPRs (one
-  // waited scalar load per joint projection and per contact): kept in VGPRs as well
-  float s_pos, friction;
-  int n_walls;
-};
-// the contact functions' view of the table (oground_position / owall_position /
-// ocontact_vel_one read S.friction and S.inv_h only)
-struct HCon {
-  float friction, inv_h;
-};
-
 struct HBody {
   v3 x, v, w;
   q4 q;

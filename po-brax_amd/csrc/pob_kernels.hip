@@ -1139,7 +1139,7 @@ __global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const M
 // (8 AntGather obs rows of the default 8 + 8 objects, 8 x 211 floats, fit: one obs pass)
 #define POB_OSTAGE_FLOATS (27 * 64)
 static_assert(POB_OSTAGE_FLOATS >= OL_FLOATS * 64, "the octet staging region holds the lanes' LDS slots");
-template <int KIND, typename QT>
+template <int KIND, typename QT, bool GACC>
 __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, const StatePtrs in,
                                                  const float *__restrict__ act, const StatePtrs out,
                                                  const uint32_t flags, const int L) {
@@ -1147,7 +1147,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
   POB_TS(0);
   __shared__ float stg[POB_OSTAGE_FLOATS];
-  __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS];
+  __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS + HW_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
@@ -1217,6 +1217,8 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     }
   }
   (void)NMAX;
+  // the action, loaded with the state (its round trip overlaps the table loads)
+  const float a_in = act_lane ? act[(size_t)b * POB_NJ + jown] : 0.0f;
   // the role table, staged after the state loads are issued (both in flight together; the
   // block is one wave, so an LDS wait orders the table writes before its reads)
   {
@@ -1224,32 +1226,67 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     stage_table<8 * OT_FLOATS>(otab, src, (int)threadIdx.x, 64);
     const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
     stage_table<POB_MAXW * POB_WALL_FLOATS>(otab + 8 * OT_FLOATS, wsrc, (int)threadIdx.x, 64);
+    hwalls_stage(S, otab + OT_TAB_FLOATS, lane);  // the walls' broadphase boxes, z extent, scalars
     wave_lds_sync();
   }
   float OT[OT_FLOATS];  // the lane's role row, in registers (constant indices only)
 #pragma unroll
   for (int i = 0; i < OT_FLOATS; ++i) OT[i] = otab[(isA ? k : 4 + k) * OT_FLOATS + i];
   const float *WT = otab + 8 * OT_FLOATS;
+  constexpr int OMW = hex_max_walls(KIND);
+  HWalls<OMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
+  hwalls_load(otab + OT_TAB_FLOATS, WT, HW);
   POB_TS(1);
 
-  // ---- physics (10 substeps in registers + the lane's LDS slots)
+  // ---- physics (10 substeps in registers)
   float jang = 0.0f, jvel = 0.0f;
   v3 cvl[ONB], cal[ONB];
   TaskOut t;
   t.tp_ok = false;
+  if (act_lane && lane0) {
+    // the task inputs, loaded before the physics so that their round trip overlaps it (the
+    // done test that zeroes steps waits for its load, so it runs after the physics)
+    t.steps = in.steps ? in.steps[b] : 0.0f;
+    t.pdone = in.done[b];
+    t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
+    t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+    task_prefetch<KIND, QT>(in, r3, t);
+  }
   if (act_lane) {
     const float xb = bd.x[0].x;
-    const float a = act[(size_t)b * POB_NJ + jown];
+    const float a = a_in;
 #pragma unroll
     for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = V(0.0f, 0.0f, 0.0f); cal[sl] = V(0.0f, 0.0f, 0.0f); }
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+    GuardBranch gb;
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
-    for (int it = 0; it < 0 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, false);  // timing experiment only
+    GuardBranch gb;
+    for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false);  // timing experiment only
 #else
-#pragma nounroll
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<hex_max_walls(KIND)>(Sp, OT, WT, isA, bd, a, cvl, cal, (it & 1) != 0);
+#define OCT_SUBSTEPS(G)                                                                       \
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
+    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0);
+    if constexpr (!GACC) {
+      GuardBranch gb;
+      OCT_SUBSTEPS(gb)
+    } else {
+      // one wave per SIMD (GACC): the substeps without guard branches (GuardAcc, as in the
+      // sixteen-lane kernel); a wave any of whose lanes met an operand outside the fast forms'
+      // range reruns them from the loaded state with the branch guards
+      const OBody b0 = bd;
+      GuardAcc ga;
+      OCT_SUBSTEPS(ga)
+      if (__builtin_expect(__any(ga.bad()), 0)) {
+        bd = b0;
+#pragma unroll
+        for (int sl = 0; sl < ONB; ++sl) { cvl[sl] = V(0.0f, 0.0f, 0.0f); cal[sl] = V(0.0f, 0.0f, 0.0f); }
+        GuardBranch gb;
+        OCT_SUBSTEPS(gb)
+      }
+    }
+#undef OCT_SUBSTEPS
 #endif
     {  // joint angle / velocity obs of the lane's joint (a3)
       const v3 ap = qrot(OTV(OT, OT_AXIS), bd.q[0]);
@@ -1263,11 +1300,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     for (int sl = 0; sl < ONB; ++sl) Ls.set3(3 * sl, cvl[sl]);
     wave_lds_sync();
     if (lane0) {
-      float steps = in.steps ? in.steps[b] : 0.0f;
-      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
-      t.steps = steps;
-      t.m0 = in.m0 ? in.m0[b] : 0.0f; t.m1 = in.m1 ? in.m1[b] : 0.0f; t.m2 = in.m2 ? in.m2[b] : 0.0f;
-      t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
+      if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && t.pdone != 0.0f) t.steps = 0.0f;
       t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
       if (KIND == POB_ANT) {
         // full action row; contact rows 0..8 = torso, then Aux k (lane A_k slot 1) and lower
@@ -1499,14 +1532,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
     stage_table<16 * HT_FLOATS>(htab, src, (int)threadIdx.x, 64);
     const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
     stage_table<POB_MAXW * POB_WALL_FLOATS>(htab + 16 * HT_FLOATS, wsrc, (int)threadIdx.x, 64);
-    if (lane < HW_FLOATS) {  // the walls' broadphase boxes (xy) and common z extent
-      const int w = lane >> 2, c = lane & 3;
-      const int e = lane - HW_CZ;
-      htab[HT_TAB_FLOATS + lane] =
-          e >= 0 ? (e == 0 ? S.wall_cz : e == 1 ? S.wall_hz : e == 2 ? S.s_pos : e == 3 ? S.friction
-                                                                                : __int_as_float(S.n_walls))
-                 : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
-    }
+    hwalls_stage(S, htab + HT_TAB_FLOATS, lane);  // the walls' broadphase boxes, z extent, scalars
     wave_lds_sync();
   }
   float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
@@ -1514,16 +1540,7 @@ __global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, 
   for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
   const float *WT = htab + 16 * HT_FLOATS;
   HWalls<HMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
-#pragma unroll
-  for (int w = 0; w < HMW; ++w) {
-    const float *bx = htab + HT_TAB_FLOATS + HW_BOX + 4 * w;
-    HW.lx[w] = bx[0]; HW.ly[w] = bx[1]; HW.hx[w] = bx[2]; HW.hy[w] = bx[3];
-#pragma unroll
-    for (int k = 0; k < POB_WALL_FLOATS; ++k) HW.row[w][k] = WT[POB_WALL_FLOATS * w + k];
-  }
-  HW.cz = htab[HT_TAB_FLOATS + HW_CZ]; HW.hz = htab[HT_TAB_FLOATS + HW_CZ + 1];
-  HW.s_pos = htab[HT_TAB_FLOATS + HW_CZ + 2]; HW.friction = htab[HT_TAB_FLOATS + HW_CZ + 3];
-  HW.n_walls = __float_as_int(htab[HT_TAB_FLOATS + HW_CZ + 4]);
+  hwalls_load(htab + HT_TAB_FLOATS, WT, HW);
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
@@ -2467,16 +2484,26 @@ static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, 
   if (acc) launch_step_hex_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
   else launch_step_hex_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
 }
-template <typename QT>
-static void launch_step_oct(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
-                            const StatePtrs &po, uint32_t flags, int L) {
+template <typename QT, bool GACC>
+static void launch_step_oct_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
+                              const StatePtrs &po, uint32_t flags, int L) {
   const dim3 g((unsigned)((B + 7) / 8)), b(64);
   switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_oct<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step_oct<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_TAG: hipLaunchKernelGGL((k_step_oct<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    default: hipLaunchKernelGGL((k_step_oct<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_oct<POB_HEAVENHELL, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_GATHER: hipLaunchKernelGGL((k_step_oct<POB_GATHER, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_TAG: hipLaunchKernelGGL((k_step_oct<POB_TAG, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    default: hipLaunchKernelGGL((k_step_oct<POB_ANT, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
+}
+// As for the sixteen-lane kernel: branch-free guards (GuardAcc) while the waves fit one per
+// SIMD (B <= 8 envs x the SIMD count), the branch guards above.  POB_OCT_GACC=0/1 forces either.
+template <typename QT>
+static void launch_step_oct(int kind, int n_cu, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
+                            const float *act, const StatePtrs &po, uint32_t flags, int L) {
+  const char *f = getenv("POB_OCT_GACC");
+  const bool acc = f ? atoi(f) != 0 : (B + 7) / 8 <= 4 * n_cu;
+  if (acc) launch_step_oct_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
+  else launch_step_oct_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
 }
 template <typename QT>
 static void launch_step_quad(int kind, bool legacy, int n_cu, hipStream_t st, const void *sp, int B,
@@ -2656,8 +2683,8 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);
   if (hex && e->sys.qp_f16) launch_step_hex<__half>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (hex) launch_step_hex<float>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
-  else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
-  else if (oct) launch_step_oct<float>(e->sys.kind, st, sp, B, pi, act, po, flags, episode_length);
+  else if (oct && e->sys.qp_f16) launch_step_oct<__half>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
+  else if (oct) launch_step_oct<float>(e->sys.kind, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else if (e->sys.qp_f16) launch_step_quad<__half>(e->sys.kind, e->sys.legacy, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   else launch_step_quad<float>(e->sys.kind, e->sys.legacy, e->n_cu, st, sp, B, pi, act, po, flags, episode_length);
   return hip_check(hipGetLastError(), "k_step launch");

@@ -81,11 +81,66 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
   p1 = vsub(b.x[s], rv);
 }
 
+// The walls in registers (the eight- and sixteen-lane kernels): every wall's broadphase box
+// (xy) and row, and the common z extent, loaded once per launch from the kernel's LDS table
+// into VGPRs.  Read from the system table instead they were ~80 scalar values per collide
+// substep -- more than the SGPR budget holds across the substep loop -- so each collide
+// substep re-issued ~20 scalar loads and waited for them (SQ_WAIT_ANY was 42 % of a wave's
+// cycles at HH B = 4 096 on the sixteen-lane kernel).
+#define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
+#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls
+#define HW_FLOATS (4 * POB_MAXW + 5)
+template <int MW>
+struct HWalls {
+  float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
+  float row[MW > 0 ? MW : 1][POB_WALL_FLOATS];
+  float cz, hz;
+  // the table scalars the compiler re-loaded inside the substep loop for want of SGPRs (one
+  // waited scalar load per joint projection and per contact): kept in VGPRs as well
+  float s_pos, friction;
+  int n_walls;
+};
+// the contact functions' view of the table (oground_position / owall_position /
+// ocontact_vel_one read S.friction and S.inv_h only)
+struct HCon {
+  float friction, inv_h;
+};
+// Fill the wall table's HW_FLOATS entries (lanes 0 .. HW_FLOATS - 1 of the block's first wave
+// write one each) and, after the caller's LDS sync, read it into registers.
+POB_D void hwalls_stage(csys_t &S, float *tab, const int lane) {
+  if (lane < HW_FLOATS) {
+    const int w = lane >> 2, c = lane & 3;
+    const int e = lane - HW_CZ;
+    tab[lane] = e >= 0 ? (e == 0 ? S.wall_cz : e == 1 ? S.wall_hz : e == 2 ? S.s_pos : e == 3 ? S.friction
+                                                                                  : __int_as_float(S.n_walls))
+                       : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
+  }
+}
+template <int MW>
+POB_D void hwalls_load(const float *tab, const float *WT, HWalls<MW> &HW) {
+#pragma unroll
+  for (int w = 0; w < MW; ++w) {
+    const float *bx = tab + HW_BOX + 4 * w;
+    HW.lx[w] = bx[0]; HW.ly[w] = bx[1]; HW.hx[w] = bx[2]; HW.hy[w] = bx[3];
+#pragma unroll
+    for (int k = 0; k < POB_WALL_FLOATS; ++k) HW.row[w][k] = WT[POB_WALL_FLOATS * w + k];
+  }
+  HW.cz = tab[HW_CZ]; HW.hz = tab[HW_CZ + 1];
+  HW.s_pos = tab[HW_CZ + 2]; HW.friction = tab[HW_CZ + 3];
+  HW.n_walls = __float_as_int(tab[HW_CZ + 4]);
+}
+
 // Contact detection of a collide substep on one lane: the ground contact of its ground
 // body and, per slot, the deepest wall contact over the walls near the lane's two body
-// centres (qdetect's exact per-lane broadphase and d2 pre-cull, wall rows in LDS).
-template <int MW>
-POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslot1, const OBody &b, OContacts &ct) {
+// centres (qdetect's exact per-lane broadphase and d2 pre-cull).  The broadphase boxes, the
+// walls' z extent and the contact scalars come from registers (HWalls); each lane walks its
+// own near-wall mask reading the rows from LDS (WT).  (An unrolled walk over register rows
+// with a wave-uniform guard per wall measured equal or slower: TAG / GA B = 8 192 ±1 %, HH
+// B = 16 384 +5 %.)  Culled pairs have penetration < 0 and the walk keeps the oracle's
+// (wall, end) order with the strict ">", so the deepest contact is unchanged.
+template <int MW, class G>
+POB_D void odetect(G &g, const float *OT, const float *WT, const HWalls<MW> &HW, const bool gslot1, const OBody &b,
+                   OContacts &ct) {
   {
     const v3 xg = vsel3(gslot1, b.x[1], b.x[0]);
     const q4 qg = qsel(gslot1, b.q[1], b.q[0]);
@@ -96,26 +151,20 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
   if (MW > 0) {
     const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
     const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
-    csys_t &S = *OLAUNDER(Sp);
 #ifdef POB_EXP_NO_WALLS
     const int nw = 0;  // timing experiment only
 #else
-    const int nw = S.n_walls;
+    const int nw = HW.n_walls;
 #endif
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
-      // all MW boxes loaded at once, w < nw as a predicate (a runtime loop waited
-      // one scalar-load round trip per wall)
-      const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
-      const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
+      const bool near = (mnx <= HW.hx[w]) & (mxx >= HW.lx[w]) & (mny <= HW.hy[w]) & (mxy >= HW.ly[w]);
       lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
   const bool any_near = MW > 0 && __any(lane_mask != 0u);
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
-    POB_FENCE();
-    csys_t &S = *OLAUNDER(Sp);
     float best = 0.0f;
     v3 bn = V(0.0f, 0.0f, 0.0f);
     bool bsel = false;
@@ -130,8 +179,13 @@ POB_D void odetect(csys_t *Sp, const float *OT, const float *WT, const bool gslo
         const bool on = m != 0u;
         const int w = on ? __builtin_ctz(m) : 0;
         m &= m - 1u;
+        const float *R = WT + POB_WALL_FLOATS * w;
+        const float2 r01 = *reinterpret_cast<const float2 *>(R);
+        const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
+        const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
+        for (int q = 0; q < 2; ++q)
+          qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
       }
     }
     ct.pen[s] = best;
@@ -200,20 +254,19 @@ POB_D void owall_position(G &g, const SS &S, const float pen, const v3 pe, const
 }
 
 // contact processing order of one body = the oracle's: ground contact first, then wall
-POB_D void ocontact_position(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const v3 (&pxs)[ONB],
-                             const q4 (&pqs)[ONB], const OContacts &ct, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
-  GuardBranch gb;
+template <class G>
+POB_D void ocontact_position(G &gd, const HCon &SC, const float *OT, const bool gslot1, const OBody &b,
+                             const v3 (&pxs)[ONB], const q4 (&pqs)[ONB], const OContacts &ct, v3 (&DX)[ONB],
+                             v3 (&DA)[ONB]) {
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
-    POB_FENCE();
-    csys_t &S = *OLAUNDER(Sp);
     const float im = OT[OT_B(s)];
     const q4 pq = pqs[s];
     const v3 px = pxs[s];
     const bool g = (s == 1) == gslot1;  // this slot holds the lane's ground body
-    if (g && ct.gpen > 0.0f) oground_position(gb, S, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+    if (g && ct.gpen > 0.0f) oground_position(gd, SC, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
     if (ct.pen[s] > 0.0f)
-      owall_position(gb, S, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+      owall_position(gd, SC, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
   }
 }
 
@@ -259,22 +312,20 @@ POB_D void ocontact_vel_one(G &g, const SS &S, const bool ground, const float pe
   }
 }
 
-POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, const OBody &b, const OContacts &ct,
-                             v3 (&dV)[ONB], v3 (&dW)[ONB]) {
-  GuardBranch gb;
+template <class G>
+POB_D void ocontact_velocity(G &gd, const HCon &SC, const float *OT, const bool gslot1, const OBody &b,
+                             const OContacts &ct, v3 (&dV)[ONB], v3 (&dW)[ONB]) {
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
-    POB_FENCE();
-    csys_t &S = *OLAUNDER(Sp);
     const float im = OT[OT_B(s)];
     const bool g = (s == 1) == gslot1;
     if (g && ct.gpen > 0.0f)
-      ocontact_vel_one(gb, S, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
+      ocontact_vel_one(gd, SC, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
                        b.w[s], dV[s], dW[s]);
     if (ct.pen[s] > 0.0f) {
       const v3 e0 = OTV(OT, OT_B(s) + 2);
       const v3 e = ct.sel[s] ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(gb, S, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
+      ocontact_vel_one(gd, SC, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
                        dW[s]);
     }
   }
@@ -285,8 +336,8 @@ POB_D void ocontact_velocity(csys_t *Sp, const float *OT, const bool gslot1, con
 struct OJoint {
   v3 P, xp, xc, s;
 };
-POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &J) {
-  csys_t &S = *OLAUNDER(Sp);
+template <class G>
+POB_D void ojoint_position(G &g, csys_t &S, const float s_pos, const float *OT, const OBody &b, OJoint &J) {
   const float imp = OT[OT_B(0)], imc = OT[OT_B(1)];
   const m3 Rp = qmat(b.q[0]), Rc = qmat(b.q[1]);
   // (offsets lie in the body xy-plane for every Ant joint, checked by pob_system.cpp: the
@@ -301,11 +352,11 @@ POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &
   if (L2 > 0.0f) {
     const v3 ep = vcross(rp, d), ec = vcross(rc, d);
     const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
-    const float k = POB_DIV(L2 * S.s_pos, den);
+    const float k = (L2 * s_pos) * g.rcp(den);  // POB_DIV(L2 * s_pos, den)
     J.P = vscl(d, k); J.xp = vscl(ep, k); J.xc = vscl(ec, k);
   }
   const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
-  const float psi = pob_atan2f(vdot(vcross(fp, fc), ap), vdot(fp, fc));
+  const float psi = pob_atan2f_g(g, vdot(vcross(fp, fc), ap), vdot(fp, fc));
   float dl = 0.0f;
   if (psi < OT[OT_LO]) dl = psi - OT[OT_LO];
   else if (psi > OT[OT_HI]) dl = psi - OT[OT_HI];
@@ -317,9 +368,12 @@ POB_D void ojoint_position(csys_t *Sp, const float *OT, const OBody &b, OJoint &
 // (the substep-start poses px / pq and the Info.contact accumulators cv / ca stay in
 // registers: at one or two waves per SIMD there are registers to spare, and an LDS round
 // trip would sit on the lone wave's dependency chain)
-template <int MW>
-POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool isA, OBody &b, const float act,
-                        v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE) {
+// G: the range-guard policy (pob_math.h GuardBranch / GuardAcc); HW: the walls and the
+// loop's table scalars in registers.
+template <int MW, class G>
+POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, OBody &b,
+                        const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE) {
+  const HCon SC{HW.friction, OLAUNDER(Sp)->inv_h};
   v3 px[ONB];
   q4 pq[ONB];
 #pragma unroll
@@ -362,7 +416,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       q4 q = b.q[s];
       q.w = FMA(S.half_h, dq.w, q.w); q.x = FMA(S.half_h, dq.x, q.x);
       q.y = FMA(S.half_h, dq.y, q.y); q.z = FMA(S.half_h, dq.z, q.z);
-      b.q[s] = qnormalize(q);
+      b.q[s] = g.qnorm(q);
     }
   }
   // 3. position projection
@@ -372,7 +426,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
     v3 DX[ONB], DA[ONB];
     POB_FENCE();
     OJoint J;
-    ojoint_position(Sp, OT, b, J);
+    ojoint_position(g, *OLAUNDER(Sp), HW.s_pos, OT, b, J);
     POB_FENCE();
     {
       const float imp = OT[OT_B(0)], imc = OT[OT_B(1)];
@@ -400,8 +454,8 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
       DX[1] = vsel3(isA, dx_aux, dx_leg); DA[1] = vsel3(isA, da_aux, da_leg);
     }
     if (COLLIDE) {
-      odetect<MW>(Sp, OT, WT, gslot1, b, ct);
-      ocontact_position(Sp, OT, gslot1, b, px, pq, ct, DX, DA);
+      odetect<MW>(g, OT, WT, HW, gslot1, b, ct);
+      ocontact_position(g, SC, OT, gslot1, b, px, pq, ct, DX, DA);
     }
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
@@ -413,7 +467,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
     csys_t &S = *OLAUNDER(Sp);
-    b.q[s] = qnormalize(b.q[s]);
+    b.q[s] = g.qnorm(b.q[s]);
     b.v[s] = vscl(vsub(b.x[s], px[s]), S.inv_h);
     q4 dq = qmul(b.q[s], qinv(pq[s]));
     const float k2 = 2.0f * S.inv_h;
@@ -425,7 +479,7 @@ POB_D void opbd_substep(csys_t *Sp, const float *OT, const float *WT, const bool
     v3 dV[ONB], dW[ONB];
 #pragma unroll
     for (int s = 0; s < ONB; ++s) { dV[s] = V(0.0f, 0.0f, 0.0f); dW[s] = V(0.0f, 0.0f, 0.0f); }
-    ocontact_velocity(Sp, OT, gslot1, b, ct, dV, dW);
+    ocontact_velocity(g, SC, OT, gslot1, b, ct, dV, dW);
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);

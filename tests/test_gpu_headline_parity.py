@@ -210,18 +210,18 @@ def test_wall_stress_256_thread_blocks(monkeypatch, name, kernel):
         compare_states(s, so, f"{name} wall B={B} step {t}")
 
 
-@pytest.mark.parametrize("lanes,B,gacc", [(16, 70, "1"), (16, 70, "0"), (8, 9000, None), (4, 70, None)])
+@pytest.mark.parametrize("lanes,B,gacc", [(16, 70, "1"), (16, 70, "0"), (8, 70, "1"), (8, 9000, "0"), (4, 70, None)])
 def test_out_of_range_inputs_take_exact_fallbacks(monkeypatch, lanes, B, gacc):
     """The kernels' fast reciprocal / square root / quaternion normalisation fall back to
     the IEEE forms behind wave-uniform guards (pob_math.h pob_rcp, qnormalize).  States that
     take the fallbacks -- a torso at 1e25 m/s (joint anchors drift beyond 2^96), a zero
     quaternion (normalisation fallback), a 1e30 rad/s spin -- must still match the oracle
     bit for bit (NaN / inf included), in the lanes that hold them and in their neighbours,
-    on the sixteen-, eight- and four-lane kernels.  The sixteen-lane kernel runs both guard
-    policies (pob_math.h GuardAcc: no branches, the wave reruns its substeps under the branch
-    guards when a lane saw an operand out of range; GuardBranch)."""
+    on the sixteen-, eight- and four-lane kernels.  The sixteen- and eight-lane kernels run
+    both guard policies (pob_math.h GuardAcc: no branches, the wave reruns its substeps under
+    the branch guards when a lane saw an operand out of range; GuardBranch)."""
     if gacc is not None:
-        monkeypatch.setenv("POB_HEX_GACC", gacc)
+        monkeypatch.setenv("POB_HEX_GACC" if lanes == 16 else "POB_OCT_GACC", gacc)
     if lanes <= 8:
         monkeypatch.setenv("POB_HEXA_MAX_B", "0")
     if lanes == 4:
