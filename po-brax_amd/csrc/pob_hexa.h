@@ -66,13 +66,6 @@ __host__ __device__ constexpr int hex_max_walls(int kind) {
   return kind == POB_ANT ? 0 : (kind == POB_HEAVENHELL ? POB_MAXW : 4);
 }
 
-// The walls in registers (POB_HEX_VWALLS, default on; HWalls, pob_octet.h).
-#ifndef POB_HEX_VWALLS
-#define POB_HEX_VWALLS 1
-#endif
-#ifndef POB_HEX_BF_WALL  // branch-free wall-end search step (qwall_end_bf)
-#define POB_HEX_BF_WALL 0
-#endif
 struct HBody {
   v3 x, v, w;
   q4 q;
@@ -90,36 +83,26 @@ struct HContacts {
 // deepest wall contact over the walls whose grown box (pob_sys::wall_lo/hi) holds the body
 // centre -- exact: a culled pair has every capsule point farther than r from the wall box,
 // penetration < 0, and the strict ">" of the deepest-contact search keeps the oracle's
-// (wall, end) order.  (Per-body boxes would not shorten the walk: the wave iterates over the
-// most walls any of its lanes is near, a lower leg's.)
+// (wall, end) order.  The boxes, the walls' z extent and the wall count come from registers
+// (HWalls); each lane walks its own near-wall mask in increasing wall order reading the rows
+// from LDS (WT), so the wave runs as many iterations as its busiest lane.  (An unrolled walk
+// over all rows held in registers, each behind a wave-uniform guard, runs the union of the
+// walls near any lane: HH B = 4 096 0.0294 ms against 0.0283 for this walk, TAG / GA +0.5 %.)
 template <int MW, class G>
-POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, const HBody &b,
-                   HContacts &ct) {
+POB_D void hdetect(G &g, const float *HT, const float *WT, const HWalls<MW> &HW, const HBody &b, HContacts &ct) {
   ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
-  // (both wall loops are unrolled over POB_MAXW with wave-uniform guards, so the walls' boxes
-  // and rows are scalar-table constants the compiler keeps in SGPRs: a runtime wall loop
-  // re-loads them each iteration, one scalar-load round trip per wall -- with four envs per
-  // wave the union of the walls near any lane is as short as the longest per-lane walk)
   uint32_t m = 0u;
   if (MW > 0) {
 #ifdef POB_EXP_NO_WALLS
     const int nw = 0;  // timing experiment only
-#elif POB_HEX_VWALLS
-    const int nw = HW.n_walls;
 #else
-    const int nw = S.n_walls;
+    const int nw = HW.n_walls;
 #endif
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
-      // every wall's box is loaded (the table always holds POB_MAXW rows) and w < nw is a
-      // predicate: loads behind a per-wall branch were one scalar round trip per wall
-#if POB_HEX_VWALLS
-      const float lx = HW.lx[w], ly = HW.ly[w], hx = HW.hx[w], hy = HW.hy[w];
-#else
-      const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
-#endif
-      const bool near = (b.x.x <= hx) & (b.x.x >= lx) & (b.x.y <= hy) & (b.x.y >= ly);
+      // every wall's box is tested (the table always holds POB_MAXW rows), w < nw a predicate
+      const bool near = (b.x.x <= HW.hx[w]) & (b.x.x >= HW.lx[w]) & (b.x.y <= HW.hy[w]) & (b.x.y >= HW.ly[w]);
       m |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
@@ -131,37 +114,18 @@ POB_D void hdetect(G &g, csys_t &S, const float *HT, const float *WT, const HWal
     const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
     const float r = HT[HT_R];
     const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
-#if POB_HEX_VWALLS
-    const float (&R)[MW > 0 ? MW : 1][POB_WALL_FLOATS] = HW.row;
-    const float hz = HW.hz, cz = HW.cz;
-#else
-    // every wall row in one scalar round trip (not one per near wall inside its branch)
-    float R[MW > 0 ? MW : 1][POB_WALL_FLOATS];
-#pragma unroll
-    for (int w = 0; w < MW; ++w)
-#pragma unroll
-      for (int k = 0; k < POB_WALL_FLOATS; ++k) R[w][k] = S.wall_row[w][k];
-    const float hz = S.wall_hz, cz = S.wall_cz;
-#endif
-#pragma unroll
-    for (int w = 0; w < MW; ++w) {
-      const bool on = ((m >> w) & 1u) != 0u;
-#ifdef POB_EXP_NO_ANY_WALL  // experiment: every wall row evaluated, no per-wall wave branch
-      if (true) {
-#else
-      if (__any(on)) {
-#endif
-#if POB_HEX_BF_WALL
-        qwall_end_bf(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
-        qwall_end_bf(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
-#else
-        qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe0, r, T, on, false, best, bn, bsel, bpe);
-        qwall_end_vz(g, hz, cz, R[w][0], R[w][1], R[w][2], R[w][3], R[w][4], R[w][5], pe1, r, T, on, true, best, bn, bsel, bpe);
-#endif
-      }
+    while (__any(m != 0u)) {
+      const bool on = m != 0u;
+      const int w = on ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      const float *R = WT + POB_WALL_FLOATS * w;
+      const float2 r01 = *reinterpret_cast<const float2 *>(R);
+      const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
+      const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
+      qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe0, r, T, on, false, best, bn, bsel, bpe);
+      qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe1, r, T, on, true, best, bn, bsel, bpe);
     }
   }
-  (void)WT;
   ct.pen = best;
   ct.n = bn;
   ct.sel = bsel;
@@ -192,11 +156,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
 #endif
   const bool isP = HT[HT_ISP] != 0.0f, hip = HT[HT_ISHIP] != 0.0f;
   const bool torso = isP && hip, leg = !isP && !hip;
-#if POB_HEX_VWALLS
   const HCon SC{HW.friction, S.inv_h};
-#else
-  const csys_t &SC = S;
-#endif
   const v3 px = b.x;
   const q4 pq = b.q;
   // 1. acceleration level: the joint's torque tt (actuator + damping) on both of its lanes
@@ -253,11 +213,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
       if (L2 > 0.0f) {
         const v3 ep = vcross(rp, d), ec = vcross(rc, d);
         const float den = FMA(L2, imp + imc, vdot(ep, ep) + vdot(ec, ec));
-#if POB_HEX_VWALLS
         const float k = (L2 * HW.s_pos) * g.rcp(den);
-#else
-        const float k = (L2 * S.s_pos) * g.rcp(den);
-#endif
         P = vscl(d, k); xp = vscl(ep, k); xc = vscl(ec, k);
       }
       const v3 Pa = vscl(vcross(ap, ac), S.half_s_ang);
@@ -290,7 +246,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     }
     HSUB_T(1)
     if (COLLIDE) {
-      hdetect<MW>(g, S, HT, WT, HW, b, ct);
+      hdetect<MW>(g, HT, WT, HW, b, ct);
       HSUB_T(4)
 #ifdef POB_EXP_NO_WALL_RESPONSE  // timing experiment only: detection kept, no wall response
       asm volatile("" ::"v"(ct.pen), "v"(ct.n.x), "v"(ct.n.y), "v"(ct.n.z), "v"(ct.pe.x), "v"(ct.pe.y), "v"(ct.pe.z));

@@ -82,8 +82,8 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
 }
 
 // The walls in registers (the eight- and sixteen-lane kernels): every wall's broadphase box
-// (xy) and row, and the common z extent, loaded once per launch from the kernel's LDS table
-// into VGPRs.  Read from the system table instead they were ~80 scalar values per collide
+// (xy), the common z extent and the loop's table scalars, loaded once per launch from the
+// kernel's LDS table into VGPRs (the wall rows stay in LDS, read by the per-lane walk).  Read from the system table instead they were ~80 scalar values per collide
 // substep -- more than the SGPR budget holds across the substep loop -- so each collide
 // substep re-issued ~20 scalar loads and waited for them (SQ_WAIT_ANY was 42 % of a wave's
 // cycles at HH B = 4 096 on the sixteen-lane kernel).
@@ -93,7 +93,6 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
 template <int MW>
 struct HWalls {
   float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
-  float row[MW > 0 ? MW : 1][POB_WALL_FLOATS];
   float cz, hz;
   // the table scalars the compiler re-loaded inside the substep loop for want of SGPRs (one
   // waited scalar load per joint projection and per contact): kept in VGPRs as well
@@ -117,13 +116,11 @@ POB_D void hwalls_stage(csys_t &S, float *tab, const int lane) {
   }
 }
 template <int MW>
-POB_D void hwalls_load(const float *tab, const float *WT, HWalls<MW> &HW) {
+POB_D void hwalls_load(const float *tab, HWalls<MW> &HW) {
 #pragma unroll
   for (int w = 0; w < MW; ++w) {
     const float *bx = tab + HW_BOX + 4 * w;
     HW.lx[w] = bx[0]; HW.ly[w] = bx[1]; HW.hx[w] = bx[2]; HW.hy[w] = bx[3];
-#pragma unroll
-    for (int k = 0; k < POB_WALL_FLOATS; ++k) HW.row[w][k] = WT[POB_WALL_FLOATS * w + k];
   }
   HW.cz = tab[HW_CZ]; HW.hz = tab[HW_CZ + 1];
   HW.s_pos = tab[HW_CZ + 2]; HW.friction = tab[HW_CZ + 3];

@@ -113,7 +113,7 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 // sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
 // (the row's six floats given as values: LDS rows for a per-lane wall walk, the system
 // table's scalars for a wave-uniform one)
-// (wall_hz / wall_cz given as values: the sixteen-lane kernel keeps them in registers)
+// (wall_hz / wall_cz given as values: the eight- and sixteen-lane kernels keep them in registers)
 template <class G = GuardBranch>
 POB_D void qwall_end_vz(G &g, const float wall_hz, const float wall_cz, const float cx, const float cy, const float c,
                         const float s, const float hx, const float hy, v3 p, float r, float T, bool on, bool q1,
@@ -143,42 +143,6 @@ POB_D void qwall_end_vz(G &g, const float wall_hz, const float wall_cz, const fl
       bsel = q1;
       bpe = p;
     }
-  }
-}
-// The same search step without branches inside the contact block (the sixteen-lane kernel,
-// one wave per SIMD, where every branch is on the wave's critical path): both the outside
-// (square root) and the inside (least face depth) cases are evaluated and selected, and the
-// deepest-contact update is a select.  Same operations per value, same results; the square
-// root of an inside lane's d2 = 0 is replaced by that of 1 (never selected) so that a range
-// guard never sees it, exactly as when the branch skipped it.
-template <class G = GuardBranch>
-POB_D void qwall_end_bf(G &g, const float wall_hz, const float wall_cz, const float cx, const float cy, const float c,
-                        const float s, const float hx, const float hy, v3 p, float r, float T, bool on, bool q1,
-                        float &best, v3 &bn, bool &bsel, v3 &bpe) {
-  const v3 h = V(hx, hy, wall_hz);
-  v3 d = vsub(p, V(cx, cy, wall_cz));
-  float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
-  float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
-  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
-  float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
-  if (!(d2 >= T)) {
-    const bool out = d2 > 0.0f;
-    float dist, inv;
-    g.sqrt_rcp(out ? d2 : 1.0f, dist, inv);
-    const float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
-    const bool ux = (fx <= fy) & (fx <= fz);
-    const bool uy = !ux & (fy <= fz);
-    const bool uz = !ux & !uy;
-    const float pen = out ? r - dist : r + (ux ? fx : (uy ? fy : fz));
-    const float nx = out ? ex * inv : (ux ? (lx < 0.0f ? -1.0f : 1.0f) : 0.0f);
-    const float ny = out ? ey * inv : (uy ? (ly < 0.0f ? -1.0f : 1.0f) : 0.0f);
-    const float nz = out ? ez * inv : (uz ? (lz < 0.0f ? -1.0f : 1.0f) : 0.0f);
-    const bool take = on && pen > best;
-    const v3 nn = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
-    best = take ? pen : best;
-    bn = vsel3(take, nn, bn);
-    bsel = take ? q1 : bsel;
-    bpe = vsel3(take, p, bpe);
   }
 }
 template <class G = GuardBranch>
