@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pob.h"
@@ -2087,9 +2088,14 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       row[3 * g] = b.x[l].x; row[3 * g + 1] = b.x[l].y; row[3 * g + 2] = b.x[l].z;
     }
     for (int i = POB_NDYN + k; i < N; i += 4) {
+      // (the task bodies written whole below are skipped: every element of the row is written
+      // by one lane once, so the row may go straight to global memory, k_reset's masked path)
+      if (KIND == POB_HEAVENHELL && (i == 11 || i == 12)) continue;
+      if (KIND == POB_TAG && i == 10) continue;
+      if (KIND == POB_GATHER && i >= 11 && i < 11 + S.n_obj) continue;
       row[3 * i] = S.frozen_pos[i][0]; row[3 * i + 1] = S.frozen_pos[i][1]; row[3 * i + 2] = S.frozen_pos[i][2];
     }
-    if (KIND == POB_GATHER) {  // (after the frozen fill in program order) object o on quad lane o % 4
+    if (KIND == POB_GATHER) {  // object o on quad lane o % 4
       const float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
       for (int o = k; o < S.n_obj; o += 4) {
         float *d = row + 3 * (11 + o);
@@ -2305,6 +2311,21 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
   const bool full = mode == RESET_FULL && s.first_pos;
   float *myrow = stg + (lane >> 2) * WP;
+  // A masked reset with few done envs in the wave (the gym step's case: about one) writes each
+  // env's rows straight from its quad's registers to global memory: no LDS staging, no wave
+  // syncs between the arrays (the five staged passes were a quarter of the reset wave's life,
+  // 7.7 K of 28.5 K ticks at HH B = 65 536).  float32 qp storage only (binary16 rows take the
+  // staged path and its converting stores).
+  if (std::is_same<QT, float>::value && mode != RESET_FULL && 4 * __popc(rows) < nenv) {
+    if (active) {
+#pragma unroll 1
+      for (int arr = 0; arr < 5; ++arr) {
+        const int W = arr == RROW_OBS ? D : (arr == RROW_ROT ? 4 * N : 3 * N);
+        float *X = arr == RROW_POS ? s.pos : (arr == RROW_ROT ? s.rot : (arr == RROW_VEL ? s.vel : (arr == RROW_ANG ? s.ang : s.obs)));
+        qreset_row<KIND, BS>(S, R, k, arr, X + (size_t)b * W, ga_obj);
+      }
+    }
+  } else {
 #pragma unroll 1
   for (int arr = 0; arr < 5; ++arr) {
     const int W = arr == RROW_OBS ? D : (arr == RROW_ROT ? 4 * N : 3 * N);
@@ -2319,6 +2340,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     if (arr == RROW_OBS) reset_store_rows<float>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
     else reset_store_rows<QT>(X, FX, (size_t)e0, W, nenv, WP, stg, rows, lane);
     wave_lds_sync();
+  }
   }
   POB_TS(3);
   POB_TS(8);  // (marks the row as a reset wave's: the step kernels do not set stamp 8)

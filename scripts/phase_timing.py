@@ -43,7 +43,7 @@ else:
         jumpy.random_actions_(key, B, 0, act)
         s = env.step_(s, act)
 torch.cuda.synchronize()
-LPE = 4 if GYM else (16 if B <= 8192 else (8 if B <= 16384 else 4))  # lanes per env
+LPE = 4 if GYM else (16 if B <= 4096 else (8 if B <= 16384 else 4))  # lanes per env (default switch points on 256 CUs)
 
 W = (B * LPE + 63) // 64
 NTS = 10  # POB_TS_N
