@@ -253,6 +253,58 @@ def test_randomized_autoreset_naive():
         close(s.obs, so["obs"], f"naive obs t={t}")
 
 
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("mode", ["own", "gym"])
+def test_sparse_masked_reset_rows(name, mode):
+    """Masked resets with a handful of done envs per wave (the gym step's usual case: rows
+    written straight from the quad's registers) next to a wave whose 16 envs are all done
+    (rows staged in LDS), B = 1 000 (ragged last wave).  Done rows equal the oracle's reset
+    -- from the env's own info['rng'] (RandomizedAutoResetWrapperNaive, wrappers.py:30-52)
+    or from split(gym_key, B + 1)[1 + b] (AutoresetVmapGymWrapper, wrappers.py:245-262) --
+    and every other row, and every field the mode does not own, is untouched."""
+    from po_brax_amd import _lib
+    B = 1000
+    envs = _envs()
+    env = envs.create(name, batch_size=B, auto_reset=False, episode_length=1000)
+    s = env.reset(torch.from_numpy(_keys(B, 21)).cuda())
+    rng = np.random.default_rng(5)
+    for _ in range(2):
+        s = env.step_(s, torch.from_numpy(rng.uniform(-1, 1, (B, 8)).astype(np.float32)).cuda())
+    done = np.zeros(B, np.float32)
+    done[[3, 17, 18, 200, 515, 777, 998, 999]] = 1.0   # one or two per wave (direct rows)
+    done[320:336] = 1.0                                  # a whole wave (staged rows)
+    done[480:483] = 1.0                                  # three in one wave (direct rows)
+    s.aux["done"].copy_(torch.from_numpy(done).cuda())
+    before = _state_np(s)
+    o = orc.OracleEnv(name)
+    d = done != 0
+    if mode == "own":
+        env.unwrapped._reset_where_done(s, _lib.RESET_OWN)
+        fresh = o.reset(before["rng"][d])
+    else:
+        gk = P.prngkey(9)
+        gin = torch.from_numpy(gk.astype(np.uint32)).cuda()
+        gout = torch.zeros(2, dtype=torch.uint32, device="cuda")
+        words = torch.zeros(8, dtype=torch.uint32, device="cuda")
+        words[0] = 1  # the step's any-done word: set
+        s.aux["any_done"], s.aux["any_done_clear"] = words[0:4], words[4:8]
+        env.unwrapped._reset_where_done(s, _lib.RESET_GYM, gin, gout, total=B, first=0)
+        ks = P.split(gk, B + 1)
+        fresh = o.reset(ks[1:][d])
+        np.testing.assert_array_equal(_np(gout), ks[0], err_msg="advanced gym key")
+        assert int(words[4]) == 0
+    after = _state_np(s)
+    for k in ("pos", "rot", "vel", "ang", "obs"):
+        exp = before[k].copy()
+        exp[d] = fresh[k]
+        close(after[k], exp, f"{name} {mode} sparse masked reset {k}")
+    exp_steps = np.where(d, 0.0, before["steps"]) if mode == "gym" else before["steps"]
+    np.testing.assert_array_equal(after["steps"], exp_steps)
+    for k in ("reward", "done", "m0", "m1", "m2", "truncation"):
+        np.testing.assert_array_equal(after[k], before[k], err_msg=k)
+    np.testing.assert_array_equal(after["rng"], before["rng"])
+
+
 # ---------------------------------------------------------------------- misc surface
 def test_obs_mask_gather():
     from po_brax_amd import standard_observability_masks as M
