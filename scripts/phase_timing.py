@@ -33,7 +33,7 @@ if MASKED:
 elif GYM:
     gym = envs.create_gym_env(NAME, batch_size=B, seed=0, episode_length=1000)
     gym.reset()
-    for _ in range(30):
+    for _ in range(int(os.environ.get("PT_STEPS", "30"))):  # (the last step's reset waves are recorded)
         jumpy.random_actions_(key, B, 0, act)
         gym.step(act)
 else:
