@@ -2077,7 +2077,11 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
 // over the quad; lane 0 then writes the task rows (program order: after the frozen fill).
 enum { RROW_POS = 0, RROW_ROT = 1, RROW_VEL = 2, RROW_ANG = 3, RROW_OBS = 4 };
 template <int KIND, int BS>
-POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const float *ga_obj) {
+// fill_const = false: the frozen bodies' constant parts (identity rotations, zero velocities,
+// zero contact-force obs) are left to the caller (k_reset's masked path fills them with the
+// whole wave); every element this function writes is disjoint from them.
+POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const float *ga_obj,
+                      const bool fill_const = true) {
   const int N = n_bodies<KIND>(S);
   const QBody &b = R.bd;
   if (arr == RROW_POS) {
@@ -2120,7 +2124,8 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       const int g = qbody_global(l, k);
       row[4 * g] = b.q[l].w; row[4 * g + 1] = b.q[l].x; row[4 * g + 2] = b.q[l].y; row[4 * g + 3] = b.q[l].z;
     }
-    for (int i = POB_NDYN + k; i < N; i += 4) { row[4 * i] = 1.0f; row[4 * i + 1] = 0.0f; row[4 * i + 2] = 0.0f; row[4 * i + 3] = 0.0f; }
+    if (fill_const)
+      for (int i = POB_NDYN + k; i < N; i += 4) { row[4 * i] = 1.0f; row[4 * i + 1] = 0.0f; row[4 * i + 2] = 0.0f; row[4 * i + 3] = 0.0f; }
   } else if (arr == RROW_VEL || arr == RROW_ANG) {
     const v3 *v = arr == RROW_VEL ? b.v : b.w;
 #pragma unroll
@@ -2129,7 +2134,8 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       const int g = qbody_global(l, k);
       row[3 * g] = v[l].x; row[3 * g + 1] = v[l].y; row[3 * g + 2] = v[l].z;
     }
-    for (int i = 3 * POB_NDYN + k; i < 3 * N; i += 4) row[i] = 0.0f;
+    if (fill_const)
+      for (int i = 3 * POB_NDYN + k; i < 3 * N; i += 4) row[i] = 0.0f;
   } else {
     const int sh = obs_shift(KIND);
 #pragma unroll
@@ -2145,7 +2151,8 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       oc[3 * g] = clip1(R.cv[l].x); oc[1 + 3 * g] = clip1(R.cv[l].y); oc[2 + 3 * g] = clip1(R.cv[l].z);
       oc[3 * N + 3 * g] = clip1(R.ca[l].x); oc[1 + 3 * N + 3 * g] = clip1(R.ca[l].y); oc[2 + 3 * N + 3 * g] = clip1(R.ca[l].z);
     }
-    for (int q = 3 * POB_NDYN + k; q < 3 * N; q += 4) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
+    if (fill_const)
+      for (int q = 3 * POB_NDYN + k; q < 3 * N; q += 4) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
     if (k == 0) {
       if (sh == 0) { row[0] = b.x[0].x; row[1] = b.x[0].y; }
       row[sh + 2] = b.x[0].z;
@@ -2322,8 +2329,20 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
       for (int arr = 0; arr < 5; ++arr) {
         const int W = arr == RROW_OBS ? D : (arr == RROW_ROT ? 4 * N : 3 * N);
         float *X = arr == RROW_POS ? s.pos : (arr == RROW_ROT ? s.rot : (arr == RROW_VEL ? s.vel : (arr == RROW_ANG ? s.ang : s.obs)));
-        qreset_row<KIND, BS>(S, R, k, arr, X + (size_t)b * W, ga_obj);
+        qreset_row<KIND, BS>(S, R, k, arr, X + (size_t)b * W, ga_obj, false);
       }
+    }
+    // the frozen bodies' constant parts, by the whole wave (AntGather: 288 floats per env,
+    // 72 single-float stores per lane of the env's quad): identity rotations, zero linear /
+    // angular velocities, zero contact-force obs
+    const int nf = N - POB_NDYN, sh = obs_shift(KIND);
+    for (uint32_t m = rows; m != 0u; m &= m - 1u) {
+      const size_t rb = (size_t)(e0 + __builtin_ctz(m));
+      float *rot = s.rot + rb * 4 * N + 4 * POB_NDYN;
+      float *vel = s.vel + rb * 3 * N + 3 * POB_NDYN, *ang = s.ang + rb * 3 * N + 3 * POB_NDYN;
+      float *oc = s.obs + rb * D + 29 + sh + 3 * POB_NDYN;
+      for (int i = lane; i < 4 * nf; i += 64) rot[i] = (i & 3) == 0 ? 1.0f : 0.0f;
+      for (int i = lane; i < 3 * nf; i += 64) { vel[i] = 0.0f; ang[i] = 0.0f; oc[i] = 0.0f; oc[3 * N + i] = 0.0f; }
     }
   } else {
 #pragma unroll 1

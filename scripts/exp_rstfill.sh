@@ -1,23 +1,23 @@
-# masked reset stores: staged 5-pass (base) vs direct from registers vs LDS rows + one pass (current)
+# masked reset: direct rows (base: build_variants/direct.so) vs + whole-wave constant fills (current)
 set -o pipefail
-mkdir -p gpurun_out/rsthyb
+mkdir -p gpurun_out/rstfill
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
-  -k "gym or autoreset or reset or randomized or eval or sharded or rollout or fp16 or mixed" > gpurun_out/rsthyb/pytest.log 2>&1 || { grep -E "^E |FAILED|Error" gpurun_out/rsthyb/pytest.log | head -30; exit 1; }
-tail -1 gpurun_out/rsthyb/pytest.log
+  -k "gym or autoreset or reset or randomized or eval or sharded or rollout or fp16 or mixed" > gpurun_out/rstfill/pytest.log 2>&1 || { grep -E "^E |FAILED|Error" gpurun_out/rstfill/pytest.log | head -30; exit 1; }
+tail -1 gpurun_out/rstfill/pytest.log
 for r in 1 2 3; do
   for spec in ant_heavenhell:65536 ant_gather:16384 ant_tag:65536; do
     env=${spec%%:*}; B=${spec#*:}
-    for v in base direct hyb; do
-      case $v in base|direct) X="POB_LIB=$PWD/build_variants/$v.so";; hyb) X="";; esac
+    for v in direct fill; do
+      case $v in direct) X="POB_LIB=$PWD/build_variants/$v.so";; fill) X="";; esac
       env $X timeout -k 10 120 python bench.py --no-cpu-baseline --gym --steps 300 --env $env --global-batch $B \
-        > gpurun_out/rsthyb/$v.$env.$B.$r.json 2>/dev/null || exit 1
+        > gpurun_out/rstfill/$v.$env.$B.$r.json 2>/dev/null || exit 1
     done
   done
 done
 python - <<'PY'
 import glob, json, collections, statistics
 d = collections.defaultdict(list)
-for f in glob.glob("gpurun_out/rsthyb/*.json"):
+for f in glob.glob("gpurun_out/rstfill/*.json"):
     v, env, B, r = f.split("/")[-1][:-5].split(".")
     d[(env, int(B), v)].append(json.load(open(f))["ms_per_step"])
 for k in sorted(d):
