@@ -103,6 +103,27 @@ def test_per_step_parity_eight_lane_default(name, B):
     _per_step(name, B, seed=6)
 
 
+@pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag", "ant"])
+@pytest.mark.parametrize("B", [4096, 8192, 16400])  # the sixteen-, eight- and four-lane kernels
+def test_free_running_300_steps(name, B):
+    """GPU and oracle each run 300 steps from the same reset with no restart (episode length
+    100: three autoresets per env on the way), every kernel's default batch range: any float
+    divergence would compound through the contact dynamics, so bit-equality at the end is a
+    strong statement about every step on the way."""
+    T, L = 300, 100
+    env = _envs().create(name, batch_size=B, episode_length=L)
+    keys = _keys(B, 77)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name)
+    so = o.reset(keys, first=True, nthreads=NT)
+    rng = np.random.default_rng(B)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        s = env.step_(s, torch.from_numpy(act).cuda())
+        so = o.step(so, act, flags=FLAGS, episode_length=L, nthreads=NT, inplace=True)
+    compare_states(s, so, f"{name} B={B} free-running t={T}")
+
+
 def _prefix_identical(Ba, Bb, env_a=None, env_b=None):
     envs = _envs()
     for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
