@@ -1943,7 +1943,8 @@ POB_D void choice_topk_wave(uint32_t k0, uint32_t k1, int n, int K, uint2 *lcand
 
 template <int KIND, int BS>
 POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const int k, uint32_t k0, uint32_t k1,
-                          QReset &R, uint32_t *lds_key, int *lds_idx, const bool wave_choice, float *ga_obj) {
+                          QReset &R, uint32_t *lds_key, int *lds_idx, const bool wave_choice, float *ga_obj,
+                          const bool objects_by_wave = false) {
   csys_t &S = *Sp;
   // random_split(rng, 5) (HH, TAG) | 4 (GA) | 3 (stock ant, brax envs/ant.py reset)
   const uint32_t ns = KIND == POB_GATHER ? 4u : (KIND == POB_ANT ? 3u : 5u);
@@ -2013,9 +2014,10 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
     R.rng0 = k0; R.rng1 = k1;  // ant_gather.py:106 stores the input key
     // the objects' positions and sensor readings (ant_gather.py:118-123, _get_readings), object
     // o on quad lane o % 4, into the env's LDS table (GA_OBJ: x, y, z, intensity, slot)
+    // (objects_by_wave: k_reset computes the table with one lane per object instead)
     float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
     const float ori = ga_orientation(b.q[0]);
-    for (int o = k; o < S.n_obj; o += 4) {
+    for (int o = k; o < (objects_by_wave ? 0 : S.n_obj); o += 4) {
       const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + (threadIdx.x >> 2)];
       const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
       float inten;
@@ -2077,11 +2079,12 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
 // over the quad; lane 0 then writes the task rows (program order: after the frozen fill).
 enum { RROW_POS = 0, RROW_ROT = 1, RROW_VEL = 2, RROW_ANG = 3, RROW_OBS = 4 };
 template <int KIND, int BS>
-// fill_const = false: the frozen bodies' constant parts (identity rotations, zero velocities,
-// zero contact-force obs) are left to the caller (k_reset's masked path fills them with the
-// whole wave); every element this function writes is disjoint from them.
+// quad_all = false: the frozen bodies' constant parts (identity rotations, zero velocities,
+// zero contact-force obs) and AntGather's object rows and sensor readings are left to the
+// caller (k_reset's masked path writes them with the whole wave); every element this
+// function writes is disjoint from them.
 POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, float *row, const float *ga_obj,
-                      const bool fill_const = true) {
+                      const bool quad_all = true) {
   const int N = n_bodies<KIND>(S);
   const QBody &b = R.bd;
   if (arr == RROW_POS) {
@@ -2099,7 +2102,7 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       if (KIND == POB_GATHER && i >= 11 && i < 11 + S.n_obj) continue;
       row[3 * i] = S.frozen_pos[i][0]; row[3 * i + 1] = S.frozen_pos[i][1]; row[3 * i + 2] = S.frozen_pos[i][2];
     }
-    if (KIND == POB_GATHER) {  // object o on quad lane o % 4
+    if (KIND == POB_GATHER && quad_all) {  // object o on quad lane o % 4
       const float *eo = ga_obj + (threadIdx.x >> 2) * GA_OBJ_F * POB_MAXOBJ;
       for (int o = k; o < S.n_obj; o += 4) {
         float *d = row + 3 * (11 + o);
@@ -2124,7 +2127,7 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       const int g = qbody_global(l, k);
       row[4 * g] = b.q[l].w; row[4 * g + 1] = b.q[l].x; row[4 * g + 2] = b.q[l].y; row[4 * g + 3] = b.q[l].z;
     }
-    if (fill_const)
+    if (quad_all)
       for (int i = POB_NDYN + k; i < N; i += 4) { row[4 * i] = 1.0f; row[4 * i + 1] = 0.0f; row[4 * i + 2] = 0.0f; row[4 * i + 3] = 0.0f; }
   } else if (arr == RROW_VEL || arr == RROW_ANG) {
     const v3 *v = arr == RROW_VEL ? b.v : b.w;
@@ -2134,7 +2137,7 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       const int g = qbody_global(l, k);
       row[3 * g] = v[l].x; row[3 * g + 1] = v[l].y; row[3 * g + 2] = v[l].z;
     }
-    if (fill_const)
+    if (quad_all)
       for (int i = 3 * POB_NDYN + k; i < 3 * N; i += 4) row[i] = 0.0f;
   } else {
     const int sh = obs_shift(KIND);
@@ -2151,7 +2154,7 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       oc[3 * g] = clip1(R.cv[l].x); oc[1 + 3 * g] = clip1(R.cv[l].y); oc[2 + 3 * g] = clip1(R.cv[l].z);
       oc[3 * N + 3 * g] = clip1(R.ca[l].x); oc[1 + 3 * N + 3 * g] = clip1(R.ca[l].y); oc[2 + 3 * N + 3 * g] = clip1(R.ca[l].z);
     }
-    if (fill_const)
+    if (quad_all)
       for (int q = 3 * POB_NDYN + k; q < 3 * N; q += 4) { oc[q] = 0.0f; oc[3 * N + q] = 0.0f; }
     if (k == 0) {
       if (sh == 0) { row[0] = b.x[0].x; row[1] = b.x[0].y; }
@@ -2162,7 +2165,7 @@ POB_D void qreset_row(csys_t &S, const QReset &R, const int k, const int arr, fl
       const int base = 29 + 6 * N;
       if (KIND == POB_HEAVENHELL) {
         row[base] = 0.0f;  // priest_in_range = 0 at reset
-      } else if (KIND == POB_GATHER) {
+      } else if (KIND == POB_GATHER && quad_all) {
         // the scatter readings[slot] = intensity in object order (a later object wins a slot)
         float *rd = row + base;
         ga_readings_begin(S, rd);
@@ -2303,8 +2306,32 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
     }
   }
   QReset R;
-  if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx, wave_choice, ga_obj);
-  if (KIND == POB_GATHER) wave_lds_sync();  // the objects' table, read by other lanes of the quad
+  // a masked reset with few done envs in the wave (the gym step's case: about one) writes the
+  // rows straight from registers, and the per-object work takes one lane per object
+  const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
+  const bool few = mode != RESET_FULL && 4 * __popc(rows) < nenv;
+  const bool objects_by_wave = KIND == POB_GATHER && few && wave_choice && S.n_obj <= BS;
+  if (active) qreset_compute<KIND, BS>(Sp, LT, WT, k, k0, k1, R, lds_key, lds_idx, wave_choice, ga_obj, objects_by_wave);
+  if (objects_by_wave) {
+    // ant_gather.py:118-123: object o of env e on lane o (the quad's loop ran four in a row)
+    const float ori_l = active ? ga_orientation(R.bd.q[0]) : 0.0f;
+    const float tx_l = active ? R.bd.x[0].x : 0.0f, ty_l = active ? R.bd.x[0].y : 0.0f;
+    for (uint32_t m = rows; m != 0u; m &= m - 1u) {
+      const int e = __builtin_ctz(m);
+      const float ori = __shfl(ori_l, 4 * e), tx = __shfl(tx_l, 4 * e), ty = __shfl(ty_l, 4 * e);
+      if (lane < S.n_obj) {  // (S.n_obj <= BS: checked above)
+        const int o = lane;
+        const int g = lds_idx[POB_MAXOBJ * BS + o * (BS / 4) + e];
+        const float ox = S.grid[3 * g], oy = S.grid[3 * g + 1];
+        float inten;
+        const int slot = ga_reading_slot(S, o, ox, oy, dist2d(tx, ty, ox, oy), ori, inten);
+        float *eo = ga_obj + e * GA_OBJ_F * POB_MAXOBJ;
+        eo[o] = ox; eo[POB_MAXOBJ + o] = oy; eo[2 * POB_MAXOBJ + o] = o < S.ga_n_apples ? 1.0f : S.grid[3 * g + 2];
+        eo[3 * POB_MAXOBJ + o] = inten; eo[4 * POB_MAXOBJ + o] = __int_as_float(slot);
+      }
+    }
+  }
+  if (KIND == POB_GATHER) wave_lds_sync();  // the objects' table, read by other lanes
   POB_TS(2);
 #ifdef POB_EXP_TIMING
   {  // the first active lane's stamps inside the compute (stamps 4..7 of the wave's row)
@@ -2315,7 +2342,6 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   }
 #endif
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
-  const int nenv = B - e0 < BS / 4 ? B - e0 : BS / 4;
   const bool full = mode == RESET_FULL && s.first_pos;
   float *myrow = stg + (lane >> 2) * WP;
   // A masked reset with few done envs in the wave (the gym step's case: about one) writes each
@@ -2323,7 +2349,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   // syncs between the arrays (the five staged passes were a quarter of the reset wave's life,
   // 7.7 K of 28.5 K ticks at HH B = 65 536).  float32 qp storage only (binary16 rows take the
   // staged path and its converting stores).
-  if (std::is_same<QT, float>::value && mode != RESET_FULL && 4 * __popc(rows) < nenv) {
+  if (std::is_same<QT, float>::value && few) {
     if (active) {
 #pragma unroll 1
       for (int arr = 0; arr < 5; ++arr) {
@@ -2343,6 +2369,21 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
       float *oc = s.obs + rb * D + 29 + sh + 3 * POB_NDYN;
       for (int i = lane; i < 4 * nf; i += 64) rot[i] = (i & 3) == 0 ? 1.0f : 0.0f;
       for (int i = lane; i < 3 * nf; i += 64) { vel[i] = 0.0f; ang[i] = 0.0f; oc[i] = 0.0f; oc[3 * N + i] = 0.0f; }
+      if (KIND == POB_GATHER) {
+        // the objects' pos rows (object o on lane o) and the sensor readings (slot r on lane r:
+        // the scatter's last writer in object order, 0 where no object lands)
+        const float *eo = ga_obj + __builtin_ctz(m) * GA_OBJ_F * POB_MAXOBJ;
+        for (int o = lane; o < S.n_obj; o += 64) {
+          float *d = s.pos + rb * 3 * N + 3 * (11 + o);
+          d[0] = eo[o]; d[1] = eo[POB_MAXOBJ + o]; d[2] = eo[2 * POB_MAXOBJ + o];
+        }
+        for (int r = lane; r < 2 * S.ga_n_bins; r += 64) {
+          float v = 0.0f;
+          for (int o = 0; o < S.n_obj; ++o)
+            if (__float_as_int(eo[4 * POB_MAXOBJ + o]) == r) v = eo[3 * POB_MAXOBJ + o];
+          s.obs[rb * D + 29 + 6 * N + r] = v;
+        }
+      }
     }
   } else {
 #pragma unroll 1
