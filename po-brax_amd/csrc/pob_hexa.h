@@ -133,19 +133,7 @@ POB_D void hdetect(G &g, const float *HT, const float *WT, const HWalls<MW> &HW,
 }
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
-// timing experiment only (POB_EXP_TIMING_SUB): shader-clock durations of the substep's
-// phases summed into tacc[0..7] (accel + kinetic, joint, contact position (wall response), velocity
-// contacts (wall), contact detection, ground position, velocity projection, ground velocity)
-#ifdef POB_EXP_TIMING_SUB
-#define HSUB_T(i)                                                  \
-  {                                                                \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();   \
-    if (tacc) tacc[i] += _t - _tl;                                 \
-    _tl = _t;                                                      \
-  }
-#else
-#define HSUB_T(i)
-#endif
+// (HSUB_T: pob_octet.h)
 template <int MW, class G>
 POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, HBody &b,
                         const float act, v3 &cv, v3 &ca, const bool COLLIDE, unsigned long long *tacc = nullptr) {

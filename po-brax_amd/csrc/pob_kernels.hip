@@ -1266,9 +1266,15 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     GuardBranch gb;
     for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false);  // timing experiment only
 #else
+#ifdef POB_EXP_TIMING_SUB  // timing experiment only: phase durations into stamps 5..12
+#define OCT_SUBSTEPS(G)                                                                       \
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
+    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
+#else
 #define OCT_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
     opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0);
+#endif
     if constexpr (!GACC) {
       GuardBranch gb;
       OCT_SUBSTEPS(gb)

@@ -328,6 +328,20 @@ POB_D void ocontact_velocity(G &gd, const HCon &SC, const float *OT, const bool 
   }
 }
 
+// timing experiment only (POB_EXP_TIMING_SUB): shader-clock durations of the eight- and
+// sixteen-lane substeps'
+// phases summed into tacc[0..7] (accel + kinetic, joint, contact position (wall response), velocity
+// contacts (wall), contact detection, ground position, velocity projection, ground velocity)
+#ifdef POB_EXP_TIMING_SUB
+#define HSUB_T(i)                                                  \
+  {                                                                \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();   \
+    if (tacc) tacc[i] += _t - _tl;                                 \
+    _tl = _t;                                                      \
+  }
+#else
+#define HSUB_T(i)
+#endif
 // the lane's joint, oracle joints_position form: point-to-point impulse P and its angular
 // parts xp / xc, hinge alignment + angle limit s
 struct OJoint {
@@ -369,7 +383,13 @@ POB_D void ojoint_position(G &g, csys_t &S, const float s_pos, const float *OT, 
 // loop's table scalars in registers.
 template <int MW, class G>
 POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, OBody &b,
-                        const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE) {
+                        const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE,
+                        unsigned long long *tacc = nullptr) {
+#ifdef POB_EXP_TIMING_SUB
+  unsigned long long _tl = __builtin_amdgcn_s_memtime();
+#else
+  (void)tacc;
+#endif
   const HCon SC{HW.friction, OLAUNDER(Sp)->inv_h};
   v3 px[ONB];
   q4 pq[ONB];
@@ -416,6 +436,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
       b.q[s] = g.qnorm(q);
     }
   }
+  HSUB_T(0)
   // 3. position projection
   OContacts ct;
   const bool gslot1 = !isA;
@@ -450,9 +471,12 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
       DX[0] = vsel3(isA, dxt, dx_aux); DA[0] = vsel3(isA, dat, da_aux);
       DX[1] = vsel3(isA, dx_aux, dx_leg); DA[1] = vsel3(isA, da_aux, da_leg);
     }
+    HSUB_T(1)
     if (COLLIDE) {
       odetect<MW>(g, OT, WT, HW, gslot1, b, ct);
+      HSUB_T(4)
       ocontact_position(g, SC, OT, gslot1, b, px, pq, ct, DX, DA);
+      HSUB_T(5)
     }
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
@@ -460,6 +484,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
       qadd_half(b.q[s], qmul_vq(DA[s], b.q[s]), 1.0f);
     }
   }
+  HSUB_T(2)
   // 4. velocity projection
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
@@ -471,6 +496,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     const float kw = dq.w >= 0.0f ? k2 : -k2;
     b.w[s] = V(dq.x * kw, dq.y * kw, dq.z * kw);
   }
+  HSUB_T(6)
   // 5. velocity-level contacts
   if (COLLIDE) {
     v3 dV[ONB], dW[ONB];
@@ -484,4 +510,5 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
       ca[s] = vadd(ca[s], dW[s]);
     }
   }
+  HSUB_T(3)
 }

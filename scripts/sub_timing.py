@@ -4,7 +4,7 @@ Needs a library built with -DPOB_EXP_TIMING -DPOB_EXP_TIMING_SUB (POB_LIB=...): 
 each wave's row hold the shader-clock durations of the step's substep phases summed over its
 ten substeps (accel + kinetic, joint projection, wall-contact position + the state update,
 wall-contact velocity, contact detection, ground-contact position, velocity projection,
-ground-contact velocity).  argv: B (<= 8192), env name."""
+ground-contact velocity).  argv: B (<= 16 384: the sixteen-lane kernel up to 4 096, the eight-lane one above), env name."""
 import ctypes as C
 import os
 import sys
@@ -25,7 +25,8 @@ for _ in range(20):
     jumpy.random_actions_(key, B, 0, act)
     s = env.step_(s, act)
 torch.cuda.synchronize()
-W = (B * 16 + 63) // 64
+LPE = 16 if B <= 4096 else 8  # lanes per env: the default switch on 256 CUs (B <= 16 384)
+W = (B * LPE + 63) // 64
 NTS = 16  # POB_TS_N of a POB_EXP_TIMING_SUB build
 buf = np.zeros((W, NTS + 4), np.uint64)
 f = _lib.lib.pob_debug_timing
@@ -36,7 +37,9 @@ tot = t[:, NTS - 1] - t[:, 0]
 print(f"{NAME} B={B} waves={W}: wave ticks p50 {np.median(tot):.0f} max {tot.max()}")
 phys = t[:, 2] - t[:, 1]
 print(f"physics (stamp 1->2) p50 {np.median(phys):.0f}")
-names = ("accel+kinetic", "joint", "wall position+update", "wall contact vel", "contact detect",
-         "ground position", "velocity projection", "ground contact vel")
+names = (("accel+kinetic", "joint", "wall position+update", "wall contact vel", "contact detect",
+          "ground position", "velocity projection", "ground contact vel") if LPE == 16 else
+         ("accel+kinetic", "joint", "position update", "contact vel (ground+wall)", "contact detect",
+          "contact position (ground+wall)", "velocity projection", "-"))
 for i, n in zip(range(5, 13), names):
     print(f"{n:26s} p50 {np.median(t[:, i]):8.0f}  p90 {np.percentile(t[:, i], 90):8.0f}  max {t[:, i].max():8.0f}")
