@@ -854,11 +854,23 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       // and the last one runs its final substeps alone, at one-wave latency (measured per
       // wave with POB_EXP_TIMING: p0..max of the physics phase 94 K..211 K ticks before,
       // 133 K..182 K with this; kernel 0.120 -> 0.112 ms at B = 65 536).
-#if POB_QUAD_PRIO
+#if POB_QUAD_PRIO == 1
       const int lvl = (it * 4) / (2 * iters);
       if (lvl == 0) __builtin_amdgcn_s_setprio(3);
       else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
       else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+#elif POB_QUAD_PRIO == 2  // experiment: the levels spent on the last three substeps
+      const int left = 2 * iters - it;
+      if (left > 3) __builtin_amdgcn_s_setprio(3);
+      else if (left == 3) __builtin_amdgcn_s_setprio(2);
+      else if (left == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+#elif POB_QUAD_PRIO == 3  // experiment: the levels spent on the last six substeps, two each
+      const int left = 2 * iters - it;
+      if (left > 6) __builtin_amdgcn_s_setprio(3);
+      else if (left > 4) __builtin_amdgcn_s_setprio(2);
+      else if (left > 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
 #endif
       qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);

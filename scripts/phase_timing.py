@@ -75,3 +75,5 @@ pct = lambda a: " ".join(f"p{q} {np.percentile(a, q) / 100:.1f}" for q in (0, 10
 print(f"wave start us: {pct(r0)}")
 print(f"wave end   us: {pct(r1)}")
 print(f"wave life  us: {pct(r1 - r0)}")
+if os.environ.get("PT_DUMP"):  # raw per-wave rows for offline analysis (hw id, xcc, stamps, clock)
+    np.savez(os.environ["PT_DUMP"], hw=hw, xcc=xcc, t=t, rt=rt, cols=np.array(cols))
