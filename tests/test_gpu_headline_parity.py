@@ -124,6 +124,36 @@ def test_free_running_300_steps(name, B):
     compare_states(s, so, f"{name} B={B} free-running t={T}")
 
 
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 65536), ("ant_gather", 16384), ("ant_tag", 65536)])
+def test_gym_parity_full_size(name, B):
+    """The gym path (create_gym_env -> AutoresetVmapGymWrapper, wrappers.py:240-262) at the
+    bench's sizes: every step's obs, done, qp, episode counter and gym key equal the oracle's
+    (episode length 4: every env resets at step 4 through the gym key's split rows)."""
+    import pob_np as P
+    from test_gpu_parity import close, _np
+    envs = _envs()
+    L, T = 4, 6
+    g = envs.create_gym_env(name, batch_size=B, seed=3, episode_length=L)
+    obs = g.reset()
+    o = orc.OracleEnv(name)
+    ks = P.split(P.prngkey(3), B + 1)
+    so, gkey = o.reset(ks[1:], nthreads=NT), ks[0].copy()
+    np.testing.assert_array_equal(_np(obs), so["obs"])
+    rng = np.random.default_rng(B)
+    for t in range(T):
+        act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+        obs, rew, done, info = g.step(torch.from_numpy(act).cuda())
+        so = o.step(so, act, flags=orc.F_EPISODE, episode_length=L, inplace=True, nthreads=NT)
+        np.testing.assert_array_equal(_np(done), so["done"], err_msg=f"t={t}")
+        o.gym_autoreset(so, gkey, nthreads=NT)
+        close(obs, so["obs"], f"{name} B={B} gym obs t={t}")
+        close(rew, so["reward"], f"{name} B={B} gym reward t={t}")
+        close(g._state.qp.pos, so["pos"], f"{name} B={B} gym pos t={t}")
+        close(g._state.qp.rot, so["rot"], f"{name} B={B} gym rot t={t}")
+        np.testing.assert_array_equal(_np(g._key), gkey, err_msg=f"gym key t={t}")
+        np.testing.assert_array_equal(_np(g._state.info["steps"]), so["steps"])
+
+
 def _prefix_identical(Ba, Bb, env_a=None, env_b=None):
     envs = _envs()
     for name in ("ant_heavenhell", "ant_gather", "ant_tag", "ant"):
