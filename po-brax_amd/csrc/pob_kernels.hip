@@ -2271,13 +2271,17 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   // used the other word, and the next launch on the stream reads this one after it is zero
   if (s.any_done_clear && blockIdx.x == 0 && lane == 0) *s.any_done_clear = 0u;
   bool active = b < B;
-  // the env's done flag is loaded together with the any-done word (one round trip, not two)
+  // the env's done flag is loaded together with the any-done word and the gym key (one round
+  // trip, not two: the key's hash below would otherwise wait for a load issued after the
+  // any-done test)
   const float dn = active && mode != RESET_FULL ? s.done[b] : 1.0f;
+  uint32_t gk0 = 0u, gk1 = 0u;
+  if (mode == RESET_GYM) { gk0 = gym_in[0]; gk1 = gym_in[1]; }
   if (mode == RESET_GYM) {
     const bool any = *any_flag != 0u;
     if (b == 0 && k == 0 && gym_out) {
-      uint32_t g0 = gym_in[0], g1 = gym_in[1];
-      if (any) tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, 0u, g0, g1);
+      uint32_t g0 = gk0, g1 = gk1;
+      if (any) tf_split(gk0, gk1, (uint32_t)total + 1u, 0u, g0, g1);
       gym_out[0] = g0; gym_out[1] = g1;
     }
     if (!any) return;  // block-uniform
@@ -2302,7 +2306,7 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   if (active) {
     if (mode == RESET_FULL) { k0 = keys[2 * b]; k1 = keys[2 * b + 1]; }
     else if (mode == RESET_GYM)
-      tf_split(gym_in[0], gym_in[1], (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
+      tf_split(gk0, gk1, (uint32_t)total + 1u, (uint32_t)(first + b) + 1u, k0, k1);
     else { k0 = s.rng[2 * b]; k1 = s.rng[2 * b + 1]; }
   }
   POB_TS(1);

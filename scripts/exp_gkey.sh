@@ -1,0 +1,25 @@
+# masked reset: gym key loaded with the done flag and any-done word (new) vs after the any-done test (cur)
+set -o pipefail
+mkdir -p gpurun_out/gkey
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+  -k "gym or autoreset or reset or randomized or eval or sharded or rollout or fp16 or mixed" > gpurun_out/gkey/pytest.log 2>&1 || { grep -E "^E |FAILED|Error" gpurun_out/gkey/pytest.log | head -30; exit 1; }
+tail -1 gpurun_out/gkey/pytest.log
+for r in 1 2 3; do
+  for spec in ant_heavenhell:65536 ant_gather:16384 ant_tag:65536; do
+    env=${spec%%:*}; B=${spec#*:}
+    for v in cur new; do
+      case $v in cur) X="POB_LIB=$PWD/build_variants/$v.so";; new) X="";; esac
+      env $X timeout -k 10 120 python bench.py --no-cpu-baseline --gym --steps 300 --env $env --global-batch $B \
+        > gpurun_out/gkey/$v.$env.$B.$r.json 2>/dev/null || exit 1
+    done
+  done
+done
+python - <<'PY'
+import glob, json, collections, statistics
+d = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/gkey/*.json"):
+    v, env, B, r = f.split("/")[-1][:-5].split(".")
+    d[(env, int(B), v)].append(json.load(open(f))["ms_per_step"])
+for k in sorted(d):
+    print(*k, "median %.4f" % statistics.median(d[k]), sorted(d[k]))
+PY
