@@ -29,6 +29,9 @@
 #ifndef POB_QUAD_PRIO  // the four-lane kernel's falling issue priority over the substeps (k_step_quad)
 #define POB_QUAD_PRIO 1
 #endif
+#ifndef POB_OCT_PRIO  // the same in the eight-lane kernel's branch-guard build (two waves per SIMD)
+#define POB_OCT_PRIO 1
+#endif
 #include "pob_quad.h"
 #include "pob_octet.h"
 #include "pob_hexa.h"
@@ -1289,9 +1292,20 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
     opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
 #else
+// At two waves per SIMD (the branch-guard build, B > 8 x SIMDs) the four-lane kernel's falling
+// issue priority keeps a SIMD's waves together (k_step_quad): HH B = 16 384 -2.2 %, TAG -3 %,
+// GA -0.5 % (profiles/r3t/oct_prio_ab.txt); a lone wave per SIMD has no one to yield to.
 #define OCT_SUBSTEPS(G)                                                                       \
-  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0);
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it) {                               \
+    if (!GACC && POB_OCT_PRIO) {                                                               \
+      const int lvl_ = (it * 4) / (2 * iters);                                                 \
+      if (lvl_ == 0) __builtin_amdgcn_s_setprio(3);                                            \
+      else if (lvl_ == 1) __builtin_amdgcn_s_setprio(2);                                       \
+      else if (lvl_ == 2) __builtin_amdgcn_s_setprio(1);                                       \
+      else __builtin_amdgcn_s_setprio(0);                                                      \
+    }                                                                                          \
+    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0);                \
+  }
 #endif
     if constexpr (!GACC) {
       GuardBranch gb;
