@@ -1496,8 +1496,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 // block; lane r of an env owns one body and one side of one joint (P_hip_r / C_hip_(7-r) /
 // P_knee_(r-8) / C_knee_(15-r)).  Lane 0 (P_hip_0, the torso) runs the per-env POMDP tail.
 #define POB_HSTAGE_FLOATS (OL_FLOATS * 64)
+#ifndef POB_HEX_MINW  // experiment: the register budget of this many waves per SIMD
+#define POB_HEX_MINW 1
+#endif
 template <int KIND, typename QT, bool GACC>
-__global__ __launch_bounds__(64) void k_step_hex(const void *sysp, const int B, const StatePtrs in,
+__global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp, const int B, const StatePtrs in,
                                                  const float *__restrict__ act, const StatePtrs out,
                                                  const uint32_t flags, const int L) {
   static_assert(KIND != POB_MIXED, "the sixteen-lane kernel runs one env kind per launch");
