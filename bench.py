@@ -99,7 +99,15 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
                          "hipGraph (po_brax_amd.rollout); --gather-obs and the sharded gym path are eager")
+    ap.add_argument("--legacy-spring", action="store_true",
+                    help="brax <= 0.0.12 spring/impulse dynamics (the physics notebooks/ant_tag.ipynb:449 "
+                         "pins) instead of PBD")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without torchrun: start the N ranks here, before anything
+        # touches the GPU in this process (children by subprocess, never exec)
+        return launch_ranks(args.gpus)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,6 +122,10 @@ def main() -> int:
         dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
     if args.gym and args.env == "mixed":
         ap.error("--gym runs one env kind")
+    if args.legacy_spring and args.env == "mixed":
+        ap.error("--legacy-spring runs one env kind")
+    ranks = rank_devices(dev, world)  # every rank's device, gathered over the process group
+    ekw = {"legacy_spring": True} if args.legacy_spring else {}
 
     from po_brax_amd import envs, jumpy
     from po_brax_amd.sharding import ObsGatherer, Shard, shard_keys
@@ -127,7 +139,7 @@ def main() -> int:
     gym = None
     if args.gym:
         gym = envs.create_gym_env(args.env, batch_size=total, seed=0, episode_length=args.episode_length,
-                                  device=dev, qp_dtype=qp_dtype, shard=shard if world > 1 else None)
+                                  device=dev, qp_dtype=qp_dtype, shard=shard if world > 1 else None, **ekw)
         gym.reset()
         state = None
     elif args.env == "mixed":
@@ -139,7 +151,7 @@ def main() -> int:
         state = [e.reset(keys[o:o + b].contiguous()) for e, o, b in zip(env.envs, env.offsets(), sizes)]
     else:
         env = envs.create(args.env, batch_size=B, episode_length=args.episode_length, device=dev,
-                          qp_dtype=qp_dtype)
+                          qp_dtype=qp_dtype, **ekw)
         state = env.reset(shard_keys(key, total, world, rank))
     act_key = jumpy.random_split(key, total + 1)[0].contiguous()  # VmapGymWrapper: key <- keys[0]
 
@@ -273,15 +285,19 @@ def main() -> int:
     bpe = sum(bytes_per_env_step(n, qb) * b for n, b in kinds) / B
     try:
         import orc  # test-infrastructure oracle: FLOP count of the restated algorithm only
-        f_ref = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_REF_PAIRS) * b for n, b in kinds) / B
-        f_exe = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_EXECUTED) * b for n, b in kinds) / B
+        okw = {"legacy_spring": 1} if args.legacy_spring else {}
+        f_ref = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_REF_PAIRS, **okw) * b
+                    for n, b in kinds) / B
+        f_exe = sum(orc.flops_per_env_step(n, B=64, steps=10, mode=orc.FLOPS_EXECUTED, **okw) * b
+                    for n, b in kinds) / B
     except Exception as ex:  # pragma: no cover
         print(f"flop count unavailable: {ex}", file=sys.stderr)
         f_ref = f_exe = float("nan")
     ks = kern_ms * 1e-3
     hbm_gbs = bpe * B / ks / 1e9
     tflops = f_ref * B / ks / 1e12
-    kname = "k_step_mixed" if args.env == "mixed" else f"{step_kernel(B)}<{args.env}>"
+    kname = "k_step_mixed" if args.env == "mixed" else (
+        f"k_step_legacy<{args.env}>" if args.legacy_spring else f"{step_kernel(B)}<{args.env}>")
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TF, "unit": "TFLOP/s",
         "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
@@ -300,7 +316,7 @@ def main() -> int:
         "hbm": {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
     }
-    prof = committed_profile(args.env, B, args.qp_dtype)
+    prof = committed_profile(args.env, B, args.qp_dtype, args.legacy_spring)
     if prof is not None and gym is None:
         if prof.get("traffic_bytes"):
             roofline["traffic"] = prof["traffic_bytes"]
@@ -321,13 +337,14 @@ def main() -> int:
     cpu = None
     if not args.no_cpu_baseline and world == 1 and gym is None:
         cpu = cpu_baseline("ant_heavenhell" if args.env == "mixed" else args.env, B, args.cpu_seconds,
-                           args.cpu_threads)
+                           args.cpu_threads, legacy=args.legacy_spring)
 
     par = f"env-shard x{world}" + (" (strong: global batch split)" if strong else " (weak: batch per GPU)")
     line = {
         "metric": HEADLINE_METRIC if (args.env == "ant_heavenhell" and strong and total == 65536 and gym is None
-                                      and not args.policy_mlp)
-                  else f"env-steps/sec {args.env} " + (f"global batch {total}" if strong else f"batch {args.batch}/GPU")
+                                      and not args.policy_mlp and not args.legacy_spring)
+                  else f"env-steps/sec {args.env} " + ("legacy_spring " if args.legacy_spring else "")
+                  + (f"global batch {total}" if strong else f"batch {args.batch}/GPU")
                   + (f" with a {args.policy_mlp}-hidden MLP policy in the loop" if args.policy_mlp else ""),
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -335,7 +352,9 @@ def main() -> int:
         "config": {"workload": f"{args.env} B={B}/GPU (global {total}), "
                                + ("create_gym_env (AutoresetVmapGymWrapper, gym-side autoreset)"
                                   if gym is not None else "create(batch_size=B) autoreset chain")
-                               + f", episode_length {args.episode_length}, PBD 10 substeps, random "
+                               + f", episode_length {args.episode_length}, "
+                               + ("legacy spring/impulse (brax <= 0.0.12)" if args.legacy_spring else "PBD")
+                               + " 10 substeps, random "
                                "uniform(-1,1) actions (threefry)"
                                + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else "")
                                + (", RCCL obs all-gather per step" if do_gather else "")
@@ -343,10 +362,15 @@ def main() -> int:
                                   if args.policy_mlp else ""),
                    "env": args.env, "global_batch": total, "batch_per_gpu": B,
                    "episode_length": args.episode_length, "qp_storage": args.qp_dtype, "parallelism": par,
+                   "dynamics": "legacy_spring" if args.legacy_spring else "pbd",
                    "path": "gym" if gym is not None else "brax",
                    "launch": "hipGraph replay of the K steps" if roll is not None else "eager per step"},
         "gpu_event_ms_per_step": round(kern_ms_max + (float(elapsed[2]) if do_gather else 0.0), 4),
         "roofline": roofline, "cpu_baseline": cpu, "obs_finite": finite,
+        # what ran: the process group's size and each rank's device (so a reader can tell N ranks
+        # on N devices from N ranks sharing one)
+        "world_size": world, "dist_backend": args.dist_backend if world > 1 else None,
+        "rank_devices": ranks, "distinct_devices": len({r["device"] for r in ranks}),
     }
     if do_gather:
         line["obs_allgather_ms"] = round(float(elapsed[2]), 4)
@@ -356,6 +380,61 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def launch_ranks(n: int, argv=None, script: str = None) -> int:
+    """Run this command as ``n`` ranks on this node (what torchrun would do): child processes
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, sharing this
+    process's stdout (rank 0 prints the JSON line).  Returns non-zero if any rank fails; the
+    other ranks are then terminated (they would wait at a barrier)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__),
+                                       *(sys.argv[1:] if argv is None else argv)], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
+def rank_devices(dev, world: int) -> list:
+    """[{rank, device, pci}] of every rank (all_gather_object over the process group)."""
+    me = {"rank": int(os.environ.get("RANK", "0")), "device": f"cuda:{dev.index}"}
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        me["pci"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+        me["device"] = me["pci"]
+    except Exception:  # pragma: no cover (older torch: no PCI ids)
+        pass
+    if world == 1:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
 
 
 def step_kernel(B: int) -> str:
@@ -370,7 +449,7 @@ def step_kernel(B: int) -> str:
     return "k_step_quad"
 
 
-def committed_profile(env: str, B: int, qp: str):
+def committed_profile(env: str, B: int, qp: str, legacy: bool = False):
     """Counters per launch from the newest committed PMC profile of this exact config
     (profiles/*_traffic.json, written by profiles/summarize.py); None if there is none."""
     best, key = None, None
@@ -380,14 +459,14 @@ def committed_profile(env: str, B: int, qp: str):
         except (OSError, ValueError):
             continue
         if t.get("env") == env and t.get("batch") == B and t.get("qp_storage", "f32") == qp and \
-                "k_step" in (t.get("kernel") or ""):
+                "k_step" in (t.get("kernel") or "") and bool(t.get("legacy_spring", False)) == bool(legacy):
             k = (t.get("generated", 0.0), p)  # newest by the summary's timestamp, then name
             if key is None or k > key:
                 best, key = t, k
     return best
 
 
-def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0) -> dict:
+def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0, legacy: bool = False) -> dict:
     """The C restatement (kind "port": same algorithm, oracle/pob_oracle.c) compiled
     -O3 -march=native on this host, timed on the same workload (this GPU's batch B): on the
     process's CPU share and on one thread (OpenMP over envs, static schedule; time-boxed).
@@ -396,8 +475,10 @@ def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0) -> dict:
     thread pools to it: ``sched_getaffinity`` there lists the whole shared host, 256 cores,
     most of them other tenants'), or every affinity core when it is unset; ``threads`` (bench
     ``--cpu-threads``, e.g. all cores of a dedicated host) overrides it.  The reported
-    ``value`` is the multi-threaded leg; ``all_cores_linear_bound`` = single-thread rate x
-    affinity cores is an upper bound for the whole host, not a measurement."""
+    ``value`` is the multi-threaded leg.  No all-cores leg runs on the GPU pool: its hosts are
+    shared, each GPU's job gets a 16-thread CPU share and the pool's rules ask jobs to size
+    their thread pools to it (the line says so in ``all_cores``); ``--cpu-threads N`` times N
+    threads on a dedicated host."""
     import numpy as np
     import orc
     import pob_np as P
@@ -407,7 +488,7 @@ def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0) -> dict:
         aff = os.cpu_count() or 1
     share = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff)))
     nt_multi = max(1, min(aff, threads)) if threads > 0 else share
-    e = orc.OracleEnv(name, native=True)
+    e = orc.OracleEnv(name, native=True, **({"legacy_spring": 1} if legacy else {}))
     s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True, nthreads=nt_multi)
     acts = np.random.default_rng(0).uniform(-1, 1, (2, B, 8)).astype(np.float32)
     out = {}
@@ -425,8 +506,13 @@ def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0) -> dict:
     v1 = out["single"][0]
     return {"value": round(v, 1), "unit": "env-steps/s", "cores": nt_multi, "kind": "port",
             "single_thread_value": round(v1, 1),
-            "all_cores_linear_bound": round(v1 * aff, 1),
-            "sample": f"{name} B={B} (the GPU workload's batch), the same fused step (oracle/pob_oracle.c, "
+            "all_cores": (f"measured: {nt_multi} threads = every affinity core" if nt_multi >= aff else
+                          f"not run: this host's {aff} affinity cores are shared by the GPU pool's jobs, which "
+                          f"give each GPU's job a {share}-thread CPU share (OMP_NUM_THREADS) and require thread "
+                          "pools sized to it; an all-core leg would time other tenants' load. "
+                          "`bench.py --cpu-threads N` times N threads on a dedicated host"),
+            "sample": f"{name} B={B} (the GPU workload's batch)" + (", legacy spring dynamics" if legacy else "")
+                      + ", the same fused step (oracle/pob_oracle.c, "
                       "gcc -O3 -march=native, OpenMP over envs): "
                       + "; ".join(f"{o[1]} steps in {o[2]:.1f} s on {o[3]} thread(s)" for o in out.values()),
             "threads_basis": ("--cpu-threads" if threads > 0 else

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 5
+#define POB_ABI_VERSION 6
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -131,9 +131,13 @@ const char *pob_last_error(void);
 int pob_default_params(pob_params *p);
 int pob_env_create(int kind, const pob_params *p, pob_env **out);
 /* Never calls the HIP runtime (safe while a stream is being captured into a hipGraph): the
- * env's device tables are released by the next pob_env_create.  The caller must not destroy
- * an env whose launches are still queued or captured in a graph it will replay. */
+ * env's device tables (~4 KB) are KEPT until the next pob_env_create or
+ * pob_release_deferred call.  The caller must not destroy an env whose launches are still
+ * queued or captured in a graph it will replay. */
 void pob_env_destroy(pob_env *env);
+/* Free the device tables of every destroyed env now (ABI v6); returns how many buffers were
+ * released.  Calls hipFree: never call it while a stream is being captured. */
+int pob_release_deferred(void);
 int pob_env_dims(const pob_env *env, int *n_bodies, int *obs_dim, int *act_dim);
 /* host copy of default_angle() (8 floats, radians): System.default_angle [ext] */
 int pob_env_default_angle(const pob_env *env, float *out8);

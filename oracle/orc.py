@@ -240,7 +240,7 @@ FLOPS_REF_PAIRS, FLOPS_EXECUTED = 0, 1
 
 
 def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_EPISODE | F_AUTORESET,
-                       seed: int = 0, mode: int = FLOPS_REF_PAIRS) -> float:
+                       seed: int = 0, mode: int = FLOPS_REF_PAIRS, **params) -> float:
     """Algorithmic FLOPs of one fused env-step (physics + POMDP + obs), counted by the
     instrumented restatement on a random-action rollout (single-threaded).
 
@@ -248,7 +248,7 @@ def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_E
     algorithm); FLOPS_EXECUTED: only the pairs the HIP kernel evaluates after its exact
     culls (same results).  Executed branches only in both (an inactive contact is free)."""
     import pob_np as P
-    e = OracleEnv(name, count_flops=True)
+    e = OracleEnv(name, count_flops=True, **params)
     s = e.reset(P.split(P.prngkey(seed), B + 1)[1:], first=True)
     rng = np.random.default_rng(seed)
     e._L.orc_flops_set_mode(mode)

@@ -2729,6 +2729,16 @@ void pob_env_destroy(pob_env *e) {
   delete e;
 }
 
+int pob_release_deferred(void) {
+  size_t n;
+  {
+    std::lock_guard<std::mutex> lk(g_grave_mu);
+    n = g_grave.size();
+  }
+  drain_grave();
+  return (int)n;
+}
+
 int pob_env_dims(const pob_env *e, int *n, int *d, int *a) {
   if (!e) return fail(POB_EINVAL, "env is NULL");
   if (n) *n = e->sys.N;

@@ -22,7 +22,7 @@ RESET_GYM, RESET_OWN = 0, 1
 KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 QP_F32, QP_F16 = 0, 1
 MIX_MAX = 4
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class pob_params(C.Structure):
@@ -54,7 +54,7 @@ class pob_state(C.Structure):
 # Every symbol include/pob.h declares (checked by tests/test_lib_symbols.py).
 EXPORTS = (
     "pob_abi_version", "pob_last_error", "pob_default_params", "pob_env_create",
-    "pob_env_destroy", "pob_env_dims", "pob_env_default_angle", "pob_reset", "pob_step",
+    "pob_env_destroy", "pob_release_deferred", "pob_env_dims", "pob_env_default_angle", "pob_reset", "pob_step",
     "pob_step_mixed", "pob_reset_where_done", "pob_reset_where_done_shard", "pob_default_qp",
     "pob_random_split", "pob_random_split_batch", "pob_random_uniform", "pob_random_actions", "pob_obs_gather",
 )
@@ -76,6 +76,7 @@ def _load():
     lib.pob_env_create.argtypes = [C.c_int, C.POINTER(pob_params), C.POINTER(_VP)]
     lib.pob_env_destroy.argtypes = [_VP]
     lib.pob_env_destroy.restype = None
+    lib.pob_release_deferred.argtypes = []
     lib.pob_env_dims.argtypes = [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.pob_env_default_angle.argtypes = [_VP, C.POINTER(C.c_float)]
     lib.pob_reset.argtypes = [_VP, C.c_int, _VP, C.POINTER(pob_state), _VP]
@@ -128,6 +129,12 @@ def check(rc: int) -> None:
     if rc == POB_EINVAL:
         raise ValueError(msg)
     raise PobError(f"libpob status {rc}: {msg}")
+
+
+def release_deferred() -> int:
+    """Free the device tables of destroyed envs now (pob_release_deferred; otherwise they wait
+    for the next env creation).  Calls hipFree: never inside a hipGraph capture."""
+    return int(lib.pob_release_deferred())
 
 
 def stream_handle(device=None) -> int:

@@ -431,7 +431,10 @@ class PoBraxEnv(Env):
 
     @staticmethod
     def _same_refs(a: tuple, b: tuple) -> bool:
-        return len(a) == len(b) and all(x is y or (type(x) is int and x == y) for x, y in zip(a, b))
+        # ints (flags, episode length) compare by value, everything else by identity; an int
+        # cached where a tensor now sits (or the reverse) is a mismatch, never a tensor compare
+        return len(a) == len(b) and all(x is y or (type(x) is int and type(y) is int and x == y)
+                                        for x, y in zip(a, b))
 
     def _step_impl(self, state: State, action, flags: int, episode_length: int, inplace: bool) -> State:
         if inplace and _CAPTURE is None:

@@ -26,6 +26,13 @@ from typing import Sequence
 import torch
 
 
+def _release_deferred():
+    """Outside a capture: free the tables of envs destroyed (possibly by a GC pass inside the
+    capture) since the last env creation (include/pob.h pob_release_deferred)."""
+    from . import _lib
+    _lib.release_deferred()
+
+
 @contextlib.contextmanager
 def no_gc():
     """Keep the cyclic garbage collector off for the span of a hipGraph capture: a collection
@@ -102,6 +109,7 @@ class GraphRollout:
                     # follow the returned State: its public typed outputs (TAG done, GA
                     # counts) are the buffers the captured kernels write
                     self.state = self.env.step_(self.state, self.actions[t])
+            _release_deferred()
             return
         bounds = [(B * g // groups, B * (g + 1) // groups) for g in range(groups)]
         # the typed step outputs (TAG bool done, GA int32 counts) live in the whole batch's
@@ -121,6 +129,7 @@ class GraphRollout:
             for st in streams[1:]:
                 cap.wait_stream(st)  # join
         self.parts = parts
+        _release_deferred()
         # the whole batch's State after a step (public fields in the reference's dtypes)
         self.state = u._state_of(u._bufs_of(self.state), True, False)
 
@@ -153,11 +162,24 @@ class GymGraphRollout:
     only: the sharded wrapper's per-step RCCL all-reduce stays eager."""
 
     def __init__(self, gym, actions: torch.Tensor):
+        from .envs.wrappers import AutoresetVmapGymWrapper, EvalGymWrapper
         if actions.dim() != 3 or actions.shape[0] % 2:
             raise ValueError("actions must be (T, B, A) with T even")
+        # Only the bare device-side gym is capture-safe.  A wrapper with host-side per-step
+        # bookkeeping (EvalGymWrapper's queue count / growth; it forwards _shard / _state to the
+        # inner gym) would not advance on replay -- its queue would overrun its fixed capacity --
+        # and may sync the host inside the capture, so it is refused by type.
+        if isinstance(gym, EvalGymWrapper):
+            raise NotImplementedError("GymGraphRollout cannot capture an EvalGymWrapper (host-side episode "
+                                      "queues); capture the inner gym and step the eval wrapper eagerly")
+        if not isinstance(gym, AutoresetVmapGymWrapper):
+            raise NotImplementedError(f"GymGraphRollout captures create_gym_env's AutoresetVmapGymWrapper, "
+                                      f"not {type(gym).__name__}")
         sh = getattr(gym, "_shard", None)
         if sh is not None and sh.world > 1:
             raise NotImplementedError("a sharded gym step (RCCL any-done all-reduce) runs eagerly")
+        if gym._state is None:
+            raise ValueError("reset() the gym before capturing its steps")
         self.gym, self.actions = gym, actions
         self.steps = int(actions.shape[0])
         dev = actions.device
@@ -166,12 +188,19 @@ class GymGraphRollout:
         with no_gc(), torch.cuda.graph(self.graph):
             for t in range(self.steps):
                 gym.step(self.actions[t])
+        # the buffers the captured kernels read and write (T even: the key pair is back in order)
+        self._captured = (gym._state, gym._key, gym._key2)
+        _release_deferred()
 
     def replay(self):
         """Run the captured gym steps; returns (obs, reward, done, metrics) of the last."""
+        st, k, k2 = self._captured
+        g = self.gym
+        if g._state is not st or g._key is not k or g._key2 is not k2:
+            raise RuntimeError("the gym was reset or stepped outside the captured graph since capture; "
+                               "rebuild the GymGraphRollout")
         self.graph.replay()
-        s = self.gym._state
-        return s.obs, s.reward, s.done, s.metrics
+        return st.obs, st.reward, st.done, st.metrics
 
 
 class PolicyRollout:

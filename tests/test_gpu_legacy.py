@@ -96,3 +96,25 @@ def test_legacy_rejected_by_mixed_step():
     s = m.reset(jumpy.random_prngkey(0), [8, 8])
     with pytest.raises(ValueError):
         m.step(s, torch.zeros((16, 8), device="cuda"))
+
+
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 65536), ("ant_tag", 65536), ("ant_gather", 16384)])
+def test_legacy_per_step_parity_bench_sizes(name, B):
+    """Legacy dynamics at the BASELINE.json batch sizes (configs 1/4 HH / TAG 65 536, config 3
+    GA 16 384): reset parity, then per-step parity with the oracle restarted from the GPU's
+    state each step, bit-exact on every field; episode length 3 makes step 3 autoreset every
+    env (the first_qp / first_obs rows run)."""
+    from test_gpu_headline_parity import NT, _actions
+    T, L = 4, 3
+    env = _envs().create(name, batch_size=B, episode_length=L, legacy_spring=True)
+    keys = _keys(B, 23)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    o = orc.OracleEnv(name, legacy_spring=1)
+    compare_states(s, o.reset(keys, first=True, nthreads=NT), f"{name} legacy B={B} reset")
+    n_done = 0
+    for t, act in enumerate(_actions(29, B, T)):
+        so = o.step(_state_np(s), act, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=L, nthreads=NT)
+        s = env.step_(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} legacy B={B} step {t}")
+        n_done += int(so["done"].sum())
+    assert n_done >= B

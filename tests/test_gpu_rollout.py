@@ -123,8 +123,13 @@ def test_capture_survives_gc_of_dead_envs():
     for f in ("pos", "rot", "vel", "ang"):
         assert torch.equal(getattr(s1.qp, f), getattr(s2.qp, f)), f
     assert torch.equal(s1.obs, s2.obs) and torch.equal(s1.done, s2.done)
-    # the deferred tables are released by the next create (outside any capture)
-    envs.create("ant_tag", batch_size=8)
+    # the deferred tables are released by the next create or by pob_release_deferred (outside
+    # any capture)
+    from po_brax_amd import _lib
+    doomed = envs.create("ant_tag", batch_size=8).unwrapped
+    del doomed
+    assert _lib.release_deferred() >= 1
+    assert _lib.release_deferred() == 0
 
 
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag"])
@@ -152,6 +157,29 @@ def test_gym_graph_rollout_equals_eager(name):
         assert torch.equal(g1._key, g2._key), rep
         for k in m1:
             assert torch.equal(m1[k], m2[k]), (rep, k)
+
+
+def test_gym_graph_rollout_refuses_host_bookkeeping_and_stale_buffers():
+    """An eval_metrics gym (EvalGymWrapper: host-side queue count and growth, forwarded
+    attributes) is refused at construction instead of being captured with a queue that replay
+    never advances; replaying after gym.reset() (new state and key buffers) raises instead of
+    silently stepping the captured, stale buffers."""
+    from po_brax_amd import envs
+    from po_brax_amd.rollout import GymGraphRollout
+    B = 64
+    acts = _acts(2, B, 17)
+    ev = envs.create_gym_env("ant_tag", batch_size=B, seed=1, episode_length=3, eval_metrics=True)
+    ev.reset()
+    with pytest.raises(NotImplementedError, match="EvalGymWrapper"):
+        GymGraphRollout(ev, acts)
+    g = envs.create_gym_env("ant_tag", batch_size=B, seed=1, episode_length=3)
+    g.reset()
+    roll = GymGraphRollout(g, acts)
+    roll.replay()
+    g.reset()
+    with pytest.raises(RuntimeError, match="rebuild"):
+        roll.replay()
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_tag"])
