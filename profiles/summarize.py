@@ -57,6 +57,7 @@ def main(src, dst_prefix):
         traffic = {"kernel": next((r["Name"] for r in stats if "k_step" in r["Name"]), None),
                    "env": cfg.get("env"), "batch": cfg.get("batch_per_gpu", cfg.get("global_batch")),
                    "qp_storage": cfg.get("qp_storage"),
+                   "legacy_spring": cfg.get("dynamics") == "legacy_spring",
                    "fetch_bytes_raw": f, "write_bytes": w, "traffic_bytes": 2 * f + w,
                    "valu_insts": mean("SQ_INSTS_VALU"), "grbm_gui_active": mean("GRBM_GUI_ACTIVE"),
                    "waves": mean("SQ_WAVES"),
