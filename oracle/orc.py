@@ -71,7 +71,7 @@ class Params(C.Structure):
         ("tag_target_step", C.c_float), ("tag_min_spawn_distance", C.c_float),
         ("tag_cage_xy", C.c_float * 2), ("tag_dying_cost", C.c_float),
         ("action_repeat", C.c_int), ("solver_scale_pos", C.c_float), ("solver_scale_ang", C.c_float),
-        ("legacy_spring", C.c_int),
+        ("legacy_spring", C.c_int), ("wall_contact", C.c_int),
     ]
 
 
@@ -112,6 +112,9 @@ def _declare(_lib):
         _lib.orc_flops_read_and_reset.restype = C.c_longlong
         _lib.orc_flops_set_mode.argtypes = [C.c_int]
         _lib.orc_math_check.argtypes = [C.c_int, C.c_int, _FP, _FP, _FP]
+        _lib.orc_contact_stats.argtypes = [C.POINTER(C.c_longlong)]
+        _lib.orc_set_face_cull.argtypes = [C.c_int]
+        _lib.orc_contact_stats_enable.argtypes = [C.c_int]
     return _lib
 
 

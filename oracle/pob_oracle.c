@@ -353,6 +353,7 @@ void orc_default_params(orc_params *p) {
   p->action_repeat = 1;
   p->solver_scale_pos = 0.6f; p->solver_scale_ang = 0.2f;
   p->legacy_spring = 0;
+  p->wall_contact = 1;
 }
 
 /* double-precision config maths (System construction time) */
@@ -570,16 +571,31 @@ void orc_default_qp(const orc_env *e, const float *qpos, const float *qvel, floa
 }
 
 /* ------------------------------------------------------------------------- contacts */
+/* A contact: body, penetration, world normal, radius, and where on the body it sits.  Ground
+ * contacts (CapsulePlane) sit at the body-frame end point e; wall contacts (Ant x Arena) at
+ * the point x + tau * rotate(e0, q) of the capsule's segment (e0 = the capsule's end 0, the
+ * segment is x + [-1, 1] * rotate(e0, q); the torso is a sphere, e0 = 0).  Contacts are kept
+ * in the order ground (collider order), then per capsule its wall contacts in (wall, face,
+ * triangle) order; each body's corrections are accumulated in that order. */
+#define MAXCT (NDYN + NDYN * MAXW * 12)
 typedef struct {
-  float pen[NDYN + NDYN]; /* [0,n_ground): ground contacts; [n_ground, +9): wall per capsule */
-  v3 n[NDYN + NDYN];
-  v3 e[NDYN + NDYN];      /* end point (body frame) */
-  float r[NDYN + NDYN];
-  int body[NDYN + NDYN];
   int count;
+  int body[MAXCT], ground[MAXCT];
+  float pen[MAXCT], r[MAXCT], tau[MAXCT];
+  v3 n[MAXCT], e[MAXCT];
 } contacts_t;
 
-/* sphere (centre p, radius r) vs the z-rotated box w; returns penetration, world normal */
+/* world point of contact k at the body pose (x, q) */
+static inline v3 contact_point(const orc_env *e, const body_t *b, const contacts_t *ct, int k) {
+  const int i = ct->body[k];
+  if (ct->ground[k]) return cpoint(ct->e[k], b->q[i], b->x[i]);
+  FL(6);
+  const v3 rv = qrot(e->cap_end[i][0], b->q[i]);
+  return V(fmaf(rv.x, ct->tau[k], b->x[i].x), fmaf(rv.y, ct->tau[k], b->x[i].y), fmaf(rv.z, ct->tau[k], b->x[i].z));
+}
+
+/* sphere (centre p, radius r) vs the z-rotated box w; returns penetration, world normal
+ * (wall_contact = 1 only: the round-1..3 model) */
 static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
   float c = e->wall_cos[w], s = e->wall_sin[w];
   v3 h = e->wall_h[w];
@@ -608,11 +624,225 @@ static float sphere_box(const orc_env *e, int w, v3 p, float r, v3 *n) {
   return pen;
 }
 
+/* ---- brax v1 capsule x TriangulatedBox (capsule_mesh) [ext, recalled; DESIGN.md §3] ----
+ * brax v1 routes capsule x box pairs through its mesh path: the box collider becomes a
+ * TriangulatedBox (6 faces x 2 triangles) and capsule_mesh returns, for EVERY triangle, the
+ * closest points between the capsule's segment and the triangle, penetration r - |S - P| and
+ * the normal along S - P; the collider applies every penetrating one.  Restated here in the
+ * wall's own frame (the Arena is frozen at the identity rotation; each wall is a box rotated
+ * about z): local = R_z(-theta)(p - c), the same transform as the sphere-box model.  A face is
+ * the plane w = sigma h_k of axis k in face coordinates (a, b, w) = (y, z, x), (x, z, y),
+ * (x, y, z) for k = x, y, z; its rectangle [-ha, ha] x [-hb, hb] is split along the diagonal
+ * V0 = (-ha, -hb) -> V2 = (ha, hb): triangle 0 = (V0, V1 = (ha, -hb), V2), triangle 1 =
+ * (V0, V2, V3 = (-ha, hb)).  Faces in the order -x, +x, -y, +y, -z, +z.
+ *
+ * Closest points of segment S(u) = A + u D (u in [0, 1]) and triangle T: the minimum of the
+ * convex |S(u) - T| is attained at an end point (closest triangle point to A or B), at a
+ * closest pair of the segment and a triangle edge, or where the segment crosses the
+ * triangle's plane inside T -- the candidates below, taken in that order, the first strict
+ * minimum of the squared distance winning (brax's _closest_segment_triangle_points tests
+ * the same three kinds).  Degenerate contact (S on the triangle, |S - P| = 0): the normal is
+ * the face's outward normal and the penetration r.
+ *
+ * Face cull (part of this restatement, applied identically by the kernels): a face whose
+ * rectangle is separated from the segment's axis-aligned bounding box (face coordinates) by
+ * a gap >= r + 1e-3 along some axis is not evaluated -- every point pair is then at least
+ * r + 1e-3 apart, and the float evaluation of its triangles (errors ~1e-6 at these
+ * coordinates) could not produce a penetrating contact.  orc_set_face_cull(0) and the FLOP
+ * counter's reference mode evaluate every face; the results are identical (tests). */
+#define WALL_CULL_MARGIN 1e-3f
+static int g_face_cull = 1;
+void orc_set_face_cull(int on) { g_face_cull = on != 0; }
+
+static long long g_cst[16];
+static int g_cst_on = 0;
+void orc_contact_stats_enable(int on) { g_cst_on = on != 0; }
+void orc_contact_stats(long long out[16]) {
+  for (int i = 0; i < 16; ++i) { out[i] = g_cst[i]; g_cst[i] = 0; }
+}
+#define CST(i, v) do { if (g_cst_on) g_cst[i] += (v); } while (0)
+
+static inline float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+typedef struct { float a, b, w; } f3; /* face coordinates */
+
+/* is (pa, pb) in face triangle t (boundary included)? */
+static inline int tri_inside(int t, float ha, float hb, float pa, float pb) {
+  FL(4);
+  const float cr = fmaf(pa + ha, hb, -((pb + hb) * ha)); /* >= 0: on or below the diagonal */
+  return t == 0 ? (pb >= -hb && pa <= ha && cr >= 0.0f) : (pb <= hb && pa >= -ha && cr <= 0.0f);
+}
+/* closest point (qa, qb) of face triangle t to the face-plane point (pa, pb): the point itself
+ * when inside, else the nearest of the triangle's edges' nearest points (edge order: triangle
+ * 0 bottom, right, diagonal; triangle 1 diagonal, top, left; first strict minimum) */
+static void tri_closest(int t, float ha, float hb, float pa, float pb, float *qa, float *qb) {
+  if (tri_inside(t, ha, hb, pa, pb)) { *qa = pa; *qb = pb; return; }
+  FL(4 + 1 + 8 + 6 + 6);
+  /* diagonal V0 -> V2: s = clamp01(((p - V0) . (ha, hb)) / (ha^2 + hb^2)) */
+  const float s = clamp01(fmaf(pb + hb, hb, (pa + ha) * ha) * (1.0f / fmaf(hb, hb, ha * ha)));
+  const float s2 = 2.0f * s;
+  const float da = fmaf(s2, ha, -ha), db = fmaf(s2, hb, -hb);
+  float ea[3], eb[3];
+  if (t == 0) {
+    ea[0] = fminf(fmaxf(pa, -ha), ha); eb[0] = -hb;  /* bottom V0 -> V1 */
+    ea[1] = ha; eb[1] = fminf(fmaxf(pb, -hb), hb);   /* right V1 -> V2 */
+    ea[2] = da; eb[2] = db;
+  } else {
+    ea[0] = da; eb[0] = db;
+    ea[1] = fminf(fmaxf(pa, -ha), ha); eb[1] = hb;   /* top V2 -> V3 */
+    ea[2] = -ha; eb[2] = fminf(fmaxf(pb, -hb), hb);  /* left V3 -> V0 */
+  }
+  float best = 0.0f;
+  for (int k = 0; k < 3; ++k) {
+    const float ga = pa - ea[k], gb = pb - eb[k];
+    const float d2 = fmaf(gb, gb, ga * ga);
+    if (k == 0 || d2 < best) { best = d2; *qa = ea[k]; *qb = eb[k]; }
+  }
+}
+
+typedef struct { float d2, u; f3 d; } cand_t; /* squared distance, segment parameter, S - P */
+static inline void cand_take(cand_t *c, float u, f3 d) {
+  FL(5);
+  const float d2 = fmaf(d.w, d.w, fmaf(d.b, d.b, d.a * d.a));
+  if (d2 < c->d2) { c->d2 = d2; c->u = u; c->d = d; }
+}
+/* closest points of the segment A + u D and the edge E0 + t F (F in the face plane, F.w = 0):
+ * Ericson's clamped form; ee = F . F, inv_ee = 1 / ee, aa = D . D > 0, inv_aa = 1 / aa */
+static void seg_edge(cand_t *c, f3 A, f3 D, float aa, float inv_aa, float e0a, float e0b, float w0, float fa, float fb,
+                     float ee, float inv_ee) {
+  FL(3 + 3 + 5 + 3 + 3 + 2 + 3);
+  const f3 r = {A.a - e0a, A.b - e0b, A.w - w0};
+  const float f = fmaf(fb, r.b, fa * r.a);
+  const float cc = fmaf(D.w, r.w, fmaf(D.b, r.b, D.a * r.a));
+  const float bb = fmaf(D.b, fb, D.a * fa);
+  const float den = fmaf(aa, ee, -(bb * bb));
+  float u = 0.0f;
+  if (den > 0.0f) { FL(4); u = clamp01(fmaf(bb, f, -(cc * ee)) * (1.0f / den)); }
+  float t = fmaf(bb, u, f) * inv_ee;
+  if (t < 0.0f) { FL(1); t = 0.0f; u = clamp01(-cc * inv_aa); }
+  else if (t > 1.0f) { FL(2); t = 1.0f; u = clamp01((bb - cc) * inv_aa); }
+  FL(6 + 4 + 3);
+  const f3 S = {fmaf(u, D.a, A.a), fmaf(u, D.b, A.b), fmaf(u, D.w, A.w)};
+  const f3 d = {S.a - fmaf(t, fa, e0a), S.b - fmaf(t, fb, e0b), S.w - w0};
+  cand_take(c, u, d);
+}
+
+/* closest points of the segment [A, B] (or the point A when !seg) and face triangle t of the
+ * face w = w0 with half extents (ha, hb) */
+static cand_t seg_tri(int t, float ha, float hb, float w0, f3 A, f3 B, int seg, f3 D, float aa, float inv_aa) {
+  cand_t c; c.d2 = INFINITY; c.u = 0.0f; c.d.a = c.d.b = c.d.w = 0.0f;
+  float qa, qb;
+  tri_closest(t, ha, hb, A.a, A.b, &qa, &qb);
+  FL(3);
+  { const f3 d = {A.a - qa, A.b - qb, A.w - w0}; c.d2 = INFINITY; cand_take(&c, 0.0f, d); }
+  if (!seg) return c;
+  tri_closest(t, ha, hb, B.a, B.b, &qa, &qb);
+  FL(3);
+  { const f3 d = {B.a - qa, B.b - qb, B.w - w0}; cand_take(&c, 1.0f, d); }
+  /* the edges (edge vectors from the face's constant tables: 2ha, 2hb) */
+  const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
+  FL(1 + 1 + 3);
+  const float e_a = ha2 * ha2, e_b = hb2 * hb2, e_d = fmaf(hb2, hb2, ha2 * ha2);
+  const float i_a = 1.0f / e_a, i_b = 1.0f / e_b, i_d = 1.0f / e_d;
+  if (t == 0) {
+    seg_edge(&c, A, D, aa, inv_aa, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);  /* bottom V0 -> V1 */
+    seg_edge(&c, A, D, aa, inv_aa, ha, -hb, w0, 0.0f, hb2, e_b, i_b);   /* right V1 -> V2 */
+    seg_edge(&c, A, D, aa, inv_aa, -ha, -hb, w0, ha2, hb2, e_d, i_d);   /* diagonal V0 -> V2 */
+  } else {
+    seg_edge(&c, A, D, aa, inv_aa, -ha, -hb, w0, ha2, hb2, e_d, i_d);   /* diagonal V0 -> V2 */
+    seg_edge(&c, A, D, aa, inv_aa, ha, hb, w0, -ha2, 0.0f, e_a, i_a);   /* top V2 -> V3 */
+    seg_edge(&c, A, D, aa, inv_aa, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);  /* left V3 -> V0 */
+  }
+  /* the segment crossing the face plane inside the triangle */
+  FL(2);
+  const float aw = A.w - w0, bw = B.w - w0;
+  if ((aw < 0.0f && bw > 0.0f) || (aw > 0.0f && bw < 0.0f)) {
+    FL(3 + 6 + 1);
+    const float u = aw * (1.0f / (aw - bw));
+    const f3 S = {fmaf(u, D.a, A.a), fmaf(u, D.b, A.b), fmaf(u, D.w, A.w)};
+    if (tri_inside(t, ha, hb, S.a, S.b)) { const f3 d = {0.0f, 0.0f, S.w - w0}; cand_take(&c, u, d); }
+  }
+  return c;
+}
+
+/* component k of the wall-local vector (x, y, z) */
+static inline float comp(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+/* the mesh contacts of capsule i (world end points pa, pb; pb unused for the torso) against
+ * wall w, appended to ct */
+static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, contacts_t *ct) {
+  const float c = e->wall_cos[w], s = e->wall_sin[w];
+  const v3 h = e->wall_h[w];
+  const float r = e->cap_r[i];
+  const int seg = e->cap_nend[i] == 2;
+  FL(3 + 6 + (seg ? 9 : 0));
+  const v3 da = vsub(pa, e->wall_c[w]);
+  const v3 La = V(fmaf(da.y, s, da.x * c), fmaf(da.y, c, -(da.x * s)), da.z);
+  v3 Lb = La;
+  if (seg) { const v3 db = vsub(pb, e->wall_c[w]); Lb = V(fmaf(db.y, s, db.x * c), fmaf(db.y, c, -(db.x * s)), db.z); }
+  const float R = r + WALL_CULL_MARGIN;
+  CST(0, 1);
+  int n_hit = 0;
+  for (int f = 0; f < 6; ++f) {
+    const int k = f >> 1, ka = k == 0 ? 1 : 0, kb = k == 2 ? 1 : 2;
+    const float sg = (f & 1) ? 1.0f : -1.0f;
+    const float ha = comp(h, ka), hb = comp(h, kb), w0 = sg * comp(h, k);
+    const f3 A = {comp(La, ka), comp(La, kb), comp(La, k)};
+    const f3 B = {comp(Lb, ka), comp(Lb, kb), comp(Lb, k)};
+#ifdef ORC_COUNT_FLOPS
+    const int cull = g_face_cull && g_flop_mode == 1;
+#else
+    const int cull = g_face_cull;
+#endif
+    if (cull) {
+      FL(6);
+      const float gw = fmaxf(fminf(A.w, B.w) - w0, w0 - fmaxf(A.w, B.w));
+      const float ga = fmaxf(fminf(A.a, B.a) - ha, -ha - fmaxf(A.a, B.a));
+      const float gb = fmaxf(fminf(A.b, B.b) - hb, -hb - fmaxf(A.b, B.b));
+      if (gw >= R || ga >= R || gb >= R) continue;
+    }
+    CST(1, 1);
+    f3 D = {0.0f, 0.0f, 0.0f};
+    float aa = 0.0f, inv_aa = 0.0f;
+    if (seg) {
+      FL(3 + 5 + 1);
+      D.a = B.a - A.a; D.b = B.b - A.b; D.w = B.w - A.w;
+      aa = fmaf(D.w, D.w, fmaf(D.b, D.b, D.a * D.a));
+      inv_aa = 1.0f / aa;
+    }
+    for (int t = 0; t < 2; ++t) {
+      const cand_t cd = seg_tri(t, ha, hb, w0, A, B, seg, D, aa, inv_aa);
+      FL(1);
+      const float dist = sqrtf(cd.d2);
+      const float pen = r - dist;
+      if (!(pen > 0.0f)) continue;
+      f3 nf;
+      if (cd.d2 > 0.0f) { FL(4); const float inv = 1.0f / dist; nf.a = cd.d.a * inv; nf.b = cd.d.b * inv; nf.w = cd.d.w * inv; }
+      else { nf.a = 0.0f; nf.b = 0.0f; nf.w = sg; CST(6, 1); }
+      /* back to wall-local (x, y, z), then to the world */
+      float nl[3]; nl[ka] = nf.a; nl[kb] = nf.b; nl[k] = nf.w;
+      FL(6 + 1);
+      const int m = ct->count++;
+      ct->body[m] = i; ct->ground[m] = 0; ct->pen[m] = pen; ct->r[m] = r;
+      ct->tau[m] = 1.0f - 2.0f * cd.u;
+      ct->n[m] = V(fmaf(-nl[1], s, nl[0] * c), fmaf(nl[1], c, nl[0] * s), nl[2]);
+      ct->e[m] = V(0.0f, 0.0f, 0.0f);
+      ++n_hit;
+      if (g_cst_on) {
+        /* the segment point inside the box? */
+        const float u = cd.u;
+        const v3 S = V(fmaf(u, Lb.x - La.x, La.x), fmaf(u, Lb.y - La.y, La.y), fmaf(u, Lb.z - La.z, La.z));
+        if (fabsf(S.x) < h.x && fabsf(S.y) < h.y && fabsf(S.z) < h.z) CST(5, 1);
+      }
+    }
+  }
+  CST(2, n_hit);
+}
+
 #ifdef ORC_COUNT_FLOPS
 /* FLOP-count mode 1 only (no effect on any result).  The HIP kernel's per-lane broadphase
  * (pob_quad.h qdetect, boxes from pob_system.cpp): lane k of an env holds the torso, Aux
  * k+1 and lower leg k; it walks wall w iff the xy AABB of those three body centres meets
- * the wall's xy box grown by the largest capsule reach (|end| + r) + 1e-3. */
+ * the wall's xy box grown by the largest capsule reach (|end| + r) + 2e-3. */
 static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4]) {
   double reach = 0.0;
   for (int i = 0; i < NDYN; ++i)
@@ -620,7 +850,7 @@ static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4
       const v3 c = e->cap_end[i][q];
       reach = fmax(reach, sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z) + e->cap_r[i]);
     }
-  reach += 1e-3;
+  reach += 2e-3;
   for (int k = 0; k < 4; ++k) {
     const int l[3] = {0, 2 * k + 1, 2 * k + 2};
     float mnx = b->x[0].x, mxx = mnx, mny = b->x[0].y, mxy = mny;
@@ -638,9 +868,9 @@ static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4
     }
   }
 }
-/* operations of one broadphase-surviving sphere-box pair in the kernel (pob_quad.h
- * qwall_end): centre offset, local frame, clamp, distance^2 always; square root, normal
- * and its rotation only when d2 < r^2 (1 + 2^-20) (or the sphere centre is inside) */
+/* operations of one broadphase-surviving sphere-box pair in the kernel (wall_contact = 1):
+ * centre offset, local frame, clamp, distance^2 always; square root, normal and its rotation
+ * only when d2 < r^2 (1 + 2^-20) (or the sphere centre is inside) */
 static long long pair_flops_executed(const orc_env *e, int w, v3 p, float r) {
   const float c = e->wall_cos[w], s = e->wall_sin[w];
   const v3 h = e->wall_h[w];
@@ -656,8 +886,9 @@ static long long pair_flops_executed(const orc_env *e, int w, v3 p, float r) {
 }
 #endif
 
-/* contact detection for the collide substep (ground: CapsulePlane; walls: deepest
- * sphere-box over capsule end points x walls, one contact per capsule). */
+/* contact detection for the collide substep: ground (CapsulePlane on the torso and the four
+ * lower legs), then per capsule its Ant x Arena contacts (wall_contact 0: every penetrating
+ * triangle of every wall; 1: the deepest sphere-box contact over end points x walls). */
 static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   int k = 0;
   for (int g = 0; g < e->n_ground; ++g, ++k) {
@@ -666,16 +897,40 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
     FL(1);
     ct->pen[k] = e->ground_r[g] - pe.z;
     ct->n[k] = V(0.0f, 0.0f, 1.0f);
-    ct->e[k] = e->ground_end[g]; ct->r[k] = e->ground_r[g]; ct->body[k] = i;
+    ct->e[k] = e->ground_end[g]; ct->r[k] = e->ground_r[g]; ct->body[k] = i; ct->ground[k] = 1; ct->tau[k] = 0.0f;
   }
+  ct->count = k;
 #ifdef ORC_COUNT_FLOPS
   uint32_t lane_mask[4] = {0u, 0u, 0u, 0u};
   if (g_flop_mode == 1) kernel_wall_masks(e, b, lane_mask);
 #endif
-  for (int i = 0; i < NDYN; ++i, ++k) {
-    float best = 0.0f; v3 bn = V(0, 0, 0), be = e->cap_end[i][0];
+  if (e->n_walls > 0) CST(7, 1);
+  for (int i = 0; i < NDYN; ++i) {
     v3 pe[2]; /* the capsule's end points in world (independent of the wall) */
     for (int q = 0; q < e->cap_nend[i]; ++q) pe[q] = cpoint(e->cap_end[i][q], b->q[i], b->x[i]);
+#ifdef ORC_COUNT_FLOPS
+    const uint32_t lmask = i == 0 ? (lane_mask[0] | lane_mask[1] | lane_mask[2] | lane_mask[3]) : lane_mask[(i - 1) / 2];
+#endif
+    if (e->p.wall_contact == 0) {
+      const int before = ct->count;
+      for (int w = 0; w < e->n_walls; ++w) {
+#ifdef ORC_COUNT_FLOPS
+        const long long f0 = g_flops;
+#endif
+        capsule_wall_mesh(e, i, w, pe[0], pe[e->cap_nend[i] - 1], ct);
+#ifdef ORC_COUNT_FLOPS
+        if (g_flop_mode == 1 && !((lmask >> w) & 1u)) g_flops = f0;  /* culled by the kernel's broadphase */
+#endif
+      }
+      const int nh = ct->count - before;
+      if (e->n_walls > 0) {
+        CST(3, nh > 0);
+        if (g_cst_on && nh > g_cst[4]) g_cst[4] = nh;
+        CST(8 + (nh < 7 ? nh : 7), 1);
+      }
+      continue;
+    }
+    float best = 0.0f; v3 bn = V(0, 0, 0); float btau = 1.0f;
     for (int w = 0; w < e->n_walls; ++w)
       for (int q = 0; q < e->cap_nend[i]; ++q) {
 #ifdef ORC_COUNT_FLOPS
@@ -683,17 +938,16 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
 #endif
         v3 n; float pen = sphere_box(e, w, pe[q], e->cap_r[i], &n);
 #ifdef ORC_COUNT_FLOPS
-        if (g_flop_mode == 1) {
-          const uint32_t m = i == 0 ? (lane_mask[0] | lane_mask[1] | lane_mask[2] | lane_mask[3])
-                                    : lane_mask[(i - 1) / 2];
-          g_flops = f0 + (((m >> w) & 1u) ? pair_flops_executed(e, w, pe[q], e->cap_r[i]) : 0);
-        }
+        if (g_flop_mode == 1) g_flops = f0 + (((lmask >> w) & 1u) ? pair_flops_executed(e, w, pe[q], e->cap_r[i]) : 0);
 #endif
-        if (pen > best) { best = pen; bn = n; be = e->cap_end[i][q]; }
+        if (pen > best) { best = pen; bn = n; btau = q == 0 ? 1.0f : -1.0f; }
       }
-    ct->pen[k] = best; ct->n[k] = bn; ct->e[k] = be; ct->r[k] = e->cap_r[i]; ct->body[k] = i;
+    if (best > 0.0f) {
+      const int m = ct->count++;
+      ct->pen[m] = best; ct->n[m] = bn; ct->tau[m] = btau; ct->e[m] = V(0, 0, 0);
+      ct->r[m] = e->cap_r[i]; ct->body[m] = i; ct->ground[m] = 0;
+    }
   }
-  ct->count = k;
 }
 
 /* position-level contact projection (normal + static friction) into DX / DA (DA: the
@@ -705,7 +959,7 @@ static void contact_position(const orc_env *e, const body_t *b, const body_t *pr
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = cpoint(ct->e[k], b->q[i], b->x[i]);
+    v3 pe = contact_point(e, b, ct, k);
     v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 cn = vcross(rr, n);
@@ -743,7 +997,7 @@ static void contact_velocity(const orc_env *e, const body_t *b, const contacts_t
     float pen = ct->pen[k];
     if (!(pen > 0.0f)) continue;
     int i = ct->body[k]; v3 n = ct->n[k]; float im = e->inv_mass[i];
-    v3 pe = cpoint(ct->e[k], b->q[i], b->x[i]);
+    v3 pe = contact_point(e, b, ct, k);
     v3 cp = vfma(n, -ct->r[k], pe);
     v3 rr = vsub(cp, b->x[i]);
     v3 vr = vadd(b->v[i], vcross(b->w[i], rr));
@@ -943,7 +1197,7 @@ static void legacy_contacts(const orc_env *e, const body_t *b, v3 *dV, v3 *dW) {
     const float pen = ct.pen[k];
     if (!(pen > 0.0f)) continue;
     const int i = ct.body[k]; const v3 n = ct.n[k];
-    const v3 pe = cpoint(ct.e[k], b->q[i], b->x[i]);
+    const v3 pe = contact_point(e, b, &ct, k);
     const v3 rel = vsub(vfma(n, -ct.r[k], pe), b->x[i]);
     const v3 cv = vadd(b->v[i], vcross(b->w[i], rel));
     const float nv = vdot(n, cv);

@@ -45,6 +45,12 @@ typedef struct orc_params {
   /* dynamics: 0 = PBD (brax 0.0.13-0.0.16 "pbd"), 1 = legacy spring (brax <= 0.0.12, the
    * physics of the notebook trajectory notebooks/ant_tag.ipynb:449) */
   int legacy_spring;
+  /* Ant x Arena contact model: 0 = brax v1 capsule x TriangulatedBox (capsule_mesh: every
+   * box a 12-triangle mesh, closest segment-triangle points, one contact per penetrating
+   * triangle; the reference's algorithm), 1 = the round-1..3 restatement (the
+   * deepest sphere-box contact over the capsule's end points, one per capsule) -- kept only to
+   * measure the divergence between the two */
+  int wall_contact;
 } orc_params;
 
 typedef struct orc_state {
@@ -74,6 +80,17 @@ long long orc_flops_read_and_reset(void);
 /* counter mode: 0 every collider pair (reference algorithm), 1 the pairs the HIP kernel
  * evaluates (its exact culls); returns -1 when the counter is not built */
 int orc_flops_set_mode(int mode);
+/* contact statistics of the mesh contact model (single-threaded runs only; zeroed by the
+ * read): out[0] capsule x wall pairs evaluated, [1] faces surviving the face cull, [2]
+ * triangle contacts, [3] capsule-substeps with >= 1 wall contact, [4] the largest number of
+ * wall contacts of one capsule in one detection, [5] contacts whose segment point lies inside
+ * the box, [6] contacts with a zero distance (segment touching the triangle), [7] detections,
+ * [8..15] histogram of wall contacts per capsule per detection (0..6, >= 7) */
+void orc_contact_stats(long long out[16]);
+void orc_contact_stats_enable(int on);
+/* 0: evaluate every face of every wall (no face cull; the FLOP counter's reference mode does
+ * this too) -- results must be identical to the default (1) */
+void orc_set_face_cull(int on);
 /* test hook: op 0 atan2f(a, b); op 1 substep quaternion normalisation of a (n x 4) */
 void orc_math_check(int op, int n, const float *a, const float *b, float *out);
 
