@@ -353,7 +353,7 @@ void orc_default_params(orc_params *p) {
   p->action_repeat = 1;
   p->solver_scale_pos = 0.6f; p->solver_scale_ang = 0.2f;
   p->legacy_spring = 0;
-  p->wall_contact = 1;
+  p->wall_contact = 0;
 }
 
 /* double-precision config maths (System construction time) */
@@ -842,7 +842,7 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
 /* FLOP-count mode 1 only (no effect on any result).  The HIP kernel's per-lane broadphase
  * (pob_quad.h qdetect, boxes from pob_system.cpp): lane k of an env holds the torso, Aux
  * k+1 and lower leg k; it walks wall w iff the xy AABB of those three body centres meets
- * the wall's xy box grown by the largest capsule reach (|end| + r) + 2e-3. */
+ * the wall's xy box grown by the largest capsule reach (|end| + r) + 1e-3. */
 static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4]) {
   double reach = 0.0;
   for (int i = 0; i < NDYN; ++i)
@@ -850,7 +850,7 @@ static void kernel_wall_masks(const orc_env *e, const body_t *b, uint32_t mask[4
       const v3 c = e->cap_end[i][q];
       reach = fmax(reach, sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z) + e->cap_r[i]);
     }
-  reach += 2e-3;
+  reach += 1e-3;
   for (int k = 0; k < 4; ++k) {
     const int l[3] = {0, 2 * k + 1, 2 * k + 2};
     float mnx = b->x[0].x, mxx = mnx, mny = b->x[0].y, mxy = mny;

@@ -71,29 +71,57 @@ struct HBody {
   q4 q;
 };
 
-struct HContacts {
-  float gpen;  // ground contact (torso and lower legs; -1 otherwise)
-  v3 gpe;      // its sphere centre x + rotate(end, q)
-  float pen;   // deepest wall contact of the body's capsule
-  v3 n, pe;
-  bool sel;
+// the body's ground contact (torso and lower legs; pen -1 otherwise) and its wall contacts
+// (pob_quad.h QMesh: the segment at detection and the contact-bearing items)
+struct HGround {
+  float pen;
+  v3 pe;  // x + rotate(end, q)
+};
+struct HMesh {
+  v3 a, b;
+  uint64_t mc;
 };
 
-// Contact detection of a collide substep on one lane: the body's ground contact and its
-// deepest wall contact over the walls whose grown box (pob_sys::wall_lo/hi) holds the body
-// centre -- exact: a culled pair has every capsule point farther than r from the wall box,
-// penetration < 0, and the strict ">" of the deepest-contact search keeps the oracle's
-// (wall, end) order.  The boxes, the walls' z extent and the wall count come from registers
-// (HWalls); each lane walks its own near-wall mask in increasing wall order reading the rows
-// from LDS (WT), so the wave runs as many iterations as its busiest lane.  (An unrolled walk
-// over all rows held in registers, each behind a wave-uniform guard, runs the union of the
-// walls near any lane: HH B = 4 096 0.0294 ms against 0.0283 for this walk, TAG / GA +0.5 %.)
+// Contacts of a collide substep on one lane (oracle order: ground, then walls in wall / face /
+// triangle order).  Walls: the broadphase over the walls' grown boxes (registers, HWalls) by
+// the body centre, the face items of the lane's body (pob_mesh.h cull), then a walk over them
+// one per lane per iteration with the wall rows from LDS (WT).  The torso is the sphere.
+template <int MW, class G, class F>
+POB_D void hmesh_walk(G &g, const float *HT, const float *WT, const HWalls<MW> &HW, const bool torso, const HMesh &ms,
+                      uint64_t M, uint64_t *hit, F &&emit) {
+  const float r = HT[HT_R];
+  const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
+  while (__any(M != 0ull)) {
+    const bool on = M != 0ull;
+    const int bit = on ? __builtin_ctzll(M) : 0;
+    M &= M - 1ull;
+    if (on) {
+      const int w = bit >> 3, f = bit & 7;
+      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
+      const v3 La = mwall_local(W, HW.cz, ms.a);
+      const v3 Lb = torso ? La : mwall_local(W, HW.cz, ms.b);
+      bool any = false;
+      mesh_face(g, f, La, Lb, !torso, W.hx, W.hy, HW.hz, r, T, [&](const float tau, const v3 nl, const float pen) {
+        any = true;
+        emit(tau, mwall_world_n(W, nl), pen);
+      });
+      if (hit && any) *hit |= 1ull << bit;
+    }
+  }
+}
+
 template <int MW, class G>
-POB_D void hdetect(G &g, const float *HT, const float *WT, const HWalls<MW> &HW, const HBody &b, HContacts &ct) {
-  ct.gpe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
-  ct.gpen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - ct.gpe.z : -1.0f;
+POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
+                              const bool torso, const HBody &b, const v3 px, const q4 pq, HGround &gc, HMesh &ms,
+                              v3 &DX, v3 &DA) {
+  gc.pe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
+  gc.pen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - gc.pe.z : -1.0f;
+  const float im = HT[HT_IM];
+  if (gc.pen > 0.0f) oground_position(g, SC, gc.pen, gc.pe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
+  ms.mc = 0ull;
+  if (MW == 0) return;
   uint32_t m = 0u;
-  if (MW > 0) {
+  {
 #ifdef POB_EXP_NO_WALLS
     const int nw = 0;  // timing experiment only
 #else
@@ -106,30 +134,38 @@ POB_D void hdetect(G &g, const float *HT, const float *WT, const HWalls<MW> &HW,
       m |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
-  float best = 0.0f;
-  v3 bn = V(0.0f, 0.0f, 0.0f), bpe = bn;
-  bool bsel = false;
-  if (MW > 0 && __any(m != 0u)) {
-    const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
-    const v3 pe0 = vadd(b.x, rv), pe1 = vsub(b.x, rv);
-    const float r = HT[HT_R];
-    const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
-    while (__any(m != 0u)) {
-      const bool on = m != 0u;
-      const int w = on ? __builtin_ctz(m) : 0;
-      m &= m - 1u;
-      const float *R = WT + POB_WALL_FLOATS * w;
-      const float2 r01 = *reinterpret_cast<const float2 *>(R);
-      const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
-      const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
-      qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe0, r, T, on, false, best, bn, bsel, bpe);
-      qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe1, r, T, on, true, best, bn, bsel, bpe);
-    }
+  if (!__any(m != 0u)) return;
+  const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
+  ms.a = vadd(b.x, rv);
+  ms.b = vsub(b.x, rv);
+  const float R = HT[HT_R] + POB_MESH_MARGIN;
+  uint64_t M = 0ull;
+  while (__any(m != 0u)) {
+    const bool on = m != 0u;
+    const int w = on ? __builtin_ctz(m) : 0;
+    m &= m - 1u;
+    const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
+    const v3 La = mwall_local(W, HW.cz, ms.a);
+    const v3 Lb = torso ? La : mwall_local(W, HW.cz, ms.b);
+    const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, R);
+    M |= on ? (uint64_t)fm << (8 * w) : 0ull;
   }
-  ct.pen = best;
-  ct.n = bn;
-  ct.sel = bsel;
-  ct.pe = bpe;
+  hmesh_walk<MW>(g, HT, WT, HW, torso, ms, M, &ms.mc, [&](const float tau, const v3 n, const float pen) {
+    owall_position(g, SC, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+  });
+}
+
+template <int MW, class G>
+POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
+                              const bool torso, const HBody &b, const HGround &gc, const HMesh &ms, v3 &dV, v3 &dW) {
+  const float im = HT[HT_IM];
+  if (gc.pen > 0.0f)
+    ocontact_vel_one(g, SC, true, gc.pen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+  if (MW == 0 || !__any(ms.mc != 0ull)) return;
+  const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
+  hmesh_walk<MW>(g, HT, WT, HW, torso, ms, ms.mc, (uint64_t *)nullptr, [&](const float tau, const v3 n, const float pen) {
+    ocontact_vel_pe(g, SC, false, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.v, b.w, dV, dW);
+  });
 }
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
@@ -180,7 +216,8 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
   }
   HSUB_T(0)
   // 3. position projection
-  HContacts ct;
+  HGround gc;
+  HMesh ms;
   {
     v3 DX, DA;
     {
@@ -234,16 +271,8 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     }
     HSUB_T(1)
     if (COLLIDE) {
-      hdetect<MW>(g, HT, WT, HW, b, ct);
+      hcontacts_position<MW>(g, SC, HT, WT, HW, torso, b, px, pq, gc, ms, DX, DA);
       HSUB_T(4)
-#ifdef POB_EXP_NO_WALL_RESPONSE  // timing experiment only: detection kept, no wall response
-      asm volatile("" ::"v"(ct.pen), "v"(ct.n.x), "v"(ct.n.y), "v"(ct.n.z), "v"(ct.pe.x), "v"(ct.pe.y), "v"(ct.pe.z));
-      ct.pen = -1.0f;
-#endif
-      const float im = HT[HT_IM];
-      if (ct.gpen > 0.0f) oground_position(g, SC, ct.gpen, ct.gpe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
-      HSUB_T(5)
-      if (ct.pen > 0.0f) owall_position(g, SC, ct.pen, ct.pe, ct.n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
     }
     b.x = vadd(b.x, DX);
     qadd_half(b.q, qmul_vq(DA, b.q), 1.0f);
@@ -262,15 +291,8 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
   // 5. velocity-level contacts (ground first, then wall: the oracle's per-body order)
   if (COLLIDE) {
     v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
-    const float im = HT[HT_IM];
-    if (ct.gpen > 0.0f)
-      ocontact_vel_one(g, SC, true, ct.gpen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
+    hcontacts_velocity<MW>(g, SC, HT, WT, HW, torso, b, gc, ms, dV, dW);
     HSUB_T(7)
-    if (ct.pen > 0.0f) {
-      const v3 e0 = HTV(HT, HT_E0);
-      const v3 e = ct.sel ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(g, SC, false, ct.pen, e, ct.n, HT[HT_R], im, b.x, b.q, b.v, b.w, dV, dW);
-    }
     b.v = vadd(b.v, dV); b.w = vadd(b.w, dW);
     cv = vadd(cv, dV);
     ca = vadd(ca, dW);

@@ -2094,12 +2094,10 @@ POB_D void qreset_compute(csys_t *Sp, const float *LT, const float *WT, const in
   R.ts[2] = __builtin_amdgcn_s_memtime();
 #endif
   // sys.info(qp).contact: contact detection + velocity-level solve at the static qp
-  QContacts ct;
-  qdetect<KIND != POB_ANT>(Sp, LT, WT, b, ct);
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { R.cv[l] = V(0.0f, 0.0f, 0.0f); R.ca[l] = V(0.0f, 0.0f, 0.0f); }
-  if (S.legacy) qlegacy_contacts(Sp, LT, b, ct, R.cv, R.ca);  // legacy sys.info: the colliders' impulses
-  else qcontact_velocity(Sp, LT, b, ct, R.cv, R.ca, S.friction);
+  if (S.legacy) qcontacts_static<KIND != POB_ANT, true>(Sp, LT, WT, b, R.cv, R.ca, S.friction);  // the colliders' impulses
+  else qcontacts_static<KIND != POB_ANT, false>(Sp, LT, WT, b, R.cv, R.ca, S.friction);
 #ifdef POB_EXP_TIMING
   R.ts[3] = __builtin_amdgcn_s_memtime();
 #endif

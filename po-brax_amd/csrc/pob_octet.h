@@ -65,13 +65,15 @@ POB_D v3 vsel(bool c, v3 a, v3 b) { return V(c ? a.x : b.x, c ? a.y : b.y, c ? a
 // obs rows and the qp stores go through it
 #define OL_FLOATS 26
 
-struct OContacts {
-  float gpen;          // ground contact of the lane's ground body (A: torso, B: lower leg)
-  v3 gpe;              // its sphere centre (x + rotate(end, q))
-  float pen[ONB];      // deepest wall contact of slot s
-  v3 n[ONB];
-  bool sel[ONB];
-  v3 pe[ONB];
+// ground contact of the lane's ground body (A: torso, B: lower leg) and the wall contacts of
+// its two slots (pob_quad.h QMesh: the segments at detection and the contact-bearing items)
+struct OGround {
+  float pen;
+  v3 pe;  // x + rotate(end, q)
+};
+struct OMesh {
+  v3 a[ONB], b[ONB];
+  uint64_t mc[ONB];
 };
 
 // slot s's capsule end points x +- rotate(e0, q) (torso: e0 = 0, both = x)
@@ -99,11 +101,6 @@ struct HWalls {
   float s_pos, friction;
   int n_walls;
 };
-// the contact functions' view of the table (oground_position / owall_position /
-// ocontact_vel_one read S.friction and S.inv_h only)
-struct HCon {
-  float friction, inv_h;
-};
 // Fill the wall table's HW_FLOATS entries (lanes 0 .. HW_FLOATS - 1 of the block's first wave
 // write one each) and, after the caller's LDS sync, read it into registers.
 POB_D void hwalls_stage(csys_t &S, float *tab, const int lane) {
@@ -127,25 +124,73 @@ POB_D void hwalls_load(const float *tab, HWalls<MW> &HW) {
   HW.n_walls = __float_as_int(tab[HW_CZ + 4]);
 }
 
-// Contact detection of a collide substep on one lane: the ground contact of its ground
-// body and, per slot, the deepest wall contact over the walls near the lane's two body
-// centres (qdetect's exact per-lane broadphase and d2 pre-cull).  The broadphase boxes, the
-// walls' z extent and the contact scalars come from registers (HWalls); each lane walks its
-// own near-wall mask reading the rows from LDS (WT).  (An unrolled walk over register rows
-// with a wave-uniform guard per wall measured equal or slower: TAG / GA B = 8 192 ±1 %, HH
-// B = 16 384 +5 %.)  Culled pairs have penetration < 0 and the walk keeps the oracle's
-// (wall, end) order with the strict ">", so the deepest contact is unchanged.
+// Contacts of a collide substep on one lane (oracle order per body: ground, then walls in
+// wall / face / triangle order).  Walls: the lane's broadphase mask over its two body centres
+// (the boxes from registers, HWalls), the face items per slot (pob_mesh.h cull), then a walk
+// over the items one per lane per iteration with the wall rows from LDS (WT).  The torso (A
+// slot 0) is the sphere: its segment is the point x (e0 = 0).
+template <int MW, class G, class F>
+POB_D void omesh_walk(G &g, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, const OMesh &ms,
+                      uint64_t (&M)[ONB], uint64_t (*hit)[ONB], F &&emit) {
+  while (__any((M[0] | M[1]) != 0ull)) {
+    const int s = M[0] != 0ull ? 0 : 1;
+    const uint64_t ml = s == 0 ? M[0] : M[1];
+    const bool on = ml != 0ull;
+    const int bit = on ? __builtin_ctzll(ml) : 0;
+    const uint64_t rest = ml & (ml - 1ull);
+    M[0] = s == 0 ? rest : M[0];
+    M[1] = s == 1 ? rest : M[1];
+    if (on) {
+      const int w = bit >> 3, f = bit & 7;
+      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
+      const v3 A = vsel3(s == 0, ms.a[0], ms.a[1]), B = vsel3(s == 0, ms.b[0], ms.b[1]);
+      const float r = s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1];
+      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
+      const bool seg = !(isA && s == 0);
+      const v3 La = mwall_local(W, HW.cz, A);
+      const v3 Lb = seg ? mwall_local(W, HW.cz, B) : La;
+      bool any = false;
+      mesh_face(g, f, La, Lb, seg, W.hx, W.hy, HW.hz, r, T, [&](const float tau, const v3 nl, const float pen) {
+        any = true;
+        emit(s, tau, mwall_world_n(W, nl), pen);
+      });
+      if (hit && any) {
+        const uint64_t bb = 1ull << bit;
+        (*hit)[0] |= s == 0 ? bb : 0ull;
+        (*hit)[1] |= s == 1 ? bb : 0ull;
+      }
+    }
+  }
+}
+
 template <int MW, class G>
-POB_D void odetect(G &g, const float *OT, const float *WT, const HWalls<MW> &HW, const bool gslot1, const OBody &b,
-                   OContacts &ct) {
+POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
+                              const bool isA, const OBody &b, const v3 (&pxs)[ONB], const q4 (&pqs)[ONB],
+                              OGround &gc, OMesh &ms, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
+  const bool gslot1 = !isA;
   {
     const v3 xg = vsel3(gslot1, b.x[1], b.x[0]);
     const q4 qg = qsel(gslot1, b.q[1], b.q[0]);
-    ct.gpe = vadd(xg, qrot_xy(OTV(OT, OT_G), qg));
-    ct.gpen = OT[OT_G + 3] - ct.gpe.z;
+    gc.pe = vadd(xg, qrot_xy(OTV(OT, OT_G), qg));
+    gc.pen = OT[OT_G + 3] - gc.pe.z;
+  }
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    const bool gs = (s == 1) == gslot1;  // this slot holds the lane's ground body
+    if (gs && gc.pen > 0.0f)
+      oground_position(g, SC, gc.pen, gc.pe, OT[OT_G + 3], OT[OT_B(s)], b.x[s], b.q[s], pqs[s], pxs[s], DX[s], DA[s]);
+  }
+  ms.mc[0] = 0ull; ms.mc[1] = 0ull;
+  if (MW == 0) return;
+  v3 rv[ONB];
+#pragma unroll
+  for (int s = 0; s < ONB; ++s) {
+    rv[s] = qrot_xy(OTV(OT, OT_B(s) + 2), b.q[s]);
+    ms.a[s] = vadd(b.x[s], rv[s]);
+    ms.b[s] = vsub(b.x[s], rv[s]);
   }
   uint32_t lane_mask = 0u;
-  if (MW > 0) {
+  {
     const float mnx = fminf(b.x[0].x, b.x[1].x), mxx = fmaxf(b.x[0].x, b.x[1].x);
     const float mny = fminf(b.x[0].y, b.x[1].y), mxy = fmaxf(b.x[0].y, b.x[1].y);
 #ifdef POB_EXP_NO_WALLS
@@ -159,173 +204,64 @@ POB_D void odetect(G &g, const float *OT, const float *WT, const HWalls<MW> &HW,
       lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
-  const bool any_near = MW > 0 && __any(lane_mask != 0u);
+  uint64_t M[ONB] = {0ull, 0ull};
+  {
+    const float R0 = OT[OT_B(0) + 1] + POB_MESH_MARGIN, R1 = OT[OT_B(1) + 1] + POB_MESH_MARGIN;
+    uint32_t m = lane_mask;
+    while (__any(m != 0u)) {
+      const bool on = m != 0u;
+      const int w = on ? __builtin_ctz(m) : 0;
+      m &= m - 1u;
+      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
 #pragma unroll
-  for (int s = 0; s < ONB; ++s) {
-    float best = 0.0f;
-    v3 bn = V(0.0f, 0.0f, 0.0f);
-    bool bsel = false;
-    v3 bpe = bn;
-    if (any_near) {
-      v3 pe[2];
-      ocap_points(OT, b, s, pe[0], pe[1]);
-      const float r = OT[OT_B(s) + 1];
-      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), as qdetect
-      uint32_t m = lane_mask;
-      while (__any(m != 0u)) {
-        const bool on = m != 0u;
-        const int w = on ? __builtin_ctz(m) : 0;
-        m &= m - 1u;
-        const float *R = WT + POB_WALL_FLOATS * w;
-        const float2 r01 = *reinterpret_cast<const float2 *>(R);
-        const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
-        const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          qwall_end_vz(g, HW.hz, HW.cz, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
+      for (int s = 0; s < ONB; ++s) {
+        const bool seg = !(isA && s == 0);
+        const v3 La = mwall_local(W, HW.cz, ms.a[s]);
+        const v3 Lb = seg ? mwall_local(W, HW.cz, ms.b[s]) : La;
+        const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, s == 0 ? R0 : R1);
+        M[s] |= on ? (uint64_t)fm << (8 * w) : 0ull;
       }
     }
-    ct.pen[s] = best;
-    ct.n[s] = bn;
-    ct.sel[s] = bsel;
-    ct.pe[s] = bpe;
   }
+  omesh_walk<MW>(g, OT, WT, HW, isA, ms, M, &ms.mc, [&](const int s, const float tau, const v3 n, const float pen) {
+    const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
+    const q4 q = qsel(s == 0, b.q[0], b.q[1]);
+    const v3 pe = vfma(vsel3(s == 0, rv[0], rv[1]), tau, x);
+    v3 dx = vsel3(s == 0, DX[0], DX[1]), da = vsel3(s == 0, DA[0], DA[1]);
+    owall_position(g, SC, pen, pe, n, s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1], s == 0 ? OT[OT_B(0)] : OT[OT_B(1)],
+                   x, q, qsel(s == 0, pqs[0], pqs[1]), vsel3(s == 0, pxs[0], pxs[1]), dx, da);
+    DX[0] = vsel3(s == 0, dx, DX[0]); DX[1] = vsel3(s == 1, dx, DX[1]);
+    DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
+  });
 }
 
-// position-level ground contact (n = +z; qcontact_position's ground branch) on body (x, q)
-template <class G = GuardBranch, class SS = csys_t>
-POB_D void oground_position(G &g, const SS &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
-                            const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
-  const v3 cp = V(pe.x, pe.y, pe.z - rad);
-  const v3 rr = vsub(cp, x);
-  const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
-  const float lam = (pen * g.rcp(w));
-  DX.z = FMA(lam, im, DX.z);  // P = (0, 0, lam)
-  DA = V(DA.x + rr.y * lam, DA.y + -(rr.x * lam), DA.z);  // rr x P
-  const v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
-  const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
-  float lt, inv;
-  g.sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
-  if (lt > 0.0f) {
-    const float tx = dpx * inv, ty = dpy * inv;
-    const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
-    const float wt = im + vdot(ctn, ctn);
-    const float lamt = (lt * g.rcp(wt));
-    if (lamt < S.friction * lam) {
-      const float px_ = tx * -lamt, py_ = ty * -lamt;
-      DX.x = FMA(px_, im, DX.x);
-      DX.y = FMA(py_, im, DX.y);
-      DA = vadd(DA, V(-(rr.z * py_), rr.z * px_, FMA(rr.x, py_, -(rr.y * px_))));  // rr x Pt
-    }
-  }
-}
-
-// position-level wall contact (qcontact_position's general branch)
-template <class G = GuardBranch, class SS = csys_t>
-POB_D void owall_position(G &g, const SS &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
-                          const v3 x, const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
-  v3 cp = vfma(n, -rad, pe);
-  v3 rr = vsub(cp, x);
-  v3 cn = vcross(rr, n);
-  float w = im + vdot(cn, cn);
-  float lam = (pen * g.rcp(w));
-  v3 P = vscl(n, lam);
-  DX = vfma(P, im, DX);
-  DA = vadd(DA, vcross(rr, P));
-  v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
-  v3 dp = vsub(cp, cprev);
-  v3 dpt = vfma(n, -vdot(dp, n), dp);
-  float lt, ilt;
-  g.sqrt_rcp(vdot(dpt, dpt), lt, ilt);
-  if (lt > 0.0f) {
-    v3 t = vscl(dpt, ilt);
-    v3 ctn = vcross(rr, t);
-    float wt = im + vdot(ctn, ctn);
-    float lamt = (lt * g.rcp(wt));
-    if (lamt < S.friction * lam) {
-      v3 Pt = vscl(t, -lamt);
-      DX = vfma(Pt, im, DX);
-      DA = vadd(DA, vcross(rr, Pt));
-    }
-  }
-}
-
-// contact processing order of one body = the oracle's: ground contact first, then wall
-template <class G>
-POB_D void ocontact_position(G &gd, const HCon &SC, const float *OT, const bool gslot1, const OBody &b,
-                             const v3 (&pxs)[ONB], const q4 (&pqs)[ONB], const OContacts &ct, v3 (&DX)[ONB],
-                             v3 (&DA)[ONB]) {
+template <int MW, class G>
+POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
+                              const bool isA, const OBody &b, const OGround &gc, const OMesh &ms, v3 (&dV)[ONB],
+                              v3 (&dW)[ONB]) {
+  const bool gslot1 = !isA;
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
-    const float im = OT[OT_B(s)];
-    const q4 pq = pqs[s];
-    const v3 px = pxs[s];
-    const bool g = (s == 1) == gslot1;  // this slot holds the lane's ground body
-    if (g && ct.gpen > 0.0f) oground_position(gd, SC, ct.gpen, ct.gpe, OT[OT_G + 3], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
-    if (ct.pen[s] > 0.0f)
-      owall_position(gd, SC, ct.pen[s], ct.pe[s], ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], pq, px, DX[s], DA[s]);
+    const bool gs = (s == 1) == gslot1;
+    if (gs && gc.pen > 0.0f)
+      ocontact_vel_one(g, SC, true, gc.pen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], OT[OT_B(s)], b.x[s],
+                       b.q[s], b.v[s], b.w[s], dV[s], dW[s]);
   }
-}
-
-// velocity-level contact (qcontact_velocity's body of one contact); e = the body-frame end
-template <class G = GuardBranch, class SS = csys_t>
-POB_D void ocontact_vel_one(G &g, const SS &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
-                            const float im, const v3 x, const q4 q, const v3 v, const v3 w, v3 &dV, v3 &dW) {
-  v3 pe = vadd(x, qrot_xy(e, q));
-  v3 cp = vfma(n, -rad, pe);
-  v3 rr = vsub(cp, x);
-  v3 vr = vadd(v, vcross(w, rr));
-  v3 dv = V(0.0f, 0.0f, 0.0f);
-  if (ground) {
-    const float vn = vr.z;
-    float lt, ilt;
-    g.sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
-    if (lt > 0.0f) {
-      const float fr = fminf(S.friction * pen * S.inv_h, lt);
-      const float k = -(fr * ilt);
-      dv = V(vr.x * k, vr.y * k, 0.0f);
-    }
-    if (vn < 0.0f) dv.z = -vn;
-  } else {
-    float vn = vdot(vr, n);
-    v3 vt = vfma(n, -vn, vr);
-    float lt, ilt;
-    g.sqrt_rcp(vdot(vt, vt), lt, ilt);
-    if (lt > 0.0f) {
-      float fr = fminf(S.friction * pen * S.inv_h, lt);
-      dv = vscl(vt, -(fr * ilt));
-    }
-    if (vn < 0.0f) dv = vfma(n, -vn, dv);
-  }
-  float D, iD;
-  g.sqrt_rcp(vdot(dv, dv), D, iD);
-  if (D > 0.0f) {
-    v3 dh = vscl(dv, iD);
-    v3 cd = vcross(rr, dh);
-    float wgt = im + vdot(cd, cd);
-    v3 P = vscl(dv, g.rcp(wgt));
-    dV = vfma(P, im, dV);
-    dW = vadd(dW, vcross(rr, P));
-  }
-}
-
-template <class G>
-POB_D void ocontact_velocity(G &gd, const HCon &SC, const float *OT, const bool gslot1, const OBody &b,
-                             const OContacts &ct, v3 (&dV)[ONB], v3 (&dW)[ONB]) {
-#pragma unroll
-  for (int s = 0; s < ONB; ++s) {
-    const float im = OT[OT_B(s)];
-    const bool g = (s == 1) == gslot1;
-    if (g && ct.gpen > 0.0f)
-      ocontact_vel_one(gd, SC, true, ct.gpen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], im, b.x[s], b.q[s], b.v[s],
-                       b.w[s], dV[s], dW[s]);
-    if (ct.pen[s] > 0.0f) {
-      const v3 e0 = OTV(OT, OT_B(s) + 2);
-      const v3 e = ct.sel[s] ? V(-e0.x, -e0.y, -e0.z) : e0;
-      ocontact_vel_one(gd, SC, false, ct.pen[s], e, ct.n[s], OT[OT_B(s) + 1], im, b.x[s], b.q[s], b.v[s], b.w[s], dV[s],
-                       dW[s]);
-    }
-  }
+  if (MW == 0) return;
+  uint64_t M[ONB] = {ms.mc[0], ms.mc[1]};
+  if (!__any((M[0] | M[1]) != 0ull)) return;
+  omesh_walk<MW>(g, OT, WT, HW, isA, ms, M, (uint64_t(*)[ONB]) nullptr,
+                 [&](const int s, const float tau, const v3 n, const float pen) {
+    const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
+    const q4 q = qsel(s == 0, b.q[0], b.q[1]);
+    const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), tau, x);
+    v3 dv = vsel3(s == 0, dV[0], dV[1]), dw = vsel3(s == 0, dW[0], dW[1]);
+    ocontact_vel_pe(g, SC, false, pen, pe, n, s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1],
+                    s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]), vsel3(s == 0, b.w[0], b.w[1]),
+                    dv, dw);
+    dV[0] = vsel3(s == 0, dv, dV[0]); dV[1] = vsel3(s == 1, dv, dV[1]);
+    dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
+  });
 }
 
 // timing experiment only (POB_EXP_TIMING_SUB): shader-clock durations of the eight- and
@@ -438,8 +374,8 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
   }
   HSUB_T(0)
   // 3. position projection
-  OContacts ct;
-  const bool gslot1 = !isA;
+  OGround gc;
+  OMesh ms;
   {
     v3 DX[ONB], DA[ONB];
     POB_FENCE();
@@ -473,10 +409,8 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     }
     HSUB_T(1)
     if (COLLIDE) {
-      odetect<MW>(g, OT, WT, HW, gslot1, b, ct);
+      ocontacts_position<MW>(g, SC, OT, WT, HW, isA, b, px, pq, gc, ms, DX, DA);
       HSUB_T(4)
-      ocontact_position(g, SC, OT, gslot1, b, px, pq, ct, DX, DA);
-      HSUB_T(5)
     }
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
@@ -502,7 +436,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     v3 dV[ONB], dW[ONB];
 #pragma unroll
     for (int s = 0; s < ONB; ++s) { dV[s] = V(0.0f, 0.0f, 0.0f); dW[s] = V(0.0f, 0.0f, 0.0f); }
-    ocontact_velocity(g, SC, OT, gslot1, b, ct, dV, dW);
+    ocontacts_velocity<MW>(g, SC, OT, WT, HW, isA, b, gc, ms, dV, dW);
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);

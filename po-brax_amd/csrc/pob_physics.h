@@ -1,7 +1,6 @@
 // pob_physics.h -- shared physics pieces of the rollout kernels (gfx950): the system-table
-// access helpers, the per-lane LDS view, sphere-box and the whole-ant (one lane) contact
-// detection + velocity-level contact solve used by the reset kernel's sys.info(qp)
-// (a2).  The step itself runs four lanes per env (pob_quad.h).
+// access helpers, the per-lane LDS view and one contact's position / velocity / legacy
+// impulse response (the contacts themselves: ground in each kernel, walls pob_mesh.h).
 //
 // Algorithm = brax v1 System.step with dynamics_mode "pbd" as restated in DESIGN.md §3
 // (brax is not vendored: reference call sites ant_heavenhell.py:108, ant_gather.py:127,
@@ -9,20 +8,13 @@
 #pragma once
 #include "pob_math.h"
 #include "pob_sys.h"
+#include "pob_mesh.h"
 
 struct Body {
   v3 x[POB_NDYN];
   q4 q[POB_NDYN];
   v3 v[POB_NDYN];
   v3 w[POB_NDYN];
-};
-
-struct Contacts {
-  // [0, 5): ground (CapsulePlane, normal +z, end point S.ground_end[k]),
-  // [5, 14): deepest wall contact of capsule i (normal n[i], end point cap_end[i][sel[i]])
-  float pen[POB_NGROUND + POB_NDYN];
-  v3 n[POB_NDYN];
-  bool sel[POB_NDYN];
 };
 
 // launder(): with POB_LAUNDER the table pointer is hidden from loop-invariant code motion
@@ -68,147 +60,142 @@ POB_D constexpr int contact_body(int k) { return k < POB_NGROUND ? 2 * k : k - P
 
 #define SV(a) V((a)[0], (a)[1], (a)[2])
 
-// sphere (centre p, radius r) vs z-rotated box w -> penetration, world normal
-POB_D float sphere_box(csys_t &S, int w, v3 p, float r, v3 &n) {
-  const float c = S.wall_cos[w], s = S.wall_sin[w];
-  const v3 h = SV(S.wall_h[w]);
-  v3 d = vsub(p, SV(S.wall_c[w]));
-  float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
-  float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
-  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
-  float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
-  float pen, nx, ny, nz;
-  if (d2 > 0.0f) {
-    float dist, inv;
-    pob_sqrt_rcp(d2, dist, inv);
-    pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
+// ------------------------------------------------------------------ contact responses
+// One contact's position-level projection (normal + static friction) and velocity-level solve
+// (dynamic friction + inelastic normal) on its body (oracle contact_position /
+// contact_velocity, shared by every kernel).  pe = the contact's sphere centre (the capsule
+// point x + rotate(end, q), or x + tau rotate(e0, q) for a wall contact), n the world normal.
+// (the contact functions' view of the table: S.friction and S.inv_h)
+struct HCon {
+  float friction, inv_h;
+};
+// position-level ground contact (n = +z: the general form with the products by the normal's
+// exact zeros dropped, same values up to the sign of a zero)
+template <class G = GuardBranch, class SS = HCon>
+POB_D void oground_position(G &g, const SS &S, const float pen, const v3 pe, const float rad, const float im, const v3 x,
+                            const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
+  const v3 cp = V(pe.x, pe.y, pe.z - rad);
+  const v3 rr = vsub(cp, x);
+  const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
+  const float lam = (pen * g.rcp(w));
+  DX.z = FMA(lam, im, DX.z);  // P = (0, 0, lam)
+  DA = V(DA.x + rr.y * lam, DA.y + -(rr.x * lam), DA.z);  // rr x P
+  const v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
+  const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
+  float lt, inv;
+  g.sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
+  if (lt > 0.0f) {
+    const float tx = dpx * inv, ty = dpy * inv;
+    const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
+    const float wt = im + vdot(ctn, ctn);
+    const float lamt = (lt * g.rcp(wt));
+    if (lamt < S.friction * lam) {
+      const float px_ = tx * -lamt, py_ = ty * -lamt;
+      DX.x = FMA(px_, im, DX.x);
+      DX.y = FMA(py_, im, DX.y);
+      DA = vadd(DA, V(-(rr.z * py_), rr.z * px_, FMA(rr.x, py_, -(rr.y * px_))));  // rr x Pt
+    }
+  }
+}
+
+// position-level wall contact (the general form)
+template <class G = GuardBranch, class SS = HCon>
+POB_D void owall_position(G &g, const SS &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
+                          const v3 x, const q4 q, const q4 pq, const v3 px, v3 &DX, v3 &DA) {
+  v3 cp = vfma(n, -rad, pe);
+  v3 rr = vsub(cp, x);
+  v3 cn = vcross(rr, n);
+  float w = im + vdot(cn, cn);
+  float lam = (pen * g.rcp(w));
+  v3 P = vscl(n, lam);
+  DX = vfma(P, im, DX);
+  DA = vadd(DA, vcross(rr, P));
+  v3 cprev = qrot_add(qrot(rr, qinv(q)), pq, px);
+  v3 dp = vsub(cp, cprev);
+  v3 dpt = vfma(n, -vdot(dp, n), dp);
+  float lt, ilt;
+  g.sqrt_rcp(vdot(dpt, dpt), lt, ilt);
+  if (lt > 0.0f) {
+    v3 t = vscl(dpt, ilt);
+    v3 ctn = vcross(rr, t);
+    float wt = im + vdot(ctn, ctn);
+    float lamt = (lt * g.rcp(wt));
+    if (lamt < S.friction * lam) {
+      v3 Pt = vscl(t, -lamt);
+      DX = vfma(Pt, im, DX);
+      DA = vadd(DA, vcross(rr, Pt));
+    }
+  }
+}
+
+// velocity-level contact at the contact point pe (ground: n = +z with the zero products dropped)
+template <class G = GuardBranch, class SS = HCon>
+POB_D void ocontact_vel_pe(G &g, const SS &S, const bool ground, const float pen, const v3 pe, const v3 n,
+                           const float rad, const float im, const v3 x, const v3 v, const v3 w, v3 &dV, v3 &dW) {
+  v3 cp = vfma(n, -rad, pe);
+  v3 rr = vsub(cp, x);
+  v3 vr = vadd(v, vcross(w, rr));
+  v3 dv = V(0.0f, 0.0f, 0.0f);
+  if (ground) {
+    const float vn = vr.z;
+    float lt, ilt;
+    g.sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
+    if (lt > 0.0f) {
+      const float fr = fminf(S.friction * pen * S.inv_h, lt);
+      const float k = -(fr * ilt);
+      dv = V(vr.x * k, vr.y * k, 0.0f);
+    }
+    if (vn < 0.0f) dv.z = -vn;
   } else {
-    float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
-    nx = 0.0f; ny = 0.0f; nz = 0.0f;
-    if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
-    else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
-    else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
-  }
-  n = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
-  return pen;
-}
-
-// Contact detection of a collide substep: CapsulePlane on the torso and the four feet,
-// and for every capsule its deepest sphere-box contact over (wall, segment end).
-POB_D void detect(csys_t *Sp, const Body &b, Contacts &ct) {
-#pragma unroll
-  for (int g = 0; g < POB_NGROUND; ++g) {
-    csys_t &S = *launder(Sp);
-    const int i = ground_body(g);
-    v3 pe = vadd(b.x[i], qrot(SV(S.ground_end[g]), b.q[i]));
-    ct.pen[g] = S.ground_r[g] - pe.z;
-  }
-  // wave-uniform broadphase: bit w set iff some lane's body-centre AABB meets wall w's grown box
-  uint32_t near_mask = 0u;
-  {
-    v3 mn = b.x[0], mx = b.x[0];
-#pragma unroll
-    for (int i = 1; i < POB_NDYN; ++i) {
-      mn = V(fminf(mn.x, b.x[i].x), fminf(mn.y, b.x[i].y), fminf(mn.z, b.x[i].z));
-      mx = V(fmaxf(mx.x, b.x[i].x), fmaxf(mx.y, b.x[i].y), fmaxf(mx.z, b.x[i].z));
+    float vn = vdot(vr, n);
+    v3 vt = vfma(n, -vn, vr);
+    float lt, ilt;
+    g.sqrt_rcp(vdot(vt, vt), lt, ilt);
+    if (lt > 0.0f) {
+      float fr = fminf(S.friction * pen * S.inv_h, lt);
+      dv = vscl(vt, -(fr * ilt));
     }
-    csys_t &S = *launder(Sp);
-    const int nw = S.n_walls;
-    for (int w = 0; w < nw; ++w) {
-      const bool near = mn.x <= S.wall_hi[w][0] && mx.x >= S.wall_lo[w][0] && mn.y <= S.wall_hi[w][1] &&
-                        mx.y >= S.wall_lo[w][1] && mn.z <= S.wall_hi[w][2] && mx.z >= S.wall_lo[w][2];
-      if (__any(near)) near_mask |= 1u << w;
-    }
+    if (vn < 0.0f) dv = vfma(n, -vn, dv);
   }
-#pragma unroll
-  for (int i = 0; i < POB_NDYN; ++i) {
-    POB_FENCE();
-    csys_t &S = *launder(Sp);
-    const int nend = (i == 0) ? 1 : 2;
-    v3 pe[2];
-#pragma unroll
-    for (int q = 0; q < nend; ++q) pe[q] = vadd(b.x[i], qrot(SV(S.cap_end[i][q]), b.q[i]));
-    float best = 0.0f;
-    v3 bn = V(0.0f, 0.0f, 0.0f);
-    bool bsel = false;
-    const float r = S.cap_r[i];
-    const int nw = S.n_walls;
-    for (int w = 0; w < nw; ++w) {
-      if (!(near_mask & (1u << w))) continue;  // uniform: no lane can touch wall w
-#pragma unroll
-      for (int q = 0; q < nend; ++q) {
-        v3 n;
-        float pen = sphere_box(*launder(Sp), w, pe[q], r, n);
-        if (pen > best) { best = pen; bn = n; bsel = q == 1; }
-      }
-    }
-    ct.pen[POB_NGROUND + i] = best;
-    ct.n[i] = bn;
-    ct.sel[i] = bsel;
+  float D, iD;
+  g.sqrt_rcp(vdot(dv, dv), D, iD);
+  if (D > 0.0f) {
+    v3 dh = vscl(dv, iD);
+    v3 cd = vcross(rr, dh);
+    float wgt = im + vdot(cd, cd);
+    v3 P = vscl(dv, g.rcp(wgt));
+    dV = vfma(P, im, dV);
+    dW = vadd(dW, vcross(rr, P));
   }
 }
-
-// contact k: body frame end point, world normal, radius
-POB_D void contact_geom(csys_t &S, const Contacts &ct, int k, v3 &e, v3 &n, float &r) {
-  if (k < POB_NGROUND) {
-    e = SV(S.ground_end[k]);
-    n = V(0.0f, 0.0f, 1.0f);
-    r = S.ground_r[k];
-  } else {
-    const int i = k - POB_NGROUND;
-    const v3 e0 = SV(S.cap_end[i][0]), e1 = SV(S.cap_end[i][1]);
-    e = ct.sel[i] ? e1 : e0;
-    n = ct.n[i];
-    r = S.cap_r[i];
-  }
+// the same with the body-frame end point e (pe = x + rotate(e, q), e in the body xy-plane)
+template <class G = GuardBranch, class SS = HCon>
+POB_D void ocontact_vel_one(G &g, const SS &S, const bool ground, const float pen, const v3 e, const v3 n, const float rad,
+                            const float im, const v3 x, const q4 q, const v3 v, const v3 w, v3 &dV, v3 &dW) {
+  ocontact_vel_pe(g, S, ground, pen, vadd(x, qrot_xy(e, q)), n, rad, im, x, v, w, dV, dW);
 }
 
-POB_D void contact_velocity(csys_t *Sp, const Body &b, const Contacts &ct, v3 (&dV)[POB_NDYN],
-                            v3 (&dW)[POB_NDYN]) {
-#pragma unroll
-  for (int k = 0; k < POB_NGROUND + POB_NDYN; ++k) {
-    POB_FENCE();
-    const int i = contact_body(k);
-    const float pen = ct.pen[k];
-    if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
-      v3 e, n;
-      float rad;
-      contact_geom(S, ct, k, e, n, rad);
-      const float im = S.inv_mass[i];
-      v3 pe = vadd(b.x[i], qrot(e, b.q[i]));
-      v3 cp = vfma(n, -rad, pe);
-      v3 rr = vsub(cp, b.x[i]);
-      v3 vr = vadd(b.v[i], vcross(b.w[i], rr));
-      float vn = vdot(vr, n);
-      v3 vt = vfma(n, -vn, vr);
-      float lt, ilt;
-      pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
-      v3 dv = V(0.0f, 0.0f, 0.0f);
-      if (lt > 0.0f) {
-        float fr = fminf(S.friction * pen * S.inv_h, lt);
-        dv = vscl(vt, -(fr * ilt));
-      }
-      if (vn < 0.0f) dv = vfma(n, -vn, dv);
-      float D, iD;
-      pob_sqrt_rcp(vdot(dv, dv), D, iD);
-      if (D > 0.0f) {
-        v3 dh = vscl(dv, iD);
-        v3 cd = vcross(rr, dh);
-        float w = im + vdot(cd, cd);
-        v3 P = vdivs(dv, w);
-        dV[i] = vfma(P, im, dV[i]);
-        dW[i] = vadd(dW[i], vcross(rr, P));
-      }
+// One-way contact impulse of brax <= 0.0.12 (oracle legacy_contacts: Baumgarte-stabilised
+// inelastic normal impulse, Coulomb drag capped by friction * impulse; applied when
+// penetrating, approaching and positive) at the contact point pe
+template <class SS>
+POB_D void olegacy_contact(const SS &S, const float pen, const v3 pe, const v3 n, const float rad, const float im,
+                           const v3 x, const v3 v, const v3 w, v3 &dV, v3 &dW) {
+  const v3 rel = vsub(vfma(n, -rad, pe), x);
+  const v3 cv = vadd(v, vcross(w, rel));
+  const float nv = vdot(n, cv);
+  const float ang = vdot(n, vcross(vcross(rel, n), rel));
+  const float rden = pob_rcp(im + ang);
+  const float imp = (S.erp * pen - nv) * rden;
+  if (nv < 0.0f && imp > 0.0f) {
+    const v3 vd = vfma(n, -nv, cv);
+    const float nd = pob_sqrt(vdot(vd, vd));
+    v3 P = vscl(n, imp);
+    if (nd > 0.01f) {
+      const float impd = fminf(nd * rden, S.friction * imp);
+      P = vfma(vd, -(impd * pob_rcp(1e-6f + nd)), P);
     }
+    dV = vfma(P, im, dV);
+    dW = vadd(dW, vcross(rel, P));
   }
-}
-
-// sys.info(qp).contact at a static state
-POB_D void info_contact(csys_t *Sp, const Body &b, v3 (&cvel)[POB_NDYN], v3 (&cang)[POB_NDYN]) {
-  Contacts ct;
-  detect(Sp, b, ct);
-#pragma unroll
-  for (int i = 0; i < POB_NDYN; ++i) { cvel[i] = V(0.0f, 0.0f, 0.0f); cang[i] = V(0.0f, 0.0f, 0.0f); }
-  contact_velocity(Sp, b, ct, cvel, cang);
 }

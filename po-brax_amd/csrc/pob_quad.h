@@ -82,13 +82,6 @@ POB_D constexpr int qbody_global(int l, int k) { return l == 0 ? 0 : l + 2 * k; 
 #define QL_CA(l) (21 + 6 * (l) + 3)
 #define QL_FLOATS 39
 
-struct QContacts {
-  // [0] torso ground, [1] lower-leg ground, [2 + l] deepest wall contact of local capsule l
-  float pen[2 + QNB];
-  v3 n[QNB];
-  bool sel[QNB];
-  v3 pe[2 + QNB];  // the contact's sphere centre in world (x + rotate(e, q)), reused by the position pass
-};
 POB_D constexpr int qcontact_body(int c) { return c == 0 ? 0 : (c == 1 ? 2 : c - 2); }
 
 // capsule end point q of local body l (torso: the sphere centre)
@@ -106,280 +99,265 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
   return c == 0 ? S.ground_r[0] : LT[POB_LEG_GROUND + 3];
 }
 
-// sphere_box (pob_physics.h) of end point p against the wall row R staged in LDS
-// (centre x, y, cos, sin, half-extent x, y; z from the system), folded into the deepest-
-// contact search: same operations in the same order, but the square root, normal and
-// compare run only when d2 < T = r^2 (1 + 2^-20) (or d2 is NaN).  Exact: d2 >= T gives
-// sqrt_rn(d2) >= r, so pen = r - dist <= 0 never beats best (>= 0, strict ">").
-// (the row's six floats given as values: LDS rows for a per-lane wall walk, the system
-// table's scalars for a wave-uniform one)
-// (wall_hz / wall_cz given as values: the eight- and sixteen-lane kernels keep them in registers)
-template <class G = GuardBranch>
-POB_D void qwall_end_vz(G &g, const float wall_hz, const float wall_cz, const float cx, const float cy, const float c,
-                        const float s, const float hx, const float hy, v3 p, float r, float T, bool on, bool q1,
-                        float &best, v3 &bn, bool &bsel, v3 &bpe) {
-  const v3 h = V(hx, hy, wall_hz);
-  v3 d = vsub(p, V(cx, cy, wall_cz));
-  float lx = FMA(d.y, s, d.x * c), ly = FMA(d.y, c, -(d.x * s)), lz = d.z;
-  float qx = clamp_sym(lx, h.x), qy = clamp_sym(ly, h.y), qz = clamp_sym(lz, h.z);
-  float ex = lx - qx, ey = ly - qy, ez = lz - qz;
-  float d2 = FMA(ez, ez, FMA(ey, ey, ex * ex));
-  if (!(d2 >= T)) {
-    float pen, nx, ny, nz;
-    if (d2 > 0.0f) {
-      float dist, inv;
-      g.sqrt_rcp(d2, dist, inv);
-      pen = r - dist; nx = ex * inv; ny = ey * inv; nz = ez * inv;
-    } else {
-      float fx = h.x - fabsf(lx), fy = h.y - fabsf(ly), fz = h.z - fabsf(lz);
-      nx = 0.0f; ny = 0.0f; nz = 0.0f;
-      if (fx <= fy && fx <= fz) { pen = r + fx; nx = lx < 0.0f ? -1.0f : 1.0f; }
-      else if (fy <= fz) { pen = r + fy; ny = ly < 0.0f ? -1.0f : 1.0f; }
-      else { pen = r + fz; nz = lz < 0.0f ? -1.0f : 1.0f; }
-    }
-    if (on && pen > best) {
-      best = pen;
-      bn = V(FMA(-ny, s, nx * c), FMA(ny, c, nx * s), nz);
-      bsel = q1;
-      bpe = p;
-    }
-  }
-}
-template <class G = GuardBranch>
-POB_D void qwall_end_v(G &g, csys_t &S, const float cx, const float cy, const float c, const float s, const float hx,
-                       const float hy, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn, bool &bsel,
-                       v3 &bpe) {
-  qwall_end_vz(g, S.wall_hz, S.wall_cz, cx, cy, c, s, hx, hy, p, r, T, on, q1, best, bn, bsel, bpe);
-}
-POB_D void qwall_end(csys_t &S, const float *R, v3 p, float r, float T, bool on, bool q1, float &best, v3 &bn,
-                     bool &bsel, v3 &bpe) {
-  const float2 r01 = *reinterpret_cast<const float2 *>(R);
-  const float2 r23 = *reinterpret_cast<const float2 *>(R + 2);
-  const float2 r45 = *reinterpret_cast<const float2 *>(R + 4);
-  GuardBranch g;
-  qwall_end_v(g, S, r01.x, r01.y, r23.x, r23.y, r45.x, r45.y, p, r, T, on, q1, best, bn, bsel, bpe);
+// ---------------------------------------------------------------------- contacts
+// Ground (collide_include Ant x Ground: CapsulePlane on the torso and the lower leg):
+// [0] torso, [1] lower leg; pe = the sphere centre x + rotate(end, q) at detection.
+struct QGround {
+  float pen[2];
+};
+// The lane's wall contacts (pob_mesh.h, brax capsule x TriangulatedBox) of a collide substep:
+// the bodies' capsule segments at detection -- a = x + rotate(e0, q), b = x - rotate(e0, q)
+// (torso: the sphere centre a) -- and, per body, the (wall, face) items that produced a
+// contact: wall w of body l = bit 8 l + w of mc.  The velocity pass re-derives the face items
+// of exactly those walls from the stored segments and re-evaluates them (the same operations
+// on the same operands: the same contacts in the same order) instead of keeping every
+// contact in registers.
+struct QMesh {
+  v3 a[QNB], b[QNB];
+  uint32_t mc;
+};
+
+// The Ant's capsules (checked by pob_system.cpp) have opposite end points +-e0 in the body
+// xy-plane, so one rotation rv = rotate(e0, q) serves both (rotate(-e0) = -rv exactly), and a
+// lower leg's ground point is its end 1 (x - rv).  The torso sphere's points are its centre x.
+POB_D void qground_detect(csys_t &S, const float *LT, const QBody &b, const v3 rv_leg, QGround &gc, v3 (&pe)[2]) {
+  pe[0] = S.torso_point ? b.x[0] : vadd(b.x[0], qrot(qground_end(S, LT, 0), b.q[0]));
+  pe[1] = vsub(b.x[2], rv_leg);
+  gc.pen[0] = qground_r(S, LT, 0) - pe[0].z;
+  gc.pen[1] = qground_r(S, LT, 1) - pe[1].z;
 }
 
-// Contact detection of a collide substep on a lane quad.  Walls: every lane keeps a mask
-// of the walls whose grown box (pob_sys::wall_lo/hi) meets the AABB of its three body
-// centres, and walks ITS OWN mask in increasing wall order, so one pass over a wall row
-// serves lanes near different walls (a wave-uniform wall loop would run every wall any of
-// the 16 envs is near).  Culled pairs have penetration < 0 and the walk keeps the oracle's
-// (wall, end) order with the strict ">" -- the deepest contact is unchanged.
-// WALLS = false compiles the wall search out (the stock ant has no walls).
-// Contact points are x + rotate(e, q) (oracle cpoint).  The Ant's capsules (checked by
-// pob_system.cpp) have opposite end points +-e0 in the body xy-plane, so one rotation
-// rv = rotate(e0, q) serves both (rotate(-e0) = -rv exactly), and a lower leg's ground point
-// is its end 1 (x - rv).  The torso sphere's points are its centre x (rotate(0) = 0).
-template <bool WALLS>
-POB_D void qdetect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QContacts &ct) {
-  v3 rv_leg;
-  {
-    csys_t &S = *launder(Sp);
-    rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
-    const v3 pe0 = S.torso_point ? b.x[0] : vadd(b.x[0], qrot(qground_end(S, LT, 0), b.q[0]));
-    const v3 pe1 = vsub(b.x[2], rv_leg);
-    ct.pen[0] = qground_r(S, LT, 0) - pe0.z;
-    ct.pen[1] = qground_r(S, LT, 1) - pe1.z;
-    ct.pe[0] = pe0;
-    ct.pe[1] = pe1;
-  }
-  uint32_t lane_mask = 0u;
-  if (WALLS) {
-    float mnx = b.x[0].x, mxx = b.x[0].x, mny = b.x[0].y, mxy = b.x[0].y;
+// broadphase: bit w set iff wall w's grown box (pob_sys::wall_lo/hi: capsule reach + 2e-3)
+// meets the xy AABB of the lane's three body centres -- a wall outside it has every face
+// culled for every body of the lane (gap > r + 1e-3), so skipping it changes nothing
+POB_D uint32_t qwall_mask(csys_t &S, const QBody &b) {
+  float mnx = b.x[0].x, mxx = b.x[0].x, mny = b.x[0].y, mxy = b.x[0].y;
 #pragma unroll
-    for (int l = 1; l < QNB; ++l) {
-      mnx = fminf(mnx, b.x[l].x); mxx = fmaxf(mxx, b.x[l].x);
-      mny = fminf(mny, b.x[l].y); mxy = fmaxf(mxy, b.x[l].y);
-    }
-    csys_t &S = *launder(Sp);
+  for (int l = 1; l < QNB; ++l) {
+    mnx = fminf(mnx, b.x[l].x); mxx = fmaxf(mxx, b.x[l].x);
+    mny = fminf(mny, b.x[l].y); mxy = fmaxf(mxy, b.x[l].y);
+  }
 #ifdef POB_EXP_NO_WALLS
-    const int nw = 0;  // timing experiment only
+  const int nw = 0;  // timing experiment only
 #else
-    const int nw = S.n_walls;
+  const int nw = S.n_walls;
 #endif
+  uint32_t m = 0u;
 #pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w) {
-      // xy only: dropping the z test can only keep more walls (the cull stays exact)
-      // all POB_MAXW boxes loaded at once, w < nw as a predicate (a runtime loop waited
-      // one scalar-load round trip per wall)
-      const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
-      const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
-      lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
-    }
+  for (int w = 0; w < POB_MAXW; ++w) {
+    // all POB_MAXW boxes loaded at once, w < nw as a predicate
+    const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
+    const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
+    m |= (near & (w < nw)) ? 1u << w : 0u;
   }
-  const bool any_near = WALLS && __any(lane_mask != 0u);
+  return m;
+}
+
+// the lane's bodies' capsule segments (a, b) (torso: a = b = x)
+POB_D void qmesh_segments(csys_t &S, const float *LT, const QBody &b, const v3 rv_leg, QMesh &ms) {
+  const v3 rv1 = qrot_xy(qcap_end(S, LT, 1, 0), b.q[1]);
+  ms.a[0] = b.x[0]; ms.b[0] = b.x[0];
+  ms.a[1] = vadd(b.x[1], rv1); ms.b[1] = vsub(b.x[1], rv1);
+  ms.a[2] = vadd(b.x[2], rv_leg); ms.b[2] = vsub(b.x[2], rv_leg);
+}
+// x + tau rotate(e0, q) of local body l (l = 1, 2; the torso's point is x)
+POB_D v3 qseg_point(const float *LT, const int l, const v3 x, const q4 q, const float tau) {
+  const float *e = LT + POB_LEG_BODY(l) + 2;
+  return vfma(qrot_xy(V(e[0], e[1], e[2]), q), tau, x);
+}
+
+// face items of the lane's bodies: M[l] bit 8 w + f for every face f of a wall w that the
+// face cull keeps for body l, over the walls of wm (bit 8 l + w: body l's walls; walls walked
+// per lane in increasing order)
+POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, const uint32_t wm, const QMesh &ms,
+                       uint64_t (&M)[QNB]) {
 #pragma unroll
-  for (int l = 0; l < QNB; ++l) {
-    POB_FENCE();
-    csys_t &S = *launder(Sp);
-    const int nend = (l == 0) ? 1 : 2;
-    float best = 0.0f;
-    v3 bn = V(0.0f, 0.0f, 0.0f);
-    bool bsel = false;
-    v3 bpe = bn;
-    if (any_near) {
-      v3 pe[2];
-      if (l == 0) {
-        pe[0] = S.torso_point ? b.x[0] : vadd(b.x[0], qrot(qcap_end(S, LT, 0, 0), b.q[0]));
-      } else {
-        const v3 rv = l == 2 ? rv_leg : qrot_xy(qcap_end(S, LT, 1, 0), b.q[1]);
-        pe[0] = vadd(b.x[l], rv);
-        pe[1] = vsub(b.x[l], rv);
-      }
-      const float r = q_cap_r(S, LT, l);
-      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20), rounded products
-      uint32_t m = lane_mask;
-      while (__any(m != 0u)) {
-        const bool on = m != 0u;
-        const int w = on ? __builtin_ctz(m) : 0;
-        m &= m - 1u;
+  for (int l = 0; l < QNB; ++l) M[l] = 0ull;
+  const float cz = S.wall_cz, hz = S.wall_hz;
+  uint32_t m = (wm | (wm >> 8) | (wm >> 16)) & 0xFFu;
+  while (__any(m != 0u)) {
+    const bool on = m != 0u;
+    const int w = on ? __builtin_ctz(m) : 0;
+    m &= m - 1u;
+    const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
 #pragma unroll
-        for (int q = 0; q < nend; ++q) qwall_end(S, WT + POB_WALL_FLOATS * w, pe[q], r, T, on, q == 1, best, bn, bsel, bpe);
-      }
+    for (int l = 0; l < QNB; ++l) {
+      const float R = (l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1]) + POB_MESH_MARGIN;
+      const v3 La = mwall_local(W, cz, ms.a[l]);
+      const v3 Lb = l == 0 ? La : mwall_local(W, cz, ms.b[l]);
+      const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, R);
+      M[l] |= (on && ((wm >> (8 * l + w)) & 1u)) ? (uint64_t)fm << (8 * w) : 0ull;
     }
-    ct.pen[2 + l] = best;
-    ct.n[l] = bn;
-    ct.sel[l] = bsel;
-    ct.pe[2 + l] = bpe;
   }
 }
 
-POB_D void qcontact_geom(csys_t &S, const float *LT, const QContacts &ct, int c, v3 &e, v3 &n, float &r) {
-  if (c < 2) {
-    e = qground_end(S, LT, c);
-    n = V(0.0f, 0.0f, 1.0f);
-    r = qground_r(S, LT, c);
-  } else {
-    const int l = c - 2;
-    e = ct.sel[l] ? qcap_end(S, LT, l, 1) : qcap_end(S, LT, l, 0);
-    r = q_cap_r(S, LT, l);
-    n = ct.n[l];
+// Walk the lane's face items (body order, then wall / face order: the oracle's contact order
+// per body) one per lane per iteration, evaluating each face once: emit(l, tau, n, pen) for
+// every penetrating triangle.  hit (optional) collects the walls that produced a contact
+// (bit 8 l + w).
+template <class G, class F>
+POB_D void qmesh_walk(G &g, csys_t &S, const float *LT, const float *WT, const QMesh &ms, uint64_t (&M)[QNB],
+                      uint32_t *hit, F &&emit) {
+  const float cz = S.wall_cz, hz = S.wall_hz;
+  while (__any((M[0] | M[1] | M[2]) != 0ull)) {
+    const int l = M[0] != 0ull ? 0 : (M[1] != 0ull ? 1 : 2);
+    const uint64_t ml = l == 0 ? M[0] : (l == 1 ? M[1] : M[2]);
+    const bool on = ml != 0ull;
+    const int bit = on ? __builtin_ctzll(ml) : 0;
+    const uint64_t rest = ml & (ml - 1ull);
+    M[0] = l == 0 ? rest : M[0];
+    M[1] = l == 1 ? rest : M[1];
+    M[2] = l == 2 ? rest : M[2];
+    if (on) {
+      const int w = bit >> 3, f = bit & 7;
+      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
+      const v3 A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
+      const v3 B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
+      const float r = l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1];
+      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
+      const v3 La = mwall_local(W, cz, A);
+      const v3 Lb = l == 0 ? La : mwall_local(W, cz, B);
+      bool any = false;
+      mesh_face(g, f, La, Lb, l != 0, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
+        any = true;
+        emit(l, tau, mwall_world_n(W, nl), pen);
+      });
+      if (hit && any) *hit |= 1u << (8 * l + w);
+    }
   }
 }
 
-// contact processing order of one body = oracle order (ground contact first, then wall)
-POB_D void qcontact_position(csys_t *Sp, const float *LT, const QBody &b, const Lds &L, const QContacts &ct,
-                             v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
+// body l's value among the lane's three (selects: a runtime index into a register array
+// would become a private array in scratch)
+POB_D v3 qpick3(const int l, const v3 (&a)[QNB]) { return vsel3(l == 0, a[0], vsel3(l == 1, a[1], a[2])); }
+POB_D q4 qpick4(const int l, const q4 (&a)[QNB]) { return qsel(l == 0, a[0], qsel(l == 1, a[1], a[2])); }
+POB_D void qput3(const int l, v3 (&a)[QNB], const v3 v) {
+  a[0] = vsel3(l == 0, v, a[0]); a[1] = vsel3(l == 1, v, a[1]); a[2] = vsel3(l == 2, v, a[2]);
+}
+
+// Position pass of a collide substep: ground contacts (ground first per body, oracle order),
+// then every wall contact as it is detected; the segments and the contact walls are kept in
+// ms for the velocity pass
+template <bool WALLS>
+POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const Lds &L, QGround &gc,
+                              QMesh &ms, v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
+  csys_t &S = *launder(Sp);
+  const HCon SC{fric, S.inv_h};
+  GuardBranch g;
+  const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
+  {
+    v3 pe[2];
+    qground_detect(S, LT, b, rv_leg, gc, pe);
 #pragma unroll
-  for (int c = 0; c < 2 + QNB; ++c) {
+    for (int c = 0; c < 2; ++c) {
+      POB_FENCE();
+      const int l = qcontact_body(c);
+      if (gc.pen[c] > 0.0f)
+        oground_position(g, SC, gc.pen[c], pe[c], qground_r(S, LT, c), q_inv_mass(S, LT, l), b.x[l], b.q[l],
+                         L.get4(QL_PQ(l)), L.get3(QL_PX(l)), DX[l], DA[l]);
+    }
+  }
+  ms.mc = 0u;
+  if (!WALLS) return;
+  POB_FENCE();
+  qmesh_segments(S, LT, b, rv_leg, ms);
+  uint64_t M[QNB];
+  {
+    const uint32_t lw = qwall_mask(S, b);
+    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
+  }
+  qmesh_walk(g, S, LT, WT, ms, M, &ms.mc, [&](const int l, const float tau, const v3 n, const float pen) {
+    const v3 x = qpick3(l, b.x);
+    const q4 q = qpick4(l, b.q);
+    const v3 pe = l == 0 ? x : qseg_point(LT, l, x, q, tau);
+    v3 dx = qpick3(l, DX), da = qpick3(l, DA);
+    owall_position(g, SC, pen, pe, n, q_cap_r(S, LT, l), q_inv_mass(S, LT, l), x, q, L.get4(QL_PQ(0) + 7 * l),
+                   L.get3(QL_PX(0) + 7 * l), dx, da);
+    qput3(l, DX, dx);
+    qput3(l, DA, da);
+  });
+}
+
+// Velocity pass: ground contacts, then the wall contacts re-derived from the stored segments
+// (contact points x + tau rotate(e0, q) at the post-projection pose)
+template <bool WALLS>
+POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const QGround &gc,
+                              const QMesh &ms, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
+  csys_t &S = *launder(Sp);
+  const HCon SC{fric, S.inv_h};
+  GuardBranch g;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
     POB_FENCE();
     const int l = qcontact_body(c);
-    const float pen = ct.pen[c];
-    if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
-      v3 e, n;
-      float rad;
-      qcontact_geom(S, LT, ct, c, e, n, rad);
-      const float im = q_inv_mass(S, LT, l);
-      const v3 pe = ct.pe[c];  // = x + rotate(e, q) of the detection (same q, x)
-      if (c < 2) {
-        // ground contact, n = (0, 0, 1): the expressions below with the products by the
-        // normal's exact zeros dropped (same values up to the sign of a zero)
-        const v3 cp = V(pe.x, pe.y, pe.z - rad);
-        const v3 rr = vsub(cp, b.x[l]);
-        const float w = im + FMA(rr.x, rr.x, rr.y * rr.y);  // |rr x n|^2
-        const float lam = POB_DIV(pen, w);
-        DX[l].z = FMA(lam, im, DX[l].z);  // P = (0, 0, lam)
-        DA[l] = V(DA[l].x + rr.y * lam, DA[l].y + -(rr.x * lam), DA[l].z);  // rr x P
-        const v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
-        const float dpx = cp.x - cprev.x, dpy = cp.y - cprev.y;  // tangential part of cp - cprev
-        float lt, inv;
-        pob_sqrt_rcp(FMA(dpy, dpy, dpx * dpx), lt, inv);
-        if (lt > 0.0f) {
-          const float tx = dpx * inv, ty = dpy * inv;
-          const v3 ctn = V(-(rr.z * ty), rr.z * tx, FMA(rr.x, ty, -(rr.y * tx)));  // rr x t
-          const float wt = im + vdot(ctn, ctn);
-          const float lamt = POB_DIV(lt, wt);
-          if (lamt < fric * lam) {
-            const float px = tx * -lamt, py = ty * -lamt;
-            DX[l].x = FMA(px, im, DX[l].x);
-            DX[l].y = FMA(py, im, DX[l].y);
-            DA[l] = vadd(DA[l], V(-(rr.z * py), rr.z * px, FMA(rr.x, py, -(rr.y * px))));  // rr x Pt
-          }
-        }
-        continue;
-      }
-      v3 cp = vfma(n, -rad, pe);
-      v3 rr = vsub(cp, b.x[l]);
-      v3 cn = vcross(rr, n);
-      float w = im + vdot(cn, cn);
-      float lam = POB_DIV(pen, w);
-      v3 P = vscl(n, lam);
-      DX[l] = vfma(P, im, DX[l]);
-      DA[l] = vadd(DA[l], vcross(rr, P));
-      v3 cprev = qrot_add(qrot(rr, qinv(b.q[l])), L.get4(QL_PQ(l)), L.get3(QL_PX(l)));
-      v3 dp = vsub(cp, cprev);
-      v3 dpt = vfma(n, -vdot(dp, n), dp);
-      float lt, ilt;
-      pob_sqrt_rcp(vdot(dpt, dpt), lt, ilt);
-      if (lt > 0.0f) {
-        v3 t = vscl(dpt, ilt);
-        v3 ctn = vcross(rr, t);
-        float wt = im + vdot(ctn, ctn);
-        float lamt = POB_DIV(lt, wt);
-        if (lamt < fric * lam) {
-          v3 Pt = vscl(t, -lamt);
-          DX[l] = vfma(Pt, im, DX[l]);
-          DA[l] = vadd(DA[l], vcross(rr, Pt));
-        }
-      }
+    if (gc.pen[c] > 0.0f) {
+      const v3 e = qground_end(S, LT, c);
+      const v3 pe = l == 0 ? vadd(b.x[0], qrot(e, b.q[0])) : vadd(b.x[l], qrot_xy(e, b.q[l]));
+      ocontact_vel_pe(g, SC, true, gc.pen[c], pe, V(0.0f, 0.0f, 1.0f), qground_r(S, LT, c), q_inv_mass(S, LT, l), b.x[l],
+                      b.v[l], b.w[l], dV[l], dW[l]);
     }
   }
+  if (!WALLS || !__any(ms.mc != 0u)) return;
+  POB_FENCE();
+  uint64_t M[QNB];
+  qmesh_items(S, LT, WT, ms.mc, ms, M);
+  qmesh_walk(g, S, LT, WT, ms, M, (uint32_t *)nullptr, [&](const int l, const float tau, const v3 n, const float pen) {
+    const v3 x = qpick3(l, b.x);
+    const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
+    v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
+    ocontact_vel_pe(g, SC, false, pen, pe, n, q_cap_r(S, LT, l), q_inv_mass(S, LT, l), x, qpick3(l, b.v),
+                    qpick3(l, b.w), dv, dw);
+    qput3(l, dV, dv);
+    qput3(l, dW, dw);
+  });
 }
 
-POB_D void qcontact_velocity(csys_t *Sp, const float *LT, const QBody &b, const QContacts &ct, v3 (&dV)[QNB],
-                             v3 (&dW)[QNB], const float fric) {
+// sys.info(qp).contact and the legacy collisions: detection and the velocity-level response
+// (LEGACY: the one-way impulses) at ONE pose, so each contact is applied as it is detected
+template <bool WALLS, bool LEGACY>
+POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const QBody &b, v3 (&dV)[QNB],
+                            v3 (&dW)[QNB], const float fric) {
+  csys_t &S = *launder(Sp);
+  const HCon SC{fric, S.inv_h};
+  GuardBranch g;
+  const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
+  {
+    QGround gc;
+    v3 pe[2];
+    qground_detect(S, LT, b, rv_leg, gc, pe);
 #pragma unroll
-  for (int c = 0; c < 2 + QNB; ++c) {
-    POB_FENCE();
-    const int l = qcontact_body(c);
-    const float pen = ct.pen[c];
-    if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
-      v3 e, n;
-      float rad;
-      qcontact_geom(S, LT, ct, c, e, n, rad);
-      const float im = q_inv_mass(S, LT, l);
-      v3 pe = l == 0 ? vadd(b.x[0], qrot(e, b.q[0])) : vadd(b.x[l], qrot_xy(e, b.q[l]));
-      v3 cp = vfma(n, -rad, pe);
-      v3 rr = vsub(cp, b.x[l]);
-      v3 vr = vadd(b.v[l], vcross(b.w[l], rr));
-      v3 dv = V(0.0f, 0.0f, 0.0f);
-      if (c < 2) {
-        // ground, n = (0, 0, 1) (zero products dropped, as in the position pass)
-        const float vn = vr.z;
-        float lt, ilt;
-        pob_sqrt_rcp(FMA(vr.y, vr.y, vr.x * vr.x), lt, ilt);
-        if (lt > 0.0f) {
-          const float fr = fminf(fric * pen * S.inv_h, lt);
-          const float k = -(fr * ilt);
-          dv = V(vr.x * k, vr.y * k, 0.0f);
-        }
-        if (vn < 0.0f) dv.z = -vn;
-      } else {
-        float vn = vdot(vr, n);
-        v3 vt = vfma(n, -vn, vr);
-        float lt, ilt;
-        pob_sqrt_rcp(vdot(vt, vt), lt, ilt);
-        if (lt > 0.0f) {
-          float fr = fminf(fric * pen * S.inv_h, lt);
-          dv = vscl(vt, -(fr * ilt));
-        }
-        if (vn < 0.0f) dv = vfma(n, -vn, dv);
-      }
-      float D, iD;
-      pob_sqrt_rcp(vdot(dv, dv), D, iD);
-      if (D > 0.0f) {
-        v3 dh = vscl(dv, iD);
-        v3 cd = vcross(rr, dh);
-        float w = im + vdot(cd, cd);
-        v3 P = vdivs(dv, w);
-        dV[l] = vfma(P, im, dV[l]);
-        dW[l] = vadd(dW[l], vcross(rr, P));
+    for (int c = 0; c < 2; ++c) {
+      POB_FENCE();
+      const int l = qcontact_body(c);
+      if (gc.pen[c] > 0.0f) {
+        if (LEGACY)
+          olegacy_contact(S, gc.pen[c], pe[c], V(0.0f, 0.0f, 1.0f), qground_r(S, LT, c), q_inv_mass(S, LT, l), b.x[l],
+                          b.v[l], b.w[l], dV[l], dW[l]);
+        else
+          ocontact_vel_pe(g, SC, true, gc.pen[c], pe[c], V(0.0f, 0.0f, 1.0f), qground_r(S, LT, c),
+                          q_inv_mass(S, LT, l), b.x[l], b.v[l], b.w[l], dV[l], dW[l]);
       }
     }
   }
+  if (!WALLS) return;
+  POB_FENCE();
+  QMesh ms;
+  qmesh_segments(S, LT, b, rv_leg, ms);
+  uint64_t M[QNB];
+  {
+    const uint32_t lw = qwall_mask(S, b);
+    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
+  }
+  qmesh_walk(g, S, LT, WT, ms, M, (uint32_t *)nullptr, [&](const int l, const float tau, const v3 n, const float pen) {
+    const v3 x = qpick3(l, b.x);
+    const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
+    const float rl = q_cap_r(S, LT, l), iml = q_inv_mass(S, LT, l);
+    v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
+    if (LEGACY) olegacy_contact(S, pen, pe, n, rl, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
+    else ocontact_vel_pe(g, SC, false, pen, pe, n, rl, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
+    qput3(l, dV, dv);
+    qput3(l, dW, dw);
+  });
 }
 
 // torso terms of the lane's hip joint (global 2k): the oracle adds P * imp to DX[0] and
@@ -521,7 +499,8 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     }
   }
   // 3. position projection
-  QContacts ct;
+  QGround gc;
+  QMesh ms;
   {
     v3 DX[QNB];
     v3 DA[QNB];
@@ -548,10 +527,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
       qtorso_add<2>(DX[0], DA[0], tq, imp0);
       qtorso_add<3>(DX[0], DA[0], tq, imp0);
     }
-    if (COLLIDE) {
-      qdetect<WALLS>(Sp, LT, WT, b, ct);
-      qcontact_position(Sp, LT, b, L, ct, DX, DA, fric);
-    }
+    if (COLLIDE) qcontacts_position<WALLS>(Sp, LT, WT, b, L, gc, ms, DX, DA, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.x[l] = vadd(b.x[l], DX[l]);
@@ -575,7 +551,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontact_velocity(Sp, LT, b, ct, dV, dW, fric);
+    qcontacts_velocity<WALLS>(Sp, LT, WT, b, gc, ms, dV, dW, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
@@ -591,41 +567,6 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
 // actuators as accelerations, then one-way contact impulses.  Every expression follows the
 // oracle's generic form (no frame specialisation: this mode is the parity reference for the
 // notebook, not the throughput path).
-
-// one-way contact impulses of the detected contacts into dV / dW (oracle legacy_contacts;
-// per body: ground contact first, then wall)
-POB_D void qlegacy_contacts(csys_t *Sp, const float *LT, const QBody &b, const QContacts &ct, v3 (&dV)[QNB],
-                            v3 (&dW)[QNB]) {
-#pragma unroll
-  for (int c = 0; c < 2 + QNB; ++c) {
-    const int l = qcontact_body(c);
-    const float pen = ct.pen[c];
-    if (pen > 0.0f) {
-      csys_t &S = *launder(Sp);
-      v3 e, n;
-      float rad;
-      qcontact_geom(S, LT, ct, c, e, n, rad);
-      const float im = q_inv_mass(S, LT, l);
-      const v3 rel = vsub(vfma(n, -rad, ct.pe[c]), b.x[l]);  // pe = x + rotate(e, q) of the detection
-      const v3 cv = vadd(b.v[l], vcross(b.w[l], rel));
-      const float nv = vdot(n, cv);
-      const float ang = vdot(n, vcross(vcross(rel, n), rel));
-      const float rden = pob_rcp(im + ang);
-      const float imp = (S.erp * pen - nv) * rden;
-      if (nv < 0.0f && imp > 0.0f) {
-        const v3 vd = vfma(n, -nv, cv);
-        const float nd = pob_sqrt(vdot(vd, vd));
-        v3 P = vscl(n, imp);
-        if (nd > 0.01f) {
-          const float impd = fminf(nd * rden, S.friction * imp);
-          P = vfma(vd, -(impd * pob_rcp(1e-6f + nd)), P);
-        }
-        dV[l] = vfma(P, im, dV[l]);
-        dW[l] = vadd(dW[l], vcross(rel, P));
-      }
-    }
-  }
-}
 
 // spring joint jl of the lane (oracle legacy_joints): the anchor impulse imp and the angular
 // term tw (parent: + tw + rp x -imp, child: - tw + rc x imp)
@@ -702,13 +643,11 @@ POB_D void qlegacy_substep(csys_t *Sp, const float *LT, const float *WT, QBody &
                  FMA(S.ang_damp, w.z, dw[l].z * S.h));
     }
   }
-  // collisions: velocity impulses at the post-kinetic pose
-  QContacts ct;
-  qdetect<WALLS>(Sp, LT, WT, b, ct);
+  // collisions: velocity impulses at the post-kinetic pose (oracle legacy_contacts)
   v3 dV[QNB], dW[QNB];
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-  qlegacy_contacts(Sp, LT, b, ct, dV, dW);
+  qcontacts_static<WALLS, true>(Sp, LT, WT, b, dV, dW, launder(Sp)->friction);
 #pragma unroll
   for (int l = 0; l < QNB; ++l) {
     b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
