@@ -677,8 +677,9 @@ static inline int tri_inside(int t, float ha, float hb, float pa, float pb) {
 static void tri_closest(int t, float ha, float hb, float pa, float pb, float *qa, float *qb) {
   if (tri_inside(t, ha, hb, pa, pb)) { *qa = pa; *qb = pb; return; }
   FL(4 + 1 + 8 + 6 + 6);
-  /* diagonal V0 -> V2: s = clamp01(((p - V0) . (ha, hb)) / (ha^2 + hb^2)) */
-  const float s = clamp01(fmaf(pb + hb, hb, (pa + ha) * ha) * (1.0f / fmaf(hb, hb, ha * ha)));
+  /* diagonal V0 -> V2, D = (2ha, 2hb): s = clamp01(((p - V0) . D) / (D . D)) */
+  const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
+  const float s = clamp01(fmaf(pb + hb, hb2, (pa + ha) * ha2) * (1.0f / fmaf(hb2, hb2, ha2 * ha2)));
   const float s2 = 2.0f * s;
   const float da = fmaf(s2, ha, -ha), db = fmaf(s2, hb, -hb);
   float ea[3], eb[3];
@@ -836,6 +837,29 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
     }
   }
   CST(2, n_hit);
+}
+
+/* Test hook (tests/test_contact_mesh.py): the mesh contacts of one capsule against one wall
+ * box.  wall = (cx, cy, cz, cos, sin, hx, hy, hz), the capsule's world end points a, b (seg = 0:
+ * the sphere at a) and radius r; out[5 k ..] = (tau, nx, ny, nz, pen) of contact k in
+ * (face, triangle) order; returns the count (<= 12). */
+int orc_mesh_contacts(const float *wall, const float *a, const float *b, int seg, float r, float *out) {
+  orc_env *e = (orc_env *)calloc(1, sizeof(orc_env));
+  e->n_walls = 1;
+  e->wall_c[0] = V(wall[0], wall[1], wall[2]);
+  e->wall_cos[0] = wall[3]; e->wall_sin[0] = wall[4];
+  e->wall_h[0] = V(wall[5], wall[6], wall[7]);
+  e->cap_r[0] = r; e->cap_nend[0] = seg ? 2 : 1;
+  contacts_t *ct = (contacts_t *)malloc(sizeof(contacts_t));
+  ct->count = 0;
+  capsule_wall_mesh(e, 0, 0, V(a[0], a[1], a[2]), V(b[0], b[1], b[2]), ct);
+  for (int k = 0; k < ct->count; ++k) {
+    out[5 * k] = ct->tau[k]; out[5 * k + 1] = ct->n[k].x; out[5 * k + 2] = ct->n[k].y;
+    out[5 * k + 3] = ct->n[k].z; out[5 * k + 4] = ct->pen[k];
+  }
+  const int n = ct->count;
+  free(ct); free(e);
+  return n;
 }
 
 #ifdef ORC_COUNT_FLOPS

@@ -88,6 +88,9 @@ int orc_flops_set_mode(int mode);
  * [8..15] histogram of wall contacts per capsule per detection (0..6, >= 7) */
 void orc_contact_stats(long long out[16]);
 void orc_contact_stats_enable(int on);
+/* test hook: mesh contacts of one capsule (world end points a, b; seg 0 = sphere at a, radius r)
+ * against one wall box (cx, cy, cz, cos, sin, hx, hy, hz): out (tau, nx, ny, nz, pen) x count */
+int orc_mesh_contacts(const float *wall, const float *a, const float *b, int seg, float r, float *out);
 /* 0: evaluate every face of every wall (no face cull; the FLOP counter's reference mode does
  * this too) -- results must be identical to the default (1) */
 void orc_set_face_cull(int on);

@@ -50,9 +50,9 @@ POB_D uint32_t mesh_face_mask(const v3 A, const v3 B, const float hx, const floa
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float a1 = lo[k] - h[k], a2 = -h[k] - hi[k];
-    in[k] = fmaxf(a1, a2) < R;
-    fp[k] = fmaxf(a1, h[k] - hi[k]) < R;
-    fm[k] = fmaxf(lo[k] + h[k], a2) < R;
+    in[k] = !(fmaxf(a1, a2) >= R);  // (the oracle's "cull iff gap >= R": NaN keeps the face)
+    fp[k] = !(fmaxf(a1, h[k] - hi[k]) >= R);
+    fm[k] = !(fmaxf(lo[k] + h[k], a2) >= R);
   }
   uint32_t m = 0u;
   m |= (fm[0] & in[1] & in[2]) ? 1u : 0u;
@@ -83,11 +83,11 @@ POB_D void mcand_take(MCand &c, const float u, const float da, const float db, c
 
 // closest point of face triangle t to the plane point (pa, pb) (oracle tri_closest): the point
 // if inside, else the first strict minimum over the triangle's edges' nearest points;
-// inv_dd = 1 / (hb^2 + ha^2) of the diagonal
-POB_D void mtri_closest(const bool t1, const float ha, const float hb, const float inv_dd, const float pa, const float pb,
-                        float &qa, float &qb) {
+// the diagonal D = (2ha, 2hb), inv_dd = 1 / (D . D)
+POB_D void mtri_closest(const bool t1, const float ha, const float hb, const float ha2, const float hb2,
+                        const float inv_dd, const float pa, const float pb, float &qa, float &qb) {
   if (mtri_inside(t1, ha, hb, pa, pb)) { qa = pa; qb = pb; return; }
-  const float s = clamp01(FMA(pb + hb, hb, (pa + ha) * ha) * inv_dd);
+  const float s = clamp01(FMA(pb + hb, hb2, (pa + ha) * ha2) * inv_dd);
   const float s2 = 2.0f * s;
   const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
   const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
@@ -146,13 +146,14 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
   S.ab = k == 2 ? A.y : A.z;
   S.aw = k == 0 ? A.x : (k == 1 ? A.y : A.z);
   const float Ba = k == 0 ? B.y : B.x, Bb = k == 2 ? B.y : B.z, Bw = k == 0 ? B.x : (k == 1 ? B.y : B.z);
-  const float inv_dd = g.rcp(FMA(hb, hb, ha * ha));
+  const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
+  const float e_d = FMA(hb2, hb2, ha2 * ha2), i_d = g.rcp(e_d);
   MCand c[2];
   // end point A (and B) against each triangle
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     float qa, qb;
-    mtri_closest(t == 1, ha, hb, inv_dd, S.aa_, S.ab, qa, qb);
+    mtri_closest(t == 1, ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa, qb);
     c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f;
     mcand_take(c[t], 0.0f, S.aa_ - qa, S.ab - qb, S.aw - w0);
   }
@@ -160,15 +161,14 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       float qa, qb;
-      mtri_closest(t == 1, ha, hb, inv_dd, Ba, Bb, qa, qb);
+      mtri_closest(t == 1, ha, hb, ha2, hb2, i_d, Ba, Bb, qa, qb);
       mcand_take(c[t], 1.0f, Ba - qa, Bb - qb, Bw - w0);
     }
     S.Da = Ba - S.aa_; S.Db = Bb - S.ab; S.Dw = Bw - S.aw;
     S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
     S.inv_aa = g.rcp(S.aa);
-    const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
-    const float e_a = ha2 * ha2, e_b = hb2 * hb2, e_d = FMA(hb2, hb2, ha2 * ha2);
-    const float i_a = g.rcp(e_a), i_b = g.rcp(e_b), i_d = g.rcp(e_d);
+    const float e_a = ha2 * ha2, e_b = hb2 * hb2;
+    const float i_a = g.rcp(e_a), i_b = g.rcp(e_b);
     // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (the diagonal's
     // candidate is the same closest pair for both: evaluated once, taken in each order)
     mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);

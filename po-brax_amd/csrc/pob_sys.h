@@ -53,8 +53,8 @@ struct pob_sys {
   // walls: box centre (world), half extents, z-rotation cos/sin
   float wall_c[POB_MAXW][3], wall_h[POB_MAXW][3], wall_cos[POB_MAXW], wall_sin[POB_MAXW];
   // broadphase: world AABB of each wall grown by (capsule reach + radius + margin); a
-  // wave skips a wall when no lane's body centres fall inside it (exact: every culled
-  // sphere-box pair has penetration < 0, so the deepest-contact search is unchanged)
+  // lane skips a wall when none of its body centres falls inside it (exact: every triangle of
+  // a culled wall is farther than r from the capsule, no contact)
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
   float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
   float friction, s_pos, half_s_ang;

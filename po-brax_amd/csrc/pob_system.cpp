@@ -257,7 +257,8 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     R[3] = s.wall_sin[w]; R[4] = s.wall_h[w][0]; R[5] = s.wall_h[w][1];
   }
   // broadphase boxes: wall AABB + the largest distance from a body centre to any point of
-  // its capsule (|end| + r) + 1e-3 margin (>> float rounding of the sphere-box distance)
+  // its capsule (|end| + r) + 1e-3 margin: a wall outside a lane's box is farther than r + 1e-3
+  // from every capsule of the lane, so none of its triangles can be in contact (pob_mesh.h)
   double reach = 0.0;
   for (int i = 0; i < POB_NDYN; ++i)
     for (int q = 0; q < 2; ++q) {

@@ -1,0 +1,207 @@
+"""CPU: the Ant x Arena contact model (brax v1 capsule x TriangulatedBox, restated in
+oracle/pob_oracle.c capsule_wall_mesh and pob_mesh.h) against an independent brute-force
+geometry reference.
+
+brax is not vendored (parity unpinned at the float level), so the restatement is pinned to
+the geometry it claims to compute: for every one of a box's 12 triangles, the closest points
+of the capsule's segment and the triangle, a contact per triangle closer than the radius with
+penetration r - distance and the normal along (segment point - triangle point).  The reference
+here triangulates the rotated box in world coordinates (the wall frame is not used), samples
+the segment densely and takes the exact point-triangle distance at every sample (Ericson's
+region test, float64), so its minimum is within the sampling step of the true segment-triangle
+distance.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import orc
+
+# wall boxes: (centre xy, z rotation in degrees, half extents), z centre / half height 0.5 as
+# every arena wall (po_brax/envs/utils.py:6-28); the HH T-maze and TAG arena rotations plus
+# arbitrary angles
+WALLS = [((0.0, 8.5), 0.0, (6.75, 0.5)), ((6.75, 7.0), 90.0, (1.5, 0.5)), ((4.625, 5.5), 180.0, (2.125, 0.5)),
+         ((0.0, -5.75), 180.0, (5.75, 0.25)), ((1.0, 2.0), 33.0, (2.0, 0.3)), ((-1.0, 0.5), 127.5, (0.7, 0.45))]
+
+
+def _wall(c, deg, h):
+    a = np.deg2rad(np.float32(deg))
+    return np.array([c[0], c[1], 0.5, np.cos(a), np.sin(a), h[0], h[1], 0.5], np.float32)
+
+
+def _triangles(w):
+    """the box's 12 triangles in world coordinates: faces -x, +x, -y, +y, -z, +z, each split
+    along its (-a, -b) -> (+a, +b) diagonal (the restatement's face order and split)"""
+    c = w[:3].astype(np.float64)
+    ca, sa = float(w[3]), float(w[4])
+    h = w[5:8].astype(np.float64)
+    R = np.array([[ca, -sa, 0.0], [sa, ca, 0.0], [0.0, 0.0, 1.0]])
+    tris = []
+    for k in range(3):
+        ka, kb = (1, 2) if k == 0 else ((0, 2) if k == 1 else (0, 1))
+        for sg in (-1.0, 1.0):
+            def vert(ua, ub):
+                p = np.zeros(3)
+                p[k] = sg * h[k]
+                p[ka] = ua * h[ka]
+                p[kb] = ub * h[kb]
+                return c + R @ p
+            v0, v1, v2, v3 = vert(-1, -1), vert(1, -1), vert(1, 1), vert(-1, 1)
+            tris += [(v0, v1, v2), (v0, v2, v3)]
+    return tris
+
+
+def _closest_on_triangle(p, a, b, c):
+    """Ericson, Real-Time Collision Detection 5.1.5 (float64), vectorised over points p (n, 3)"""
+    ab, ac = b - a, c - a
+    ap = p - a
+    d1, d2 = ap @ ab, ap @ ac
+    bp = p - b
+    d3, d4 = bp @ ab, bp @ ac
+    cp = p - c
+    d5, d6 = cp @ ab, cp @ ac
+    va = d3 * d6 - d5 * d4
+    vb = d5 * d2 - d1 * d6
+    vc = d1 * d4 - d3 * d2
+    out = np.empty_like(p)
+    # interior by default
+    denom = 1.0 / np.where(va + vb + vc == 0, 1.0, va + vb + vc)
+    v, w = vb * denom, vc * denom
+    out[:] = a + ab * v[:, None] + ac * w[:, None]
+    m = (vc <= 0) & (d1 >= 0) & (d3 <= 0)
+    t = np.where(m, d1 / np.where(d1 - d3 == 0, 1, d1 - d3), 0)
+    out[m] = (a + ab * t[:, None])[m]
+    m2 = (vb <= 0) & (d2 >= 0) & (d6 <= 0)
+    t = np.where(m2, d2 / np.where(d2 - d6 == 0, 1, d2 - d6), 0)
+    out[m2] = (a + ac * t[:, None])[m2]
+    m3 = (va <= 0) & ((d4 - d3) >= 0) & ((d5 - d6) >= 0)
+    t = np.where(m3, (d4 - d3) / np.where((d4 - d3) + (d5 - d6) == 0, 1, (d4 - d3) + (d5 - d6)), 0)
+    out[m3] = (b + (c - b) * t[:, None])[m3]
+    out[(d1 <= 0) & (d2 <= 0)] = a
+    out[(d3 >= 0) & (d4 <= d3)] = b
+    out[(d6 >= 0) & (d5 <= d6)] = c
+    return out
+
+
+def _reference(w, pa, pb, seg, r, n_samples=4001):
+    """per triangle: (distance, segment parameter u, segment point, triangle point)"""
+    u = np.linspace(0.0, 1.0, n_samples) if seg else np.zeros(1)
+    P = pa[None, :] + u[:, None] * ((pb - pa) if seg else 0.0)
+    res = []
+    for tri in _triangles(w):
+        q = _closest_on_triangle(P, *tri)
+        d = np.linalg.norm(P - q, axis=1)
+        i = int(np.argmin(d))
+        res.append((d[i], u[i], P[i], q[i]))
+    return res
+
+
+def _case(rng, w):
+    """a capsule segment (length <= 0.57, the Ant's lower leg) placed near a random point of the
+    wall's surface, radius 0.08 (legs) or a sphere of 0.25 (torso)"""
+    c, ca, sa, h = w[:3].astype(np.float64), float(w[3]), float(w[4]), w[5:8].astype(np.float64)
+    R = np.array([[ca, -sa, 0.0], [sa, ca, 0.0], [0.0, 0.0, 1.0]])
+    loc = rng.uniform(-1.0, 1.0, 3) * h
+    k = rng.integers(3)
+    loc[k] = np.sign(rng.uniform(-1, 1)) * h[k]
+    centre = c + R @ (loc + rng.normal(0, 0.06, 3))
+    if rng.uniform() < 0.2:
+        return centre, centre, False, 0.25
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    half = rng.uniform(0.05, 0.283)
+    return centre + half * d, centre - half * d, True, 0.08
+
+
+@pytest.mark.parametrize("wi", range(len(WALLS)))
+def test_mesh_contacts_match_brute_force_geometry(wi):
+    rng = np.random.default_rng(100 + wi)
+    w = _wall(*WALLS[wi])
+    checked = 0
+    for _ in range(150):
+        pa, pb, seg, r = _case(rng, w)
+        pa32, pb32 = pa.astype(np.float32), pb.astype(np.float32)
+        got = orc.mesh_contacts(w, pa32, pb32, seg, r)
+        ref = _reference(w, pa32.astype(np.float64), pb32.astype(np.float64), seg, r)
+        step = (np.linalg.norm(pb - pa) / 4000.0) if seg else 0.0
+        tol = step + 2e-5
+        expect = [t for t, (d, *_rest) in enumerate(ref) if d < r - tol]
+        maybe = [t for t, (d, *_rest) in enumerate(ref) if d < r + tol]
+        assert len(expect) <= len(got) <= len(maybe), (wi, len(got), [ref[t][0] for t in maybe])
+        # the reported contacts, in triangle order, are the penetrating triangles
+        j = 0
+        for t in maybe:
+            d, u, S, Q = ref[t]
+            if j >= len(got):
+                assert t not in expect
+                continue
+            tau, nx, ny, nz, pen = (float(x) for x in got[j])
+            if abs((r - pen) - d) > tol + 1e-6:  # not this triangle: must be a borderline one
+                assert t not in expect, (wi, t, r - pen, d)
+                continue
+            j += 1
+            checked += 1
+            # the normal points from the triangle point to the segment point (when apart)
+            if d > 1e-3:
+                nref = (S - Q) / d
+                assert np.dot(nref, [nx, ny, nz]) > 0.999, (wi, t, nref, (nx, ny, nz))
+            # the contact sits on the segment: x + tau e0 with tau = 1 - 2 u
+            if seg and d > 1e-3:
+                Sg = 0.5 * (pa + pb) + tau * 0.5 * (pa - pb)
+                assert np.linalg.norm(Sg - S) < 5e-3 + 2 * step, (wi, t, Sg, S)
+        assert j == len(got)
+    assert checked > 20  # enough penetrating triangles were exercised
+
+
+def test_mesh_face_split_and_order():
+    """A leg lying flat against the +y face of an axis-aligned wall, crossing the face's diagonal:
+    both triangles of that face report a contact (face order -x, +x, -y, +y, ...: entries of
+    the +y face), each with the face's outward normal and the same depth."""
+    w = _wall((0.0, 0.0), 0.0, (2.0, 0.5))
+    y = 0.5 + 0.05  # segment 0.05 outside the face, radius 0.08: 0.03 deep
+    a, b = np.array([-0.2, y, 0.3], np.float32), np.array([0.2, y, 0.7], np.float32)
+    got = orc.mesh_contacts(w, a, b, True, 0.08)
+    assert len(got) == 2
+    for row in got:
+        tau, nx, ny, nz, pen = row
+        assert abs(nx) < 1e-6 and abs(ny - 1.0) < 1e-6 and abs(nz) < 1e-6
+        assert abs(pen - 0.03) < 1e-5
+
+
+def test_mesh_deep_segment_crossing_a_face():
+    """A segment piercing a face (distance 0): the face's outward normal and penetration r,
+    the contact on the segment at the crossing point."""
+    w = _wall((0.0, 0.0), 0.0, (2.0, 0.5))
+    a, b = np.array([0.3, 0.8, 0.4], np.float32), np.array([0.3, 0.2, 0.4], np.float32)
+    got = orc.mesh_contacts(w, a, b, True, 0.08)
+    pierced = [g for g in got if abs(g[4] - 0.08) < 1e-7]
+    assert pierced, got
+    for tau, nx, ny, nz, pen in pierced:
+        assert (nx, ny, nz) == (0.0, 1.0, 0.0)
+        # crossing y = 0.5: u = 0.5 -> tau = 0
+        assert abs(tau) < 1e-6
+
+
+def test_face_cull_is_exact_on_rollouts():
+    """The face cull (gap >= r + 1e-3) never changes a contact: a mesh-model rollout with the
+    cull and one evaluating every face of every wall are bit-identical (HH spawns against the
+    T-maze's bottom wall; TAG and GA arenas)."""
+    import pob_np as P
+    L = orc.lib()
+    for name in ("ant_heavenhell", "ant_tag"):
+        e = orc.OracleEnv(name, wall_contact=0)
+        k = P.split(P.prngkey(11), 129)[1:]
+        acts = np.random.default_rng(3).uniform(-1, 1, (40, 128, 8)).astype(np.float32)
+        outs = []
+        for cull in (1, 0):
+            L.orc_set_face_cull(cull)
+            try:
+                s = e.reset(k, first=True, nthreads=8)
+                for a in acts:
+                    e.step(s, a, flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=1000, nthreads=8, inplace=True)
+            finally:
+                L.orc_set_face_cull(1)
+            outs.append(s)
+        for f in ("pos", "rot", "vel", "ang", "obs"):
+            assert np.array_equal(outs[0][f], outs[1][f]), (name, f)

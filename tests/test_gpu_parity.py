@@ -392,7 +392,8 @@ def _near_wall(xy, walls, reach):
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag"])
 def test_step_parity_against_walls(name):
     """Ants teleported onto random points of the arena's bounding box (many start touching
-    or inside a wall): every sphere-box branch (outside, inside, deepest-end selection,
+    or inside a wall): every capsule x triangle branch (end points, edges, the segment crossing a
+    face, several faces / walls per capsule,
     several walls per wave) runs; one-step parity for 8 steps."""
     B, T = 512, 8
     env = _envs().create(name, batch_size=B, episode_length=1000)
