@@ -1,0 +1,109 @@
+"""CPU: the kernels' capsule x TriangulatedBox code (po-brax_amd/csrc/pob_mesh.h, the device
+header itself) compiled for the host against a small shim, bit-compared with the oracle's
+independent restatement (oracle/pob_oracle.c capsule_wall_mesh) on random capsule / wall
+pairs: the face cull, the per-face closest-point candidates, the contacts' order, tau, normal
+and penetration.  (The shim provides the few gfx950 builtins the header uses with their exact
+host equivalents: v_med3_f32 -> fminf(fmaxf()), correctly rounded reciprocal / square root ->
+IEEE 1/x and sqrtf, as the kernels' fast forms are exact in range.)"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import orc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+MESH_H = os.path.join(ROOT, "po-brax_amd", "csrc", "pob_mesh.h")
+
+SHIM = r"""
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#define POB_D static inline
+struct v3 { float x, y, z; };
+struct float2 { float x, y; };
+#define FMA(a, b, c) fmaf((a), (b), (c))
+POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+POB_D float clamp_sym(float x, float h) { return fminf(fmaxf(x, -h), h); }
+#define __builtin_amdgcn_fmed3f(x, lo, hi) fminf(fmaxf((x), (lo)), (hi))
+#define __builtin_inff() INFINITY
+struct HostGuard {
+  float rcp(float x) { return 1.0f / x; }
+  void sqrt_rcp(float x, float &s, float &i) { s = sqrtf(x); i = 1.0f / s; }
+};
+"""
+
+DRIVER = r"""
+extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b, int seg, float r, float *out) {
+  MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
+  const float cz = w[2], hz = w[7];
+  const v3 La = mwall_local(W, cz, V(a[0], a[1], a[2]));
+  const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
+  const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
+  const float T = (r * r) * 1.00000095367431640625f;
+  HostGuard g;
+  int n = 0;
+  for (int f = 0; f < 6; ++f) {
+    if (!((fm >> f) & 1u)) continue;
+    mesh_face(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float pen) {
+      const v3 nw = mwall_world_n(W, nl);
+      out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
+      ++n;
+    });
+  }
+  return n;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def host_mesh(tmp_path_factory):
+    d = tmp_path_factory.mktemp("meshhost")
+    body = open(MESH_H).read().replace('#include "pob_math.h"', "")
+    src = d / "mesh_host.cpp"
+    src.write_text(SHIM + body + DRIVER)
+    so = d / "mesh_host.so"
+    subprocess.check_call(["g++", "-O2", "-mfma", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+                           "-shared", "-o", str(so), str(src)])
+    lib = C.CDLL(str(so))
+    FP = C.POINTER(C.c_float)
+    lib.host_mesh_contacts.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def test_kernel_mesh_code_equals_oracle_bitwise(host_mesh):
+    rng = np.random.default_rng(2024)
+    n_contacts = n_cases = 0
+    for it in range(20000):
+        deg = rng.choice([0.0, 90.0, 180.0, 270.0, rng.uniform(0, 360)])
+        a = np.deg2rad(np.float32(deg))
+        h = np.array([rng.uniform(0.2, 7.0), rng.uniform(0.2, 0.6), 0.5], np.float32)
+        w = np.array([rng.uniform(-8, 8), rng.uniform(-8, 8), 0.5, np.cos(a), np.sin(a), h[0], h[1], h[2]], np.float32)
+        R = np.array([[w[3], -w[4], 0], [w[4], w[3], 0], [0, 0, 1]], np.float64)
+        loc = rng.uniform(-1.0, 1.0, 3) * h
+        k = rng.integers(3)
+        loc[k] = np.sign(rng.uniform(-1, 1)) * h[k]
+        centre = w[:3] + R @ (loc + rng.normal(0, 0.08, 3))
+        seg = rng.uniform() > 0.15
+        r = np.float32(0.08 if seg else 0.25)
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        half = rng.uniform(0.0, 0.3) if seg else 0.0
+        pa = (centre + half * d).astype(np.float32)
+        pb = (centre - half * d).astype(np.float32) if seg else pa.copy()
+        ref = orc.mesh_contacts(w, pa, pb, bool(seg), float(r))
+        out = np.zeros((12, 5), np.float32)
+        n = host_mesh.host_mesh_contacts(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out))
+        got = out[:n]
+        assert got.shape == ref.shape and np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
+            (it, deg, w, pa, pb, seg, got, ref)
+        n_cases += 1
+        n_contacts += n
+    assert n_contacts > 2000, n_contacts
