@@ -4,6 +4,7 @@ set -o pipefail
 OUT=gpurun_out/${TAG:-r4b}
 mkdir -p $OUT
 export TMPDIR=/tmp
+python scripts/check_fresh.py || exit 3
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1 || { grep -E "^E |FAILED|Error" $OUT/pytest_gpu.log | head -60; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 for spec in "default:" "hh_4096:--global-batch 4096" "ga_16384:--env ant_gather --global-batch 16384" "tag_8192:--env ant_tag --global-batch 8192" "tag_65536:--env ant_tag" "legacy:--legacy-spring"; do

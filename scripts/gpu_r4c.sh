@@ -5,6 +5,7 @@ set -o pipefail
 OUT=gpurun_out/${TAG:-r4c}
 mkdir -p $OUT
 export TMPDIR=/tmp
+python scripts/check_fresh.py || exit 3
 for spec in "default:" "hh_4096:--global-batch 4096" "ga_16384:--env ant_gather --global-batch 16384" "tag_8192:--env ant_tag --global-batch 8192" "tag_65536:--env ant_tag" "mixed_f16_32768:--env mixed --qp-dtype f16 --global-batch 32768" "legacy:--legacy-spring" "gym_hh:--gym --no-cpu-baseline"; do
   name=${spec%%:*}; args=${spec#*:}
   cb="--no-cpu-baseline"; [ "$name" = "default" ] && cb=""; [ "$name" = "legacy" ] && cb=""
