@@ -176,8 +176,11 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
     MCand dg;
     dg.d2 = __builtin_inff(); dg.u = 0.0f; dg.da = 0.0f; dg.db = 0.0f; dg.dw = 0.0f;
     mseg_edge(g, dg, S, -ha, -hb, w0, ha2, hb2, e_d, i_d);
+    // (taken on its own squared distance: an untaken dg -- a NaN or overflowing candidate,
+    // which the oracle never takes -- keeps d2 = inf, not the 0 of its cleared fields)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) mcand_take(c[t], dg.u, dg.da, dg.db, dg.dw);
+    for (int t = 0; t < 2; ++t)
+      if (dg.d2 < c[t].d2) c[t] = dg;
     mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a);
     mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);
     // the segment crossing the face plane inside the triangle

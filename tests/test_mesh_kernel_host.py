@@ -107,3 +107,27 @@ def test_kernel_mesh_code_equals_oracle_bitwise(host_mesh):
         n_cases += 1
         n_contacts += n
     assert n_contacts > 2000, n_contacts
+
+
+def test_kernel_mesh_code_non_finite_segments(host_mesh):
+    """Segments with NaN, infinite or overflowing end points (a body whose rotation went NaN
+    keeps a finite centre, the out-of-range parity case): no contact where the oracle has none,
+    the same contacts where one end point is sound.  (The diagonal candidate shared by both
+    triangles must be taken on its own squared distance: a never-taken one is not at 0.)"""
+    rng = np.random.default_rng(77)
+    bad = [np.nan, np.inf, -np.inf, 1e30, -1e30, 3e19]
+    w = np.array([0.0, 0.0, 0.5, 1.0, 0.0, 6.75, 0.5, 0.5], np.float32)
+    n_cases = 0
+    for it in range(3000):
+        pa = np.array([rng.uniform(-7, 7), rng.uniform(-0.7, 0.7), rng.uniform(-0.1, 1.1)], np.float32)
+        pb = (pa + rng.normal(0, 0.3, 3)).astype(np.float32)
+        for p in (pa, pb):
+            for k in range(3):
+                if rng.uniform() < 0.3:
+                    p[k] = np.float32(bad[rng.integers(len(bad))])
+        ref = orc.mesh_contacts(w, pa, pb, True, 0.08)
+        out = np.zeros((12, 5), np.float32)
+        n = host_mesh.host_mesh_contacts(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
+        assert n == len(ref) and np.array_equal(out[:n].view(np.uint32), ref.view(np.uint32)), (it, pa, pb, n, ref)
+        n_cases += 1
+    assert n_cases == 3000
