@@ -266,6 +266,9 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
     const uint32_t lw = qwall_mask(S, b);
     qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
+#ifdef POB_EXP_NO_WALK
+  return;  // timing experiment only: broadphase and face cull, no face walk
+#endif
   qmesh_walk(g, S, LT, WT, ms, M, &ms.mc, [&](const int l, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
     const q4 q = qpick4(l, b.q);
@@ -298,6 +301,9 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
     }
   }
   if (!WALLS || !__any(ms.mc != 0u)) return;
+#ifdef POB_EXP_NO_VWALK
+  return;  // timing experiment only: no velocity-pass re-walk
+#endif
   POB_FENCE();
   uint64_t M[QNB];
   qmesh_items(S, LT, WT, ms.mc, ms, M);

@@ -1,21 +1,26 @@
 #!/bin/bash
-# Round 4: the small-batch floor decomposition -- configs 2 / 3 / 4's per-GPU batch timed with
-# the product build, a build without wall contacts and one without physics
-# (build_variants_t/, timing experiments), interleaved three times; then per-wave phase clocks
-# (POB_EXP_TIMING build) for HH B = 4 096 and TAG B = 8 192.
+# Round 4: where the step time goes after the mesh contact port -- each config timed with the
+# product build and timing-experiment builds (build_variants_t/: no wall contacts, no face walk
+# (broadphase + face cull only), no velocity-pass re-walk, no physics), interleaved twice;
+# then per-wave phase clocks (POB_EXP_TIMING build) for HH B = 4 096 and TAG B = 8 192.
 OUT=gpurun_out/r4f
 mkdir -p $OUT
 export TMPDIR=/tmp
 python scripts/check_fresh.py || exit 3
-for r in 1 2 3; do
+P=po-brax_amd/po_brax_amd/libpob.so; T=build_variants_t
+run() {  # env B lib r
+  local tag=$(basename $3 .so)
+  POB_LIB=$PWD/$3 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 200 --env $1 --batch $2 \
+    > $OUT/$tag.$1.$2.$4.json 2> $OUT/$tag.$1.$2.$4.err || { tail -5 $OUT/$tag.$1.$2.$4.err; exit 1; }
+}
+for r in 1 2; do
   for cfg in "ant_heavenhell 4096" "ant_tag 8192" "ant_gather 16384"; do
-    set -- $cfg
-    for lib in po-brax_amd/po_brax_amd/libpob.so build_variants_t/nowalls.so build_variants_t/nophys.so; do
-      tag=$(basename $lib .so)
-      POB_LIB=$PWD/$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps 300 --env $1 --batch $2 \
-        > $OUT/$tag.$1.$2.$r.json 2> $OUT/$tag.$1.$2.$r.err || { tail -5 $OUT/$tag.$1.$2.$r.err; exit 1; }
-    done
+    for lib in $P $T/nowalls.so $T/nophys.so; do run $cfg $lib $r; done
   done
+  for cfg in "ant_heavenhell 65536" "ant_tag 65536"; do
+    for lib in $P $T/nowalls.so $T/nowalk.so $T/novwalk.so $T/nophys.so; do run $cfg $lib $r; done
+  done
+  echo "round $r done"
 done
 python - <<'PY'
 import glob, json, collections, statistics
@@ -28,6 +33,6 @@ for k in sorted(d):
 PY
 for cfg in "4096 ant_heavenhell" "8192 ant_tag"; do
   set -- $cfg
-  POB_LIB=$PWD/build_variants_t/timing.so timeout -k 10 120 python scripts/phase_timing.py $1 $2 > $OUT/phase_$2_$1.txt 2>&1 || { tail -5 $OUT/phase_$2_$1.txt; exit 1; }
+  POB_LIB=$PWD/$T/timing.so timeout -k 10 120 python scripts/phase_timing.py $1 $2 > $OUT/phase_$2_$1.txt 2>&1 || { tail -5 $OUT/phase_$2_$1.txt; exit 1; }
   echo "== phase $2 $1"; tail -12 $OUT/phase_$2_$1.txt
 done
