@@ -910,6 +910,35 @@ static long long pair_flops_executed(const orc_env *e, int w, v3 p, float r) {
 }
 #endif
 
+#ifdef ORC_COUNT_FLOPS
+/* Statistics hook (FLOP build, mode 1, single-threaded; no effect on results): per env and
+ * collide substep, the face items each four-lane kernel lane walks -- the faces the face cull
+ * keeps of its three bodies (torso, Aux k+1, leg k) over the walls of its broadphase mask --
+ * into buf[(env * nsub + substep) * 4 + k] (scripts/wall_walk_stats.py) */
+static int *g_items_buf = NULL;
+static int g_items_nsub = 0, g_items_env = 0, g_items_sub = 0;
+void orc_items_record(int *buf, int nsub) { g_items_buf = buf; g_items_nsub = nsub; }
+static int face_items(const orc_env *e, int i, int w, v3 pa, v3 pb) {
+  const float c = e->wall_cos[w], s = e->wall_sin[w];
+  const v3 h = e->wall_h[w];
+  const v3 da = vsub(pa, e->wall_c[w]), db = vsub(pb, e->wall_c[w]);
+  const v3 La = V(fmaf(da.y, s, da.x * c), fmaf(da.y, c, -(da.x * s)), da.z);
+  const v3 Lb = V(fmaf(db.y, s, db.x * c), fmaf(db.y, c, -(db.x * s)), db.z);
+  const float R = e->cap_r[i] + WALL_CULL_MARGIN;
+  int n = 0;
+  for (int f = 0; f < 6; ++f) {
+    const int k = f >> 1, ka = k == 0 ? 1 : 0, kb = k == 2 ? 1 : 2;
+    const float w0 = ((f & 1) ? 1.0f : -1.0f) * comp(h, k), ha = comp(h, ka), hb = comp(h, kb);
+    const float Aw = comp(La, k), Bw = comp(Lb, k), Aa = comp(La, ka), Ba = comp(Lb, ka), Ab = comp(La, kb), Bb = comp(Lb, kb);
+    const float gw = fmaxf(fminf(Aw, Bw) - w0, w0 - fmaxf(Aw, Bw));
+    const float ga = fmaxf(fminf(Aa, Ba) - ha, -ha - fmaxf(Aa, Ba));
+    const float gb = fmaxf(fminf(Ab, Bb) - hb, -hb - fmaxf(Ab, Bb));
+    if (!(gw >= R || ga >= R || gb >= R)) ++n;
+  }
+  return n;
+}
+#endif
+
 /* contact detection for the collide substep: ground (CapsulePlane on the torso and the four
  * lower legs), then per capsule its Ant x Arena contacts (wall_contact 0: every penetrating
  * triangle of every wall; 1: the deepest sphere-box contact over end points x walls). */
@@ -929,6 +958,24 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
   if (g_flop_mode == 1) kernel_wall_masks(e, b, lane_mask);
 #endif
   if (e->n_walls > 0) CST(7, 1);
+#ifdef ORC_COUNT_FLOPS
+  if (g_flop_mode == 1 && g_items_buf && g_items_sub < g_items_nsub) {
+    v3 sa[NDYN], sb[NDYN];
+    for (int i = 0; i < NDYN; ++i) {
+      sa[i] = cpoint(e->cap_end[i][0], b->q[i], b->x[i]);
+      sb[i] = cpoint(e->cap_end[i][e->cap_nend[i] - 1], b->q[i], b->x[i]);
+    }
+    for (int k = 0; k < 4; ++k) {
+      const int l[3] = {0, 2 * k + 1, 2 * k + 2};
+      int n = 0;
+      for (int w = 0; w < e->n_walls; ++w)
+        if ((lane_mask[k] >> w) & 1u)
+          for (int t = 0; t < 3; ++t) n += face_items(e, l[t], w, sa[l[t]], sb[l[t]]);
+      g_items_buf[((size_t)g_items_env * g_items_nsub + g_items_sub) * 4 + k] = n;
+    }
+    ++g_items_sub;
+  }
+#endif
   for (int i = 0; i < NDYN; ++i) {
     v3 pe[2]; /* the capsule's end points in world (independent of the wall) */
     for (int q = 0; q < e->cap_nend[i]; ++q) pe[q] = cpoint(e->cap_end[i][q], b->q[i], b->x[i]);
@@ -1525,6 +1572,9 @@ static void step_one(const orc_env *e, int b, const orc_state *in, const float *
   if (flags & ORC_F_AUTORESET) { if (prev_done != 0.0f) steps = 0.0f; }
 
   body_t bd; load_body(e, pos, rot, vel, ang, &bd);
+#ifdef ORC_COUNT_FLOPS
+  g_items_env = b; g_items_sub = 0;
+#endif
   const float x_before = bd.x[0].x;
   v3 cv[NDYN], ca[NDYN];
   physics_step(e, &bd, act + (size_t)b * NJ, cv, ca);

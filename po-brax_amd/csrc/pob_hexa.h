@@ -84,32 +84,8 @@ struct HMesh {
 
 // Contacts of a collide substep on one lane (oracle order: ground, then walls in wall / face /
 // triangle order).  Walls: the broadphase over the walls' grown boxes (registers, HWalls) by
-// the body centre, the face items of the lane's body (pob_mesh.h cull), then a walk over them
-// one per lane per iteration with the wall rows from LDS (WT).  The torso is the sphere.
-template <int MW, class G, class F>
-POB_D void hmesh_walk(G &g, const float *HT, const float *WT, const HWalls<MW> &HW, const bool torso, const HMesh &ms,
-                      uint64_t M, uint64_t *hit, F &&emit) {
-  const float r = HT[HT_R];
-  const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-  while (__any(M != 0ull)) {
-    const bool on = M != 0ull;
-    const int bit = on ? __builtin_ctzll(M) : 0;
-    M &= M - 1ull;
-    if (on) {
-      const int w = bit >> 3, f = bit & 7;
-      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
-      const v3 La = mwall_local(W, HW.cz, ms.a);
-      const v3 Lb = torso ? La : mwall_local(W, HW.cz, ms.b);
-      bool any = false;
-      mesh_face(g, f, La, Lb, !torso, W.hx, W.hy, HW.hz, r, T, [&](const float tau, const v3 nl, const float pen) {
-        any = true;
-        emit(tau, mwall_world_n(W, nl), pen);
-      });
-      if (hit && any) *hit |= 1ull << bit;
-    }
-  }
-}
-
+// the body centre, the face items of the lane's body (pob_mesh.h cull), then the wave's face
+// walk (pob_mesh.h mesh_wave_walk) with the wall rows from LDS (WT).  The torso is the sphere.
 template <int MW, class G>
 POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
                               const bool torso, const HBody &b, const v3 px, const q4 pq, HGround &gc, HMesh &ms,
@@ -150,8 +126,12 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
     const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, R);
     M |= on ? (uint64_t)fm << (8 * w) : 0ull;
   }
-  hmesh_walk<MW>(g, HT, WT, HW, torso, ms, M, &ms.mc, [&](const float tau, const v3 n, const float pen) {
+  uint64_t Ms[1] = {M};
+  mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
+                    [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
+                    [&](const int, const int bit, const float tau, const v3 n, const float pen) {
     owall_position(g, SC, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+    ms.mc |= 1ull << bit;
   });
 }
 
@@ -163,7 +143,10 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
     ocontact_vel_one(g, SC, true, gc.pen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
   if (MW == 0 || !__any(ms.mc != 0ull)) return;
   const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
-  hmesh_walk<MW>(g, HT, WT, HW, torso, ms, ms.mc, (uint64_t *)nullptr, [&](const float tau, const v3 n, const float pen) {
+  uint64_t Ms[1] = {ms.mc};
+  mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
+                    [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
+                    [&](const int, const int, const float tau, const v3 n, const float pen) {
     ocontact_vel_pe(g, SC, false, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.v, b.w, dV, dW);
   });
 }

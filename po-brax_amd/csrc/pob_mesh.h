@@ -215,3 +215,245 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
 POB_D v3 mwall_world_n(const MWall &W, const v3 nl) {
   return V(FMA(-nl.y, W.s, nl.x * W.c), FMA(nl.y, W.c, nl.x * W.s), nl.z);
 }
+
+// ---------------------------------------------------------------- one candidate at a time
+// mesh_face's work split into independent pieces, so that the lanes of a wave can evaluate a
+// face's candidates side by side (mesh_wave_walk): the face frame, each candidate on its own,
+// and the contact of a triangle's winner.  The first strict minimum of mesh_face's sequential
+// candidate order is the lexicographic minimum of (d2, position in that order) over the
+// candidates (mcand_take never stores a NaN; a candidate it does not take keeps d2 = +inf), so
+// the winner, and with it every bit of the contact, is mesh_face's.
+struct MFace {
+  int k;
+  float sg, ha, hb, w0, ha2, hb2, i_d;
+  float pa, pb, pw, qa, qb, qw;  // end points A and B in face coordinates (a, b, w)
+};
+template <class G>
+POB_D MFace mface(G &g, const int f, const v3 A, const v3 B, const float hx, const float hy, const float hz) {
+  MFace F;
+  const int k = f >> 1;
+  F.k = k;
+  F.sg = (f & 1) ? 1.0f : -1.0f;
+  F.ha = k == 0 ? hy : hx;
+  F.hb = k == 2 ? hy : hz;
+  F.w0 = F.sg * (k == 0 ? hx : (k == 1 ? hy : hz));
+  F.pa = k == 0 ? A.y : A.x; F.pb = k == 2 ? A.y : A.z; F.pw = k == 0 ? A.x : (k == 1 ? A.y : A.z);
+  F.qa = k == 0 ? B.y : B.x; F.qb = k == 2 ? B.y : B.z; F.qw = k == 0 ? B.x : (k == 1 ? B.y : B.z);
+  F.ha2 = 2.0f * F.ha;
+  F.hb2 = 2.0f * F.hb;
+  F.i_d = g.rcp(FMA(F.hb2, F.hb2, F.ha2 * F.ha2));
+  return F;
+}
+
+// Candidate kk of triangle t, in mesh_face's order: 0 / 1 the end point A / B, 2..4 the
+// triangle's edges (t = 0: bottom, right, diagonal; t = 1: diagonal, top, left), 5 the segment
+// crossing the face plane inside the triangle.  Any other kk, or a candidate that does not
+// apply (a sphere has its point only; no crossing), stays at d2 = +inf.  The same operations
+// on the same operands as mesh_face (its reciprocals 1 / e_a, 1 / e_b, 1 / (D . D) are taken
+// here only by the candidates that use them: the same values).
+template <class G>
+POB_D MCand mface_cand(G &g, const MFace &F, const bool seg, const int t, const int kk) {
+  MCand c;
+  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
+  if (kk == 0 || (kk == 1 && seg)) {
+    const float pa = kk == 0 ? F.pa : F.qa, pb = kk == 0 ? F.pb : F.qb, pw = kk == 0 ? F.pw : F.qw;
+    float qa, qb;
+    mtri_closest(t == 1, F.ha, F.hb, F.ha2, F.hb2, F.i_d, pa, pb, qa, qb);
+    mcand_take(c, kk == 0 ? 0.0f : 1.0f, pa - qa, pb - qb, pw - F.w0);
+  } else if (seg && kk >= 2 && kk <= 5) {
+    MSeg S;
+    S.aa_ = F.pa; S.ab = F.pb; S.aw = F.pw;
+    S.Da = F.qa - F.pa; S.Db = F.qb - F.pb; S.Dw = F.qw - F.pw;
+    if (kk < 5) {
+      S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
+      S.inv_aa = g.rcp(S.aa);
+      const bool diag = t == 0 ? kk == 4 : kk == 2;
+      const bool first = t == 0 ? kk == 2 : kk == 3;  // bottom (t = 0) / top (t = 1): along a
+      const float ha = F.ha, hb = F.hb, ha2 = F.ha2, hb2 = F.hb2;
+      // edges: bottom (-ha, -hb) + (2ha, 0), right (ha, -hb) + (0, 2hb), diagonal (-ha, -hb) +
+      // (2ha, 2hb), top (ha, hb) + (-2ha, 0), left (-ha, hb) + (0, -2hb)
+      const float e0a = diag ? -ha : (t == 0 ? (first ? -ha : ha) : (first ? ha : -ha));
+      const float e0b = diag ? -hb : (t == 0 ? -hb : hb);
+      const float fa = diag ? ha2 : (first ? (t == 0 ? ha2 : -ha2) : 0.0f);
+      const float fb = diag ? hb2 : (first ? 0.0f : (t == 0 ? hb2 : -hb2));
+      const float ee = diag ? FMA(hb2, hb2, ha2 * ha2) : (first ? ha2 * ha2 : hb2 * hb2);
+      mseg_edge(g, c, S, e0a, e0b, F.w0, fa, fb, ee, diag ? F.i_d : g.rcp(ee));
+    } else {
+      const float aw = F.pw - F.w0, bw = F.qw - F.w0;
+      if (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f))) {
+        const float u = aw * g.rcp(aw - bw);
+        const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
+        if (mtri_inside(t == 1, F.ha, F.hb, sa, sb)) mcand_take(c, u, 0.0f, 0.0f, sw - F.w0);
+      }
+    }
+  }
+  return c;
+}
+
+// the contact of a triangle whose winning candidate is c (mesh_face's emission): tau, the
+// wall-frame normal and the penetration; false when the triangle does not penetrate
+template <class G>
+POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, const float T, float &tau, v3 &nl,
+                         float &pen) {
+  if (!(c.d2 < T)) return false;
+  float dist, inv;
+  g.sqrt_rcp(c.d2, dist, inv);
+  pen = r - dist;
+  if (!(pen > 0.0f)) return false;
+  float na, nb, nw;
+  if (c.d2 > 0.0f) { na = c.da * inv; nb = c.db * inv; nw = c.dw * inv; }
+  else { na = 0.0f; nb = 0.0f; nw = F.sg; }
+  const int k = F.k;
+  nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
+  tau = 1.0f - 2.0f * c.u;
+  return true;
+}
+
+#ifndef POB_MESH_HOST
+// ---------------------------------------------------------------- the wave's face walk
+// Walk the lanes' face items (M[s]: bit 8 w + f for face f of wall w of the lane's body slot
+// s; slots, then bits, in increasing order: the oracle's contact order per body) and call
+// apply(s, bit, tau, n_world, pen) on the owning lane for every penetrating triangle, in
+// order.  seg_of(s, A, B, r, seg) gives a slot's segment (world end points), radius and
+// whether it is a capsule (false: the torso sphere at A).
+//
+// A face costs ~1 000 instructions evaluated on one lane (its twelve candidates and two
+// emissions one after another) and few lanes of a wave hold one at a time (0.7 items on the
+// busiest lane per wave and collide substep on HH rollouts, scripts/wall_walk_stats.py), so
+// the wave shares them out: each round takes the next item of up to four lanes and gives
+// each of those faces sixteen lanes -- lane 8 t + kk of the group computes candidate kk of
+// triangle t -- reduces the candidates to each triangle's winner (DPP, lexicographic (d2, kk)
+// minimum over the eight lanes), lets the winner lane compute the contact, and hands it to
+// the owner (ds_bpermute), which applies its triangles in order.  Needs all 64 lanes active
+// (the DPP reduction reads every lane of a group); with lanes masked off -- the batch's last
+// wave, a masked reset -- each lane walks its own items (mesh_lane_walk).
+POB_D float mlane_read(const float v, const int src) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+POB_D int mlane_read_i(const int v, const int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+template <int CTRL>
+POB_D void mlexmin_dpp(float &d, int &kk) {
+  const float od = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), CTRL, 0xf, 0xf, true));
+  const int ok = __builtin_amdgcn_mov_dpp(kk, CTRL, 0xf, 0xf, true);
+  const bool take = (od < d) | ((od == d) & (ok < kk));
+  d = take ? od : d;
+  kk = take ? ok : kk;
+}
+
+// each lane walks its own items, one face per iteration (mesh_face)
+template <int NB, class G, class SegOf, class Apply>
+POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
+                          Apply &&apply) {
+  while (true) {
+    bool has = false;
+    int s = 0;
+    uint64_t ml = 0ull;
+#pragma unroll
+    for (int q = NB - 1; q >= 0; --q) {
+      const bool h = M[q] != 0ull;
+      s = h ? q : s;
+      ml = h ? M[q] : ml;
+      has = has | h;
+    }
+    if (!__any(has)) break;
+    const int bit = has ? __builtin_ctzll(ml) : 0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) M[q] = (has && s == q) ? (M[q] & (M[q] - 1ull)) : M[q];
+    if (has) {
+      v3 A, B;
+      float r;
+      bool seg;
+      seg_of(s, A, B, r, seg);
+      const MWall W = mwall_row(WT + POB_WALL_FLOATS * (bit >> 3));
+      const v3 La = mwall_local(W, cz, A);
+      const v3 Lb = seg ? mwall_local(W, cz, B) : La;
+      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
+      mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
+        apply(s, bit, tau, mwall_world_n(W, nl), pen);
+      });
+    }
+  }
+}
+
+template <int NB, class G, class SegOf, class Apply>
+POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
+                          Apply &&apply) {
+  if (__ballot(1) != ~0ull) {
+    mesh_lane_walk<NB>(g, WT, cz, hz, M, seg_of, apply);
+    return;
+  }
+  const int lane = (int)__lane_id();
+  const int grp = lane >> 4, tri = (lane >> 3) & 1, kk = lane & 7;
+  while (true) {
+    bool has = false;
+    int s = 0;
+    uint64_t ml = 0ull;
+#pragma unroll
+    for (int q = NB - 1; q >= 0; --q) {
+      const bool h = M[q] != 0ull;
+      s = h ? q : s;
+      ml = h ? M[q] : ml;
+      has = has | h;
+    }
+    const uint64_t req = __ballot(has);
+    if (req == 0ull) break;
+    // the round's owners: the first four lanes with an item (wave-uniform)
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(req >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req, 0u));
+    const bool own = has && rank < 4u;
+    const int bit = has ? __builtin_ctzll(ml) : 0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) M[q] = (own && s == q) ? (M[q] & (M[q] - 1ull)) : M[q];
+    uint64_t m = req;
+    const int o0 = __builtin_ctzll(m);
+    m &= m - 1ull;
+    const int o1 = m != 0ull ? __builtin_ctzll(m) : 0;
+    m &= m - 1ull;
+    const int o2 = m != 0ull ? __builtin_ctzll(m) : 0;
+    m &= m - 1ull;
+    const int o3 = m != 0ull ? __builtin_ctzll(m) : 0;
+    const int nown = __builtin_popcountll(req);
+    // this lane's group: the owner's item, fetched from the owner
+    v3 A, B;
+    float r;
+    bool seg;
+    seg_of(s, A, B, r, seg);
+    const int meta = bit | (seg ? 64 : 0);
+    const int ol = grp == 0 ? o0 : (grp == 1 ? o1 : (grp == 2 ? o2 : o3));
+    const bool gv = grp < nown;
+    const v3 Ao = V(mlane_read(A.x, ol), mlane_read(A.y, ol), mlane_read(A.z, ol));
+    const v3 Bo = V(mlane_read(B.x, ol), mlane_read(B.y, ol), mlane_read(B.z, ol));
+    const float ro = mlane_read(r, ol);
+    const int mo = mlane_read_i(meta, ol);
+    const bool sego = (mo & 64) != 0;
+    const MWall W = mwall_row(WT + POB_WALL_FLOATS * ((mo >> 3) & 7));
+    const v3 La = mwall_local(W, cz, Ao);
+    const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
+    const MFace F = mface(g, mo & 7, La, Lb, W.hx, W.hy, hz);
+    const MCand c = mface_cand(g, F, sego, tri, gv ? kk : 7);
+    // each triangle's winner over its eight lanes
+    float dmin = c.d2;
+    int kmin = kk;
+    mlexmin_dpp<0xB1>(dmin, kmin);   // quad_perm [1, 0, 3, 2]
+    mlexmin_dpp<0x4E>(dmin, kmin);   // quad_perm [2, 3, 0, 1]
+    mlexmin_dpp<0x141>(dmin, kmin);  // row_half_mirror: the other quad of the eight
+    float tau = 0.0f, pen = 0.0f;
+    v3 nw = V(0.0f, 0.0f, 0.0f);
+    bool hit = false;
+    if (gv && kk == kmin) {
+      v3 nl;
+      hit = mface_contact(g, F, c, ro, (ro * ro) * 1.00000095367431640625f, tau, nl, pen);
+      if (hit) nw = mwall_world_n(W, nl);
+    }
+    // the owners take their two triangles' contacts, in order
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int src = 16 * (int)rank + 8 * t;
+      const int wl = src + mlane_read_i(kmin, src);
+      const int h = mlane_read_i(hit ? 1 : 0, wl);
+      const float tw = mlane_read(tau, wl), pw = mlane_read(pen, wl);
+      const v3 nn = V(mlane_read(nw.x, wl), mlane_read(nw.y, wl), mlane_read(nw.z, wl));
+      if (own && h != 0) apply(s, bit, tw, nn, pw);
+    }
+  }
+}
+#endif  // POB_MESH_HOST

@@ -126,41 +126,14 @@ POB_D void hwalls_load(const float *tab, HWalls<MW> &HW) {
 
 // Contacts of a collide substep on one lane (oracle order per body: ground, then walls in
 // wall / face / triangle order).  Walls: the lane's broadphase mask over its two body centres
-// (the boxes from registers, HWalls), the face items per slot (pob_mesh.h cull), then a walk
-// over the items one per lane per iteration with the wall rows from LDS (WT).  The torso (A
+// (the boxes from registers, HWalls), the face items per slot (pob_mesh.h cull), then the
+// wave's face walk (pob_mesh.h mesh_wave_walk) with the wall rows from LDS (WT).  The torso (A
 // slot 0) is the sphere: its segment is the point x (e0 = 0).
-template <int MW, class G, class F>
-POB_D void omesh_walk(G &g, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, const OMesh &ms,
-                      uint64_t (&M)[ONB], uint64_t (*hit)[ONB], F &&emit) {
-  while (__any((M[0] | M[1]) != 0ull)) {
-    const int s = M[0] != 0ull ? 0 : 1;
-    const uint64_t ml = s == 0 ? M[0] : M[1];
-    const bool on = ml != 0ull;
-    const int bit = on ? __builtin_ctzll(ml) : 0;
-    const uint64_t rest = ml & (ml - 1ull);
-    M[0] = s == 0 ? rest : M[0];
-    M[1] = s == 1 ? rest : M[1];
-    if (on) {
-      const int w = bit >> 3, f = bit & 7;
-      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
-      const v3 A = vsel3(s == 0, ms.a[0], ms.a[1]), B = vsel3(s == 0, ms.b[0], ms.b[1]);
-      const float r = s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1];
-      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      const bool seg = !(isA && s == 0);
-      const v3 La = mwall_local(W, HW.cz, A);
-      const v3 Lb = seg ? mwall_local(W, HW.cz, B) : La;
-      bool any = false;
-      mesh_face(g, f, La, Lb, seg, W.hx, W.hy, HW.hz, r, T, [&](const float tau, const v3 nl, const float pen) {
-        any = true;
-        emit(s, tau, mwall_world_n(W, nl), pen);
-      });
-      if (hit && any) {
-        const uint64_t bb = 1ull << bit;
-        (*hit)[0] |= s == 0 ? bb : 0ull;
-        (*hit)[1] |= s == 1 ? bb : 0ull;
-      }
-    }
-  }
+POB_D void omesh_seg(const float *OT, const bool isA, const OMesh &ms, const int s, v3 &A, v3 &B, float &r, bool &seg) {
+  A = vsel3(s == 0, ms.a[0], ms.a[1]);
+  B = vsel3(s == 0, ms.b[0], ms.b[1]);
+  r = s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1];
+  seg = !(isA && s == 0);
 }
 
 template <int MW, class G>
@@ -223,7 +196,9 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
       }
     }
   }
-  omesh_walk<MW>(g, OT, WT, HW, isA, ms, M, &ms.mc, [&](const int s, const float tau, const v3 n, const float pen) {
+  mesh_wave_walk<ONB>(g, WT, HW.cz, HW.hz, M,
+                      [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
+                      [&](const int s, const int bit, const float tau, const v3 n, const float pen) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
     const q4 q = qsel(s == 0, b.q[0], b.q[1]);
     const v3 pe = vfma(vsel3(s == 0, rv[0], rv[1]), tau, x);
@@ -232,6 +207,8 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
                    x, q, qsel(s == 0, pqs[0], pqs[1]), vsel3(s == 0, pxs[0], pxs[1]), dx, da);
     DX[0] = vsel3(s == 0, dx, DX[0]); DX[1] = vsel3(s == 1, dx, DX[1]);
     DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
+    ms.mc[0] |= s == 0 ? 1ull << bit : 0ull;
+    ms.mc[1] |= s == 1 ? 1ull << bit : 0ull;
   });
 }
 
@@ -250,8 +227,9 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
   if (MW == 0) return;
   uint64_t M[ONB] = {ms.mc[0], ms.mc[1]};
   if (!__any((M[0] | M[1]) != 0ull)) return;
-  omesh_walk<MW>(g, OT, WT, HW, isA, ms, M, (uint64_t(*)[ONB]) nullptr,
-                 [&](const int s, const float tau, const v3 n, const float pen) {
+  mesh_wave_walk<ONB>(g, WT, HW.cz, HW.hz, M,
+                      [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
+                      [&](const int s, const int, const float tau, const v3 n, const float pen) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
     const q4 q = qsel(s == 0, b.q[0], b.q[1]);
     const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), tau, x);

@@ -191,40 +191,13 @@ POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, const uint32
   }
 }
 
-// Walk the lane's face items (body order, then wall / face order: the oracle's contact order
-// per body) one per lane per iteration, evaluating each face once: emit(l, tau, n, pen) for
-// every penetrating triangle.  hit (optional) collects the walls that produced a contact
-// (bit 8 l + w).
-template <class G, class F>
-POB_D void qmesh_walk(G &g, csys_t &S, const float *LT, const float *WT, const QMesh &ms, uint64_t (&M)[QNB],
-                      uint32_t *hit, F &&emit) {
-  const float cz = S.wall_cz, hz = S.wall_hz;
-  while (__any((M[0] | M[1] | M[2]) != 0ull)) {
-    const int l = M[0] != 0ull ? 0 : (M[1] != 0ull ? 1 : 2);
-    const uint64_t ml = l == 0 ? M[0] : (l == 1 ? M[1] : M[2]);
-    const bool on = ml != 0ull;
-    const int bit = on ? __builtin_ctzll(ml) : 0;
-    const uint64_t rest = ml & (ml - 1ull);
-    M[0] = l == 0 ? rest : M[0];
-    M[1] = l == 1 ? rest : M[1];
-    M[2] = l == 2 ? rest : M[2];
-    if (on) {
-      const int w = bit >> 3, f = bit & 7;
-      const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
-      const v3 A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
-      const v3 B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
-      const float r = l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1];
-      const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      const v3 La = mwall_local(W, cz, A);
-      const v3 Lb = l == 0 ? La : mwall_local(W, cz, B);
-      bool any = false;
-      mesh_face(g, f, La, Lb, l != 0, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
-        any = true;
-        emit(l, tau, mwall_world_n(W, nl), pen);
-      });
-      if (hit && any) *hit |= 1u << (8 * l + w);
-    }
-  }
+// the wave walk's view of the lane's bodies (pob_mesh.h mesh_wave_walk): body l's segment,
+// radius and kind (the torso is the sphere at its centre)
+POB_D void qmesh_seg(csys_t &S, const float *LT, const QMesh &ms, const int l, v3 &A, v3 &B, float &r, bool &seg) {
+  A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
+  B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
+  r = l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1];
+  seg = l != 0;
 }
 
 // body l's value among the lane's three (selects: a runtime index into a register array
@@ -269,7 +242,9 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
-  qmesh_walk(g, S, LT, WT, ms, M, &ms.mc, [&](const int l, const float tau, const v3 n, const float pen) {
+  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+                      [&](const int l, const int bit, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
     const q4 q = qpick4(l, b.q);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, q, tau);
@@ -278,6 +253,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
                    L.get3(QL_PX(0) + 7 * l), dx, da);
     qput3(l, DX, dx);
     qput3(l, DA, da);
+    ms.mc |= 1u << (8 * l + (bit >> 3));
   });
 }
 
@@ -307,7 +283,9 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
   POB_FENCE();
   uint64_t M[QNB];
   qmesh_items(S, LT, WT, ms.mc, ms, M);
-  qmesh_walk(g, S, LT, WT, ms, M, (uint32_t *)nullptr, [&](const int l, const float tau, const v3 n, const float pen) {
+  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+                      [&](const int l, const int, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
     v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
@@ -354,7 +332,9 @@ POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const 
     const uint32_t lw = qwall_mask(S, b);
     qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
-  qmesh_walk(g, S, LT, WT, ms, M, (uint32_t *)nullptr, [&](const int l, const float tau, const v3 n, const float pen) {
+  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+                      [&](const int l, const int, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
     const float rl = q_cap_r(S, LT, l), iml = q_inv_mass(S, LT, l);

@@ -265,6 +265,9 @@ def main():
     ap.add_argument("--loop", type=int, default=-1, help="index of the outer loop (default: the largest)")
     ap.add_argument("--iters", type=int, default=5, help="loop iterations per env-step (substeps / 2)")
     ap.add_argument("--ghz", type=float, default=2.4)
+    ap.add_argument("--inner", action="store_true",
+                    help="also analyse each inner loop of the chosen loop (one trip of its body: the wall "
+                         "walks' cost per face item), every block of it counted as executed")
     a = ap.parse_args()
     blocks, order = load_function(a.asm, a.kernel)
     succ = cfg(blocks, order)
@@ -280,6 +283,12 @@ def main():
     print(f"kernel {a.kernel}, loop {h}: {r['instructions']} instructions in {r['blocks']} blocks on the common path "
           f"({r['inner_loops_skipped']} inner loops as zero-trip, {r['call_blocks_skipped']} call blocks skipped)")
     print(f"  by class: {r['by_class']}")
+    if a.inner:
+        for hi, bdi in sorted(((x, y) for x, y in L.items() if x != h and x in bd and y < bd), key=lambda z: order.index(z[0])):
+            ri = analyse(blocks, order, succ, hi, bdi, L)
+            print(f"  inner loop {hi}: {len(bdi)} blocks, {size(bdi)} instructions; one trip: {ri['instructions']} "
+                  f"instructions, issue {ri['issue']:.0f} / chain {ri['chain']:.0f} / inorder {ri['inorder']:.0f} cycles, "
+                  f"{ri['by_class'].get('valu', 0)} VALU")
     us = lambda c: c * a.iters / (a.ghz * 1e3)  # noqa: E731
     for k in ("issue", "chain", "inorder"):
         print(f"  {k:8s} {r[k]:9.0f} cycles / iteration  -> x{a.iters} = {r[k] * a.iters:9.0f} cycles "
