@@ -444,8 +444,8 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
       hit = mface_contact(g, F, c, ro, (ro * ro) * 1.00000095367431640625f, tau, nl, pen);
       if (hit) nw = mwall_world_n(W, nl);
     }
-    // the owners take their two triangles' contacts, in order
-#pragma unroll
+    // the owners take their two triangles' contacts, in order (one copy of apply's code)
+#pragma nounroll
     for (int t = 0; t < 2; ++t) {
       const int src = 16 * (int)rank + 8 * t;
       const int wl = src + mlane_read_i(kmin, src);
