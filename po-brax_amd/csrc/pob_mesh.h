@@ -196,8 +196,11 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     if (c[t].d2 < T) {
-      float dist, inv;
-      g.sqrt_rcp(c[t].d2, dist, inv);
+      // (d2 = 0: the segment touches or pierces the triangle -- common when a leg goes through
+      // a wall -- has distance 0 exactly and uses no reciprocal; kept out of the range guards,
+      // whose rerun (GuardAcc) would double the wave's step)
+      float dist = 0.0f, inv = 0.0f;
+      if (c[t].d2 > 0.0f) g.sqrt_rcp(c[t].d2, dist, inv);
       const float pen = r - dist;
       if (pen > 0.0f) {
         float na, nb, nw;
@@ -296,8 +299,8 @@ template <class G>
 POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, const float T, float &tau, v3 &nl,
                          float &pen) {
   if (!(c.d2 < T)) return false;
-  float dist, inv;
-  g.sqrt_rcp(c.d2, dist, inv);
+  float dist = 0.0f, inv = 0.0f;
+  if (c.d2 > 0.0f) g.sqrt_rcp(c.d2, dist, inv);  // (d2 = 0: mesh_face)
   pen = r - dist;
   if (!(pen > 0.0f)) return false;
   float na, nb, nw;
@@ -378,7 +381,11 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
 template <int NB, class G, class SegOf, class Apply>
 POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
                           Apply &&apply) {
+#ifdef POB_MESH_LANE_WALK
+  if (true) {  // A/B build switch: the per-lane walk everywhere
+#else
   if (__ballot(1) != ~0ull) {
+#endif
     mesh_lane_walk<NB>(g, WT, cz, hz, M, seg_of, apply);
     return;
   }
