@@ -80,7 +80,14 @@ struct HGround {
 struct HMesh {
   v3 a, b;
   uint64_t mc;
+  int nct;  // wall contacts of the position pass (the first HMAXC kept in the lane's LDS store)
 };
+// The position pass's wall contacts (tau, n, pen), kept in the lane's slots of the staging
+// region (idle during the substeps; lane-minor: element e of the lane at CS[64 e]) so that the
+// velocity pass applies them without evaluating their faces again; a lane with more re-walks
+// its contact faces (ms.mc) from the stored segments instead -- the same contacts either way.
+#define HMAXC 5
+#define HCS_FLOATS (5 * HMAXC)
 
 // Contacts of a collide substep on one lane (oracle order: ground, then walls in wall / face /
 // triangle order).  Walls: the broadphase over the walls' grown boxes (registers, HWalls) by
@@ -89,12 +96,13 @@ struct HMesh {
 template <int MW, class G>
 POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
                               const bool torso, const HBody &b, const v3 px, const q4 pq, HGround &gc, HMesh &ms,
-                              v3 &DX, v3 &DA) {
+                              v3 &DX, v3 &DA, float *CS) {
   gc.pe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   gc.pen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - gc.pe.z : -1.0f;
   const float im = HT[HT_IM];
   if (gc.pen > 0.0f) oground_position(g, SC, gc.pen, gc.pe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
   ms.mc = 0ull;
+  ms.nct = 0;
   if (MW == 0) return;
   uint32_t m = 0u;
   {
@@ -132,18 +140,36 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
                     [&](const int, const int bit, const float tau, const v3 n, const float pen) {
     owall_position(g, SC, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
     ms.mc |= 1ull << bit;
+    if (ms.nct < HMAXC) {
+      float *c = CS + 64 * 5 * ms.nct;
+      c[0] = tau; c[64] = n.x; c[128] = n.y; c[192] = n.z; c[256] = pen;
+    }
+    ++ms.nct;
   });
 }
 
 template <int MW, class G>
 POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
-                              const bool torso, const HBody &b, const HGround &gc, const HMesh &ms, v3 &dV, v3 &dW) {
+                              const bool torso, const HBody &b, const HGround &gc, const HMesh &ms, v3 &dV, v3 &dW,
+                              const float *CS) {
   const float im = HT[HT_IM];
   if (gc.pen > 0.0f)
     ocontact_vel_one(g, SC, true, gc.pen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
-  if (MW == 0 || !__any(ms.mc != 0ull)) return;
+  if (MW == 0 || !__any(ms.nct != 0)) return;
   const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
-  uint64_t Ms[1] = {ms.mc};
+  const bool ovf = ms.nct > HMAXC;
+  const int n = ovf ? 0 : ms.nct;
+#pragma unroll 1
+  for (int i = 0; i < HMAXC; ++i) {
+    if (!__any(i < n)) break;
+    if (i < n) {
+      const float *c = CS + 64 * 5 * i;
+      ocontact_vel_pe(g, SC, false, c[256], vfma(rv, c[0], b.x), V(c[64], c[128], c[192]), HT[HT_R], im, b.x, b.v, b.w,
+                      dV, dW);
+    }
+  }
+  if (!__any(ovf)) return;
+  uint64_t Ms[1] = {ovf ? ms.mc : 0ull};
   mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     [&](const int, const int, const float tau, const v3 n, const float pen) {
@@ -153,9 +179,11 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
 
 // One XPBD substep on an env's sixteen lanes (see the header comment for the split).
 // (HSUB_T: pob_octet.h)
+// CS: the lane's wall-contact store (HCS_FLOATS lane-minor slots of LDS, element e at CS[64 e])
 template <int MW, class G>
 POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const HWalls<MW> &HW, HBody &b,
-                        const float act, v3 &cv, v3 &ca, const bool COLLIDE, unsigned long long *tacc = nullptr) {
+                        const float act, v3 &cv, v3 &ca, const bool COLLIDE, float *CS,
+                        unsigned long long *tacc = nullptr) {
 #ifdef POB_EXP_TIMING_SUB
   unsigned long long _tl = __builtin_amdgcn_s_memtime();
 #else
@@ -254,7 +282,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     }
     HSUB_T(1)
     if (COLLIDE) {
-      hcontacts_position<MW>(g, SC, HT, WT, HW, torso, b, px, pq, gc, ms, DX, DA);
+      hcontacts_position<MW>(g, SC, HT, WT, HW, torso, b, px, pq, gc, ms, DX, DA, CS);
       HSUB_T(4)
     }
     b.x = vadd(b.x, DX);
@@ -274,7 +302,7 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
   // 5. velocity-level contacts (ground first, then wall: the oracle's per-body order)
   if (COLLIDE) {
     v3 dV = V(0.0f, 0.0f, 0.0f), dW = dV;
-    hcontacts_velocity<MW>(g, SC, HT, WT, HW, torso, b, gc, ms, dV, dW);
+    hcontacts_velocity<MW>(g, SC, HT, WT, HW, torso, b, gc, ms, dV, dW, CS);
     HSUB_T(7)
     b.v = vadd(b.v, dV); b.w = vadd(b.w, dW);
     cv = vadd(cv, dV);

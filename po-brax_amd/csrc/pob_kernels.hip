@@ -1172,7 +1172,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS + HW_FLOATS];
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
+  __shared__ float ocst[OCS_FLOATS * 64];
   const int lane = (int)threadIdx.x;
+  float *const ocs = ocst + lane;  // the lane's wall-contact store (pob_octet.h)
   const int m = lane & 7;
   const bool isA = m < 4;
   const int k = isA ? m : 7 - m;              // the leg
@@ -1282,15 +1284,15 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
     GuardBranch gb;
-    for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
 #else
 #ifdef POB_EXP_TIMING_SUB  // timing experiment only: phase durations into stamps 5..12
 #define OCT_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
+    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs, pob_ts + 5);
 #else
 // At two waves per SIMD (the branch-guard build, B > 8 x SIMDs) the four-lane kernel's falling
 // issue priority keeps a SIMD's waves together (k_step_quad): HH B = 16 384 -2.2 %, TAG -3 %,
@@ -1304,7 +1306,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       else if (lvl_ == 2) __builtin_amdgcn_s_setprio(1);                                       \
       else __builtin_amdgcn_s_setprio(0);                                                      \
     }                                                                                          \
-    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0);                \
+    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs);                \
   }
 #endif
     if constexpr (!GACC) {
@@ -1496,6 +1498,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 // block; lane r of an env owns one body and one side of one joint (P_hip_r / C_hip_(7-r) /
 // P_knee_(r-8) / C_knee_(15-r)).  Lane 0 (P_hip_0, the torso) runs the per-env POMDP tail.
 #define POB_HSTAGE_FLOATS (OL_FLOATS * 64)
+static_assert(POB_HSTAGE_FLOATS >= HCS_FLOATS * 64, "the sixteen-lane staging region holds the wall-contact store");
 #ifndef POB_HEX_MINW  // experiment: the register budget of this many waves per SIMD
 #define POB_HEX_MINW 1
 #endif
@@ -1511,6 +1514,7 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
+  float *const hcs = stg + lane;  // the lane's wall-contact store during the substeps (pob_hexa.h)
   const int r = lane & 15;
   const bool hip = r < 8, isP = r < 4 || (r >= 8 && r < 12);
   const int k = r < 4 ? r : (r < 8 ? 7 - r : (r < 12 ? r - 8 : 15 - r));  // the leg
@@ -1605,25 +1609,25 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
-    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false, hcs);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
     GuardBranch gb;
-    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) hpbd_substep<hex_max_walls(KIND)>(gb, S, HT, WT, HW, bd, a, cvl, cal, false, hcs);  // timing experiment only
 #else
 #ifdef POB_HEX_UNROLL2
 #define HEX_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < iters; ++it) {                                   \
-    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, false);                  \
-    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, true);                   \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, false, hcs);                  \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, true, hcs);                   \
   }
 #elif defined(POB_EXP_TIMING_SUB)  // timing experiment only: phase durations into stamps 5..12
 #define HEX_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, pob_ts + 5);
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, hcs, pob_ts + 5);
 #else
 #define HEX_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0);
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, hcs);
 #endif
     if constexpr (!GACC) {
       GuardBranch gb;

@@ -47,6 +47,7 @@ struct OBody {
 #define OT_THI 38
 #define OT_FLOATS POB_OCT_FLOATS
 #define OT_TAB_FLOATS (8 * OT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
+static_assert(OT_TAB_FLOATS % 4 == 0, "the broadphase boxes after the wall rows are read as float4");
 
 #define OTV(T, f) V((T)[(f)], (T)[(f) + 1], (T)[(f) + 2])
 // The eight-lane kernel runs at most a few waves per SIMD, so the system table's scalars
@@ -74,7 +75,16 @@ struct OGround {
 struct OMesh {
   v3 a[ONB], b[ONB];
   uint64_t mc[ONB];
+  int nct;  // wall contacts of the position pass (the first OMAXC kept in the lane's LDS store)
 };
+// The position pass's wall contacts (slot, tau, n, pen), kept in the lane's LDS store
+// (lane-minor: element e at CS[64 e]) so that the velocity pass applies them without evaluating
+// their faces again; a lane with more re-walks its contact faces (ms.mc) from its segments,
+// which it then leaves in the store too (elements OCS_SEG.., off the registers of the velocity
+// projection) -- the same contacts either way.
+#define OMAXC 4
+#define OCS_SEG (6 * OMAXC)
+#define OCS_FLOATS (OCS_SEG + 6 * ONB)
 
 // slot s's capsule end points x +- rotate(e0, q) (torso: e0 = 0, both = x)
 POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
@@ -139,7 +149,7 @@ POB_D void omesh_seg(const float *OT, const bool isA, const OMesh &ms, const int
 template <int MW, class G>
 POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
                               const bool isA, const OBody &b, const v3 (&pxs)[ONB], const q4 (&pqs)[ONB],
-                              OGround &gc, OMesh &ms, v3 (&DX)[ONB], v3 (&DA)[ONB]) {
+                              OGround &gc, OMesh &ms, v3 (&DX)[ONB], v3 (&DA)[ONB], float *CS) {
   const bool gslot1 = !isA;
   {
     const v3 xg = vsel3(gslot1, b.x[1], b.x[0]);
@@ -154,6 +164,7 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
       oground_position(g, SC, gc.pen, gc.pe, OT[OT_G + 3], OT[OT_B(s)], b.x[s], b.q[s], pqs[s], pxs[s], DX[s], DA[s]);
   }
   ms.mc[0] = 0ull; ms.mc[1] = 0ull;
+  ms.nct = 0;
   if (MW == 0) return;
   v3 rv[ONB];
 #pragma unroll
@@ -171,9 +182,13 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
 #else
     const int nw = HW.n_walls;
 #endif
+    // the boxes from the LDS table (HW_BOX, after the wall rows) at each collide substep: held
+    // in VGPRs across the loop they pushed the two-wave build past 256 registers
+    const float *WB = WT + POB_MAXW * POB_WALL_FLOATS + HW_BOX;
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
-      const bool near = (mnx <= HW.hx[w]) & (mxx >= HW.lx[w]) & (mny <= HW.hy[w]) & (mxy >= HW.ly[w]);
+      const float4 bx = *reinterpret_cast<const float4 *>(WB + 4 * w);
+      const bool near = (mnx <= bx.z) & (mxx >= bx.x) & (mny <= bx.w) & (mxy >= bx.y);
       lane_mask |= (near & (w < nw)) ? 1u << w : 0u;
     }
   }
@@ -209,13 +224,25 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
     DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
     ms.mc[0] |= s == 0 ? 1ull << bit : 0ull;
     ms.mc[1] |= s == 1 ? 1ull << bit : 0ull;
+    if (ms.nct < OMAXC) {
+      float *c = CS + 64 * 6 * ms.nct;
+      c[0] = (float)s; c[64] = tau; c[128] = n.x; c[192] = n.y; c[256] = n.z; c[320] = pen;
+    }
+    ++ms.nct;
   });
+  if (ms.nct > OMAXC) {
+#pragma unroll
+    for (int q = 0; q < ONB; ++q) {
+      float *c = CS + 64 * (OCS_SEG + 6 * q);
+      c[0] = ms.a[q].x; c[64] = ms.a[q].y; c[128] = ms.a[q].z; c[192] = ms.b[q].x; c[256] = ms.b[q].y; c[320] = ms.b[q].z;
+    }
+  }
 }
 
 template <int MW, class G>
 POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
                               const bool isA, const OBody &b, const OGround &gc, const OMesh &ms, v3 (&dV)[ONB],
-                              v3 (&dW)[ONB]) {
+                              v3 (&dW)[ONB], const float *CS) {
   const bool gslot1 = !isA;
 #pragma unroll
   for (int s = 0; s < ONB; ++s) {
@@ -224,11 +251,36 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
       ocontact_vel_one(g, SC, true, gc.pen, OTV(OT, OT_G), V(0.0f, 0.0f, 1.0f), OT[OT_G + 3], OT[OT_B(s)], b.x[s],
                        b.q[s], b.v[s], b.w[s], dV[s], dW[s]);
   }
-  if (MW == 0) return;
-  uint64_t M[ONB] = {ms.mc[0], ms.mc[1]};
-  if (!__any((M[0] | M[1]) != 0ull)) return;
+  if (MW == 0 || !__any(ms.nct != 0)) return;
+  const bool ovf = ms.nct > OMAXC;
+  const int nc = ovf ? 0 : ms.nct;
+#pragma unroll 1
+  for (int i = 0; i < OMAXC; ++i) {
+    if (!__any(i < nc)) break;
+    if (i < nc) {
+      const float *c = CS + 64 * 6 * i;
+      const int s = (int)c[0];
+      const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
+      const q4 q = qsel(s == 0, b.q[0], b.q[1]);
+      const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), c[64], x);
+      v3 dv = vsel3(s == 0, dV[0], dV[1]), dw = vsel3(s == 0, dW[0], dW[1]);
+      ocontact_vel_pe(g, SC, false, c[320], pe, V(c[128], c[192], c[256]), s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1],
+                      s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]),
+                      vsel3(s == 0, b.w[0], b.w[1]), dv, dw);
+      dV[0] = vsel3(s == 0, dv, dV[0]); dV[1] = vsel3(s == 1, dv, dV[1]);
+      dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
+    }
+  }
+  if (!__any(ovf)) return;
+  uint64_t M[ONB] = {ovf ? ms.mc[0] : 0ull, ovf ? ms.mc[1] : 0ull};
   mesh_wave_walk<ONB>(g, WT, HW.cz, HW.hz, M,
-                      [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
+                      [&](const int s, v3 &A, v3 &B, float &r, bool &seg) {
+                        const float *c = CS + 64 * (OCS_SEG + 6 * s);
+                        A = V(c[0], c[64], c[128]);
+                        B = V(c[192], c[256], c[320]);
+                        r = s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1];
+                        seg = !(isA && s == 0);
+                      },
                       [&](const int s, const int, const float tau, const v3 n, const float pen) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
     const q4 q = qsel(s == 0, b.q[0], b.q[1]);
@@ -297,7 +349,7 @@ POB_D void ojoint_position(G &g, csys_t &S, const float s_pos, const float *OT, 
 // loop's table scalars in registers.
 template <int MW, class G>
 POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, OBody &b,
-                        const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE,
+                        const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE, float *CS,
                         unsigned long long *tacc = nullptr) {
 #ifdef POB_EXP_TIMING_SUB
   unsigned long long _tl = __builtin_amdgcn_s_memtime();
@@ -387,7 +439,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     }
     HSUB_T(1)
     if (COLLIDE) {
-      ocontacts_position<MW>(g, SC, OT, WT, HW, isA, b, px, pq, gc, ms, DX, DA);
+      ocontacts_position<MW>(g, SC, OT, WT, HW, isA, b, px, pq, gc, ms, DX, DA, CS);
       HSUB_T(4)
     }
 #pragma unroll
@@ -414,7 +466,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     v3 dV[ONB], dW[ONB];
 #pragma unroll
     for (int s = 0; s < ONB; ++s) { dV[s] = V(0.0f, 0.0f, 0.0f); dW[s] = V(0.0f, 0.0f, 0.0f); }
-    ocontacts_velocity<MW>(g, SC, OT, WT, HW, isA, b, gc, ms, dV, dW);
+    ocontacts_velocity<MW>(g, SC, OT, WT, HW, isA, b, gc, ms, dV, dW, CS);
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);
