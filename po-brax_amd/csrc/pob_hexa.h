@@ -134,6 +134,9 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
     const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, R);
     M |= on ? (uint64_t)fm << (8 * w) : 0ull;
   }
+#ifdef POB_EXP_NO_WALK
+  return;  // timing experiment only: broadphase and face cull, no face walk
+#endif
   uint64_t Ms[1] = {M};
   mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },

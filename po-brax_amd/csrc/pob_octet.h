@@ -211,6 +211,9 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
       }
     }
   }
+#ifdef POB_EXP_NO_WALK
+  return;  // timing experiment only: broadphase and face cull, no face walk
+#endif
   mesh_wave_walk<ONB>(g, WT, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
                       [&](const int s, const int bit, const float tau, const v3 n, const float pen) {

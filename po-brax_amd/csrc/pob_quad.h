@@ -114,7 +114,7 @@ struct QGround {
 // contact in registers.
 struct QMesh {
   v3 a[QNB], b[QNB];
-  uint32_t mc;
+  uint64_t mc[QNB];  // per body: the faces that produced a contact (bit 8 w + f)
 };
 
 // The Ant's capsules (checked by pob_system.cpp) have opposite end points +-e0 in the body
@@ -191,8 +191,12 @@ POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, const uint32
   }
 }
 
-// the wave walk's view of the lane's bodies (pob_mesh.h mesh_wave_walk): body l's segment,
-// radius and kind (the torso is the sphere at its centre)
+// the walk's view of the lane's bodies: body l's segment, radius and kind (the torso is the
+// sphere at its centre).  The four-lane kernel walks per lane (pob_mesh.h mesh_lane_walk): at
+// four waves per SIMD the wave-cooperative walk measured slower (HH B = 65 536 0.1369 ->
+// 0.1598 ms, TAG 0.1238 -> 0.1415; profiles/r4h/ab1.txt) -- the SIMD is issue-bound, so the
+// cooperative round's idle-lane work and cross-lane traffic are not free, and its registers
+// pushed the 128-VGPR budget's spills from 160 to 224 B.
 POB_D void qmesh_seg(csys_t &S, const float *LT, const QMesh &ms, const int l, v3 &A, v3 &B, float &r, bool &seg) {
   A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
   B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
@@ -230,7 +234,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
                          L.get4(QL_PQ(l)), L.get3(QL_PX(l)), DX[l], DA[l]);
     }
   }
-  ms.mc = 0u;
+  ms.mc[0] = 0ull; ms.mc[1] = 0ull; ms.mc[2] = 0ull;
   if (!WALLS) return;
   POB_FENCE();
   qmesh_segments(S, LT, b, rv_leg, ms);
@@ -242,7 +246,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
-  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
                       [&](const int l, const int bit, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
@@ -253,7 +257,9 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
                    L.get3(QL_PX(0) + 7 * l), dx, da);
     qput3(l, DX, dx);
     qput3(l, DA, da);
-    ms.mc |= 1u << (8 * l + (bit >> 3));
+    ms.mc[0] |= l == 0 ? 1ull << bit : 0ull;
+    ms.mc[1] |= l == 1 ? 1ull << bit : 0ull;
+    ms.mc[2] |= l == 2 ? 1ull << bit : 0ull;
   });
 }
 
@@ -276,14 +282,14 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
                       b.v[l], b.w[l], dV[l], dW[l]);
     }
   }
-  if (!WALLS || !__any(ms.mc != 0u)) return;
+  if (!WALLS || !__any((ms.mc[0] | ms.mc[1] | ms.mc[2]) != 0ull)) return;
 #ifdef POB_EXP_NO_VWALK
   return;  // timing experiment only: no velocity-pass re-walk
 #endif
   POB_FENCE();
   uint64_t M[QNB];
-  qmesh_items(S, LT, WT, ms.mc, ms, M);
-  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  M[0] = ms.mc[0]; M[1] = ms.mc[1]; M[2] = ms.mc[2];
+  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
                       [&](const int l, const int, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
@@ -332,7 +338,7 @@ POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const 
     const uint32_t lw = qwall_mask(S, b);
     qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
-  mesh_wave_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
                       [&](const int l, const int, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
