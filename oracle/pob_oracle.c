@@ -912,9 +912,9 @@ static long long pair_flops_executed(const orc_env *e, int w, v3 p, float r) {
 
 #ifdef ORC_COUNT_FLOPS
 /* Statistics hook (FLOP build, mode 1, single-threaded; no effect on results): per env and
- * collide substep, the face items each four-lane kernel lane walks -- the faces the face cull
- * keeps of its three bodies (torso, Aux k+1, leg k) over the walls of its broadphase mask --
- * into buf[(env * nsub + substep) * 4 + k] (scripts/wall_walk_stats.py) */
+ * collide substep, the face items of each body -- the faces the face cull keeps over the walls
+ * of the four-lane kernel's broadphase mask of a lane holding the body (the torso: of lane 0) --
+ * into buf[(env * nsub + substep) * 9 + body] (scripts/wall_walk_stats.py) */
 static int *g_items_buf = NULL;
 static int g_items_nsub = 0, g_items_env = 0, g_items_sub = 0;
 void orc_items_record(int *buf, int nsub) { g_items_buf = buf; g_items_nsub = nsub; }
@@ -965,13 +965,12 @@ static void detect(const orc_env *e, const body_t *b, contacts_t *ct) {
       sa[i] = cpoint(e->cap_end[i][0], b->q[i], b->x[i]);
       sb[i] = cpoint(e->cap_end[i][e->cap_nend[i] - 1], b->q[i], b->x[i]);
     }
-    for (int k = 0; k < 4; ++k) {
-      const int l[3] = {0, 2 * k + 1, 2 * k + 2};
+    for (int i = 0; i < NDYN; ++i) {
+      const uint32_t lm = lane_mask[i == 0 ? 0 : (i - 1) / 2];
       int n = 0;
       for (int w = 0; w < e->n_walls; ++w)
-        if ((lane_mask[k] >> w) & 1u)
-          for (int t = 0; t < 3; ++t) n += face_items(e, l[t], w, sa[l[t]], sb[l[t]]);
-      g_items_buf[((size_t)g_items_env * g_items_nsub + g_items_sub) * 4 + k] = n;
+        if ((lm >> w) & 1u) n += face_items(e, i, w, sa[i], sb[i]);
+      g_items_buf[((size_t)g_items_env * g_items_nsub + g_items_sub) * NDYN + i] = n;
     }
     ++g_items_sub;
   }

@@ -72,6 +72,35 @@ POB_D bool mtri_inside(const bool t1, const float ha, const float hb, const floa
   return t1 ? ((pb <= hb) & (pa >= -ha) & (cr <= 0.0f)) : ((pb >= -hb) & (pa <= ha) & (cr >= 0.0f));
 }
 
+// mtri_closest for both triangles of the face at once (mesh_face): the inside tests share the
+// diagonal's cross term, the edge points their clamps and the diagonal's closest point -- the
+// same operations on the same operands as two mtri_closest calls, each computed once
+POB_D void mtri_closest2(const float ha, const float hb, const float ha2, const float hb2, const float inv_dd,
+                         const float pa, const float pb, float &qa0, float &qb0, float &qa1, float &qb1) {
+  const float cr = FMA(pa + ha, hb, -((pb + hb) * ha));
+  const bool in0 = (pb >= -hb) & (pa <= ha) & (cr >= 0.0f);
+  const bool in1 = (pb <= hb) & (pa >= -ha) & (cr <= 0.0f);
+  const float s = clamp01(FMA(pb + hb, hb2, (pa + ha) * ha2) * inv_dd);
+  const float s2 = 2.0f * s;
+  const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
+  const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
+  // squared distances to the edge points: bottom (ca, -hb), right (ha, cb), diagonal (da, db),
+  // top (ca, hb), left (-ha, cb)
+  const float gc = pa - ca, gd = pa - da, gr = pa - ha, gl = pa - -ha;
+  const float hbt = pb - -hb, hd = pb - db, hcb = pb - cb, htp = pb - hb;
+  const float dbot = FMA(hbt, hbt, gc * gc), drt = FMA(hcb, hcb, gr * gr), ddg = FMA(hd, hd, gd * gd);
+  const float dtop = FMA(htp, htp, gc * gc), dlf = FMA(hcb, hcb, gl * gl);
+  // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (first strict minimum)
+  float b0 = dbot, a0 = ca, c0 = -hb;
+  if (drt < b0) { b0 = drt; a0 = ha; c0 = cb; }
+  if (ddg < b0) { a0 = da; c0 = db; }
+  float b1 = ddg, a1 = da, c1 = db;
+  if (dtop < b1) { b1 = dtop; a1 = ca; c1 = hb; }
+  if (dlf < b1) { a1 = -ha; c1 = cb; }
+  qa0 = in0 ? pa : a0; qb0 = in0 ? pb : c0;
+  qa1 = in1 ? pa : a1; qb1 = in1 ? pb : c1;
+}
+
 // running closest candidate: squared distance, segment parameter, S - P (face coordinates)
 struct MCand {
   float d2, u, da, db, dw;
@@ -150,20 +179,20 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
   const float e_d = FMA(hb2, hb2, ha2 * ha2), i_d = g.rcp(e_d);
   MCand c[2];
   // end point A (and B) against each triangle
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    float qa, qb;
-    mtri_closest(t == 1, ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa, qb);
-    c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f;
-    mcand_take(c[t], 0.0f, S.aa_ - qa, S.ab - qb, S.aw - w0);
-  }
-  if (seg) {
+  {
+    float qa[2], qb[2];
+    mtri_closest2(ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa[0], qb[0], qa[1], qb[1]);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      float qa, qb;
-      mtri_closest(t == 1, ha, hb, ha2, hb2, i_d, Ba, Bb, qa, qb);
-      mcand_take(c[t], 1.0f, Ba - qa, Bb - qb, Bw - w0);
+      c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f;
+      mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0);
     }
+  }
+  if (seg) {
+    float qa[2], qb[2];
+    mtri_closest2(ha, hb, ha2, hb2, i_d, Ba, Bb, qa[0], qb[0], qa[1], qb[1]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0);
     S.Da = Ba - S.aa_; S.Db = Bb - S.ab; S.Dw = Bw - S.aw;
     S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
     S.inv_aa = g.rcp(S.aa);

@@ -246,6 +246,9 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
+#ifdef POB_EXP_WALK_DEAD
+  if (S.n_walls < 64) return;  // timing experiment only: the walk compiled in, never run
+#endif
   mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
                       [&](const int l, const int bit, const float tau, const v3 n, const float pen) {

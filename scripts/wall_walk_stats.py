@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Face items the four-lane kernel's wall walk evaluates (oracle statistics hook, FLOP build):
-per collide substep each lane walks the faces the face cull keeps of its three bodies over the
-walls of its broadphase mask, one face per iteration, so a wave (16 envs x 4 lanes) runs as
-many walk iterations as its busiest lane.  Prints, over a random-action rollout with
-autoresets, the distribution of items per lane, the wave maximum (iterations of the per-lane
-walk) and the wave total / 64 (iterations of a walk whose items were spread over the wave).
+"""Face items the kernels' wall walks evaluate (oracle statistics hook, FLOP build): per collide
+substep each body has the faces the face cull keeps over the walls of its lane's broadphase
+mask.  A lane walks the items of the bodies it holds -- four-lane kernel: torso, Aux k+1, leg
+k; eight-lane: A_k torso + Aux, B_k Aux + leg; sixteen-lane: one body, the torso on four lanes
+and each Aux on two -- so the per-lane walk runs as many iterations as a wave's busiest lane
+and the cooperative walk (pob_mesh.h mesh_wave_walk, four items a round) about total / 4.
+Prints, over a random-action rollout with autoresets, per layout: items per lane, the wave's
+busiest lane, the wave total and the rounds of the cooperative walk (also their maximum over a
+step, summed over its collide substeps: what a wave pays).
 
     python scripts/wall_walk_stats.py [env] [B] [steps]
 """
@@ -27,27 +30,35 @@ L = e._L
 L.orc_items_record.argtypes = [C.POINTER(C.c_int), C.c_int]
 s = e.reset(P.split(P.prngkey(0), B + 1)[1:], first=True)
 rng = np.random.default_rng(0)
-buf = np.zeros((B, NSUB, 4), np.int32)
+buf = np.zeros((B, NSUB, 9), np.int32)
 L.orc_items_record(buf.ctypes.data_as(C.POINTER(C.c_int)), NSUB)
 L.orc_flops_set_mode(orc.FLOPS_EXECUTED)
-lane, wmax, wtot = [], [], []
+LAYOUTS = {  # lanes per env: the bodies each lane walks
+    "four-lane": [[0, 1, 2], [0, 3, 4], [0, 5, 6], [0, 7, 8]],
+    "eight-lane": [[0, 1], [0, 3], [0, 5], [0, 7], [1, 2], [3, 4], [5, 6], [7, 8]],
+    "sixteen-lane": [[0], [0], [0], [0], [1], [3], [5], [7], [1], [3], [5], [7], [2], [4], [6], [8]],
+}
+rec = []
 try:
     for t in range(steps):
         buf[:] = 0
         s = e.step(s, rng.uniform(-1, 1, (B, 8)).astype(np.float32), flags=orc.F_EPISODE | orc.F_AUTORESET,
                    nthreads=1, inplace=True)
-        lane.append(buf.copy().ravel())
-        w = buf.reshape(B // 16, 16, NSUB, 4).transpose(0, 2, 1, 3).reshape(B // 16, NSUB, 64)
-        wmax.append(w.max(-1).ravel())
-        wtot.append(w.sum(-1).ravel())
+        rec.append(buf.copy())
 finally:
     L.orc_items_record(None, 0)
     L.orc_flops_set_mode(orc.FLOPS_REF_PAIRS)
-lane, wmax, wtot = np.concatenate(lane), np.concatenate(wmax), np.concatenate(wtot)
-print(f"{name} B={B} steps={steps}: lanes x collide substeps = {lane.size}")
-print("items per lane: mean %.3f, P(>0) %.3f, histogram %s" % (lane.mean(), (lane > 0).mean(),
-      np.bincount(np.minimum(lane, 12), minlength=13).tolist()))
-print("per wave-substep: busiest lane's items (per-lane walk iterations) mean %.2f p50 %d p90 %d max %d" % (
-      wmax.mean(), np.median(wmax), np.percentile(wmax, 90), wmax.max()))
-print("                  total items mean %.1f p90 %d max %d; spread over 64 lanes: ceil(total/64) mean %.2f" % (
-      wtot.mean(), np.percentile(wtot, 90), wtot.max(), np.ceil(wtot / 64).mean()))
+rec = np.stack(rec)  # (steps, B, NSUB, 9)
+print(f"{name} B={B} steps={steps}")
+for lay, lanes in LAYOUTS.items():
+    per_lane = np.stack([rec[..., l].sum(-1) for l in lanes], -1)  # (steps, B, NSUB, lanes/env)
+    epw = 64 // len(lanes)
+    W = per_lane.reshape(steps, B // epw, epw, NSUB, len(lanes)).transpose(0, 1, 3, 2, 4).reshape(steps, B // epw, NSUB, 64)
+    wmax, wtot = W.max(-1), W.sum(-1)
+    rounds = np.maximum(np.ceil(wtot / 4), wmax * 0)  # cooperative: four items a round
+    per_step_lane = wmax.sum(-1)  # per-lane walk iterations per step per wave
+    per_step_coop = rounds.sum(-1)
+    print(f"  {lay:13s} items/lane {per_lane.mean():.3f}; per wave-substep busiest lane {wmax.mean():.2f} "
+          f"(max {wmax.max()}), total {wtot.mean():.2f} (p99 {np.percentile(wtot, 99):.0f}, max {wtot.max()}), "
+          f"coop rounds {rounds.mean():.2f}; per step and wave: lane-walk iterations mean {per_step_lane.mean():.1f} "
+          f"max {per_step_lane.max()}, coop rounds mean {per_step_coop.mean():.1f} max {per_step_coop.max()}")
