@@ -352,8 +352,8 @@ POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, co
 // A face costs ~1 000 instructions evaluated on one lane (its twelve candidates and two
 // emissions one after another) and few lanes of a wave hold one at a time (0.7 items on the
 // busiest lane per wave and collide substep on HH rollouts, scripts/wall_walk_stats.py), so
-// the wave shares them out: each round takes the next item of up to four lanes and gives
-// each of those faces sixteen lanes -- lane 8 t + kk of the group computes candidate kk of
+// the wave shares them out: each round takes the next items of up to four lanes (a lane's
+// next two of one body when fewer lanes have one) and gives each of those faces sixteen lanes -- lane 8 t + kk of the group computes candidate kk of
 // triangle t -- reduces the candidates to each triangle's winner (DPP, lexicographic (d2, kk)
 // minimum over the eight lanes), lets the winner lane compute the contact, and hands it to
 // the owner (ds_bpermute), which applies its triangles in order.  Needs all 64 lanes active
@@ -421,6 +421,7 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
   const int lane = (int)__lane_id();
   const int grp = lane >> 4, tri = (lane >> 3) & 1, kk = lane & 7;
   while (true) {
+    // the lane's next item (slot s, face bit b1) and the one after it in the same slot (b2)
     bool has = false;
     int s = 0;
     uint64_t ml = 0ull;
@@ -431,35 +432,48 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
       ml = h ? M[q] : ml;
       has = has | h;
     }
-    const uint64_t req = __ballot(has);
-    if (req == 0ull) break;
-    // the round's owners: the first four lanes with an item (wave-uniform)
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(req >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req, 0u));
-    const bool own = has && rank < 4u;
-    const int bit = has ? __builtin_ctzll(ml) : 0;
+    const uint64_t req1 = __ballot(has);
+    if (req1 == 0ull) break;
+    const uint64_t rest = ml & (ml - 1ull);
+    const bool has2 = has && rest != 0ull;
+    const uint64_t req2 = __ballot(has2);
+    const int b1 = has ? __builtin_ctzll(ml) : 0, b2 = has2 ? __builtin_ctzll(rest) : 0;
+    // a round's four groups: the first items of the first four lanes with one, then (when
+    // fewer) the second items of lanes with two -- each lane's items in its order
+    const int n1 = __builtin_popcountll(req1), n2 = __builtin_popcountll(req2);
+    const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(req1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req1, 0u));
+    const uint32_t r2 = (uint32_t)n1 +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(req2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req2, 0u));
+    const bool own1 = has && r1 < 4u, own2 = has2 && r2 < 4u;  // (own2 implies own1: n1 < 4)
+    const uint64_t pop = (own1 ? 1ull << b1 : 0ull) | (own2 ? 1ull << b2 : 0ull);
 #pragma unroll
-    for (int q = 0; q < NB; ++q) M[q] = (own && s == q) ? (M[q] & (M[q] - 1ull)) : M[q];
-    uint64_t m = req;
-    const int o0 = __builtin_ctzll(m);
-    m &= m - 1ull;
-    const int o1 = m != 0ull ? __builtin_ctzll(m) : 0;
-    m &= m - 1ull;
-    const int o2 = m != 0ull ? __builtin_ctzll(m) : 0;
-    m &= m - 1ull;
-    const int o3 = m != 0ull ? __builtin_ctzll(m) : 0;
-    const int nown = __builtin_popcountll(req);
-    // this lane's group: the owner's item, fetched from the owner
+    for (int q = 0; q < NB; ++q) M[q] = s == q ? (M[q] & ~pop) : M[q];
+    // group owners (wave-uniform): lane and item of each of the four groups
+    int og[4];
+    {
+      uint64_t m1 = req1, m2 = req2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool first = q < n1;
+        const uint64_t m = first ? m1 : m2;
+        og[q] = m != 0ull ? __builtin_ctzll(m) : 0;
+        m1 = first ? (m1 & (m1 - 1ull)) : m1;
+        m2 = first ? m2 : (m2 & (m2 - 1ull));
+      }
+    }
+    const int ol = grp == 0 ? og[0] : (grp == 1 ? og[1] : (grp == 2 ? og[2] : og[3]));
+    const bool gv = grp < n1 + n2;
+    const bool second = grp >= n1;
     v3 A, B;
     float r;
     bool seg;
     seg_of(s, A, B, r, seg);
-    const int meta = bit | (seg ? 64 : 0);
-    const int ol = grp == 0 ? o0 : (grp == 1 ? o1 : (grp == 2 ? o2 : o3));
-    const bool gv = grp < nown;
+    const int meta1 = b1 | (seg ? 64 : 0), meta2 = b2 | (seg ? 64 : 0);
     const v3 Ao = V(mlane_read(A.x, ol), mlane_read(A.y, ol), mlane_read(A.z, ol));
     const v3 Bo = V(mlane_read(B.x, ol), mlane_read(B.y, ol), mlane_read(B.z, ol));
     const float ro = mlane_read(r, ol);
-    const int mo = mlane_read_i(meta, ol);
+    const int ma = mlane_read_i(meta1, ol), mb = mlane_read_i(meta2, ol);
+    const int mo = second ? mb : ma;
     const bool sego = (mo & 64) != 0;
     const MWall W = mwall_row(WT + POB_WALL_FLOATS * ((mo >> 3) & 7));
     const v3 La = mwall_local(W, cz, Ao);
@@ -480,15 +494,19 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
       hit = mface_contact(g, F, c, ro, (ro * ro) * 1.00000095367431640625f, tau, nl, pen);
       if (hit) nw = mwall_world_n(W, nl);
     }
-    // the owners take their two triangles' contacts, in order (one copy of apply's code)
+    // the owners take their items' triangles in order: the winners' lanes first (all four
+    // fetches in flight), then each contact
+    const int g1 = 16 * (int)r1, g2 = 16 * (int)r2;
+    const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 8 + mlane_read_i(kmin, g1 + 8);
+    const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 8 + mlane_read_i(kmin, g2 + 8);
+    const int nt = __any(own2) ? 4 : 2;
 #pragma nounroll
-    for (int t = 0; t < 2; ++t) {
-      const int src = 16 * (int)rank + 8 * t;
-      const int wl = src + mlane_read_i(kmin, src);
+    for (int t = 0; t < nt; ++t) {
+      const int wl = t == 0 ? w10 : (t == 1 ? w11 : (t == 2 ? w20 : w21));
       const int h = mlane_read_i(hit ? 1 : 0, wl);
       const float tw = mlane_read(tau, wl), pw = mlane_read(pen, wl);
       const v3 nn = V(mlane_read(nw.x, wl), mlane_read(nw.y, wl), mlane_read(nw.z, wl));
-      if (own && h != 0) apply(s, bit, tw, nn, pw);
+      if ((t < 2 ? own1 : own2) && h != 0) apply(s, t < 2 ? b1 : b2, tw, nn, pw);
     }
   }
 }
