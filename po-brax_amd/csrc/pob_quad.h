@@ -153,25 +153,6 @@ POB_D uint32_t qwall_mask(csys_t &S, const QBody &b) {
   return m;
 }
 
-// the per-body broadphase (pob_sys wall_blo / wall_bhi): bit 8 l + w when body l's segment's xy
-// AABB meets wall w's box grown by the largest radius + 2e-3 (walls of the lane's broadphase
-// mask lw only, w < n_walls)
-POB_D uint32_t qbody_walls(csys_t &S, const QMesh &ms, const uint32_t lw) {
-  uint32_t wm = 0u;
-#pragma unroll
-  for (int l = 0; l < QNB; ++l) {
-    const float mnx = fminf(ms.a[l].x, ms.b[l].x), mxx = fmaxf(ms.a[l].x, ms.b[l].x);
-    const float mny = fminf(ms.a[l].y, ms.b[l].y), mxy = fmaxf(ms.a[l].y, ms.b[l].y);
-#pragma unroll
-    for (int w = 0; w < POB_MAXW; ++w) {
-      const bool near = (mnx <= S.wall_bhi[w][0]) & (mxx >= S.wall_blo[w][0]) & (mny <= S.wall_bhi[w][1]) &
-                        (mxy >= S.wall_blo[w][1]) & (((lw >> w) & 1u) != 0u);
-      wm |= near ? 1u << (8 * l + w) : 0u;
-    }
-  }
-  return wm;
-}
-
 // the lane's bodies' capsule segments (a, b) (torso: a = b = x)
 POB_D void qmesh_segments(csys_t &S, const float *LT, const QBody &b, const v3 rv_leg, QMesh &ms) {
   const v3 rv1 = qrot_xy(qcap_end(S, LT, 1, 0), b.q[1]);
@@ -186,28 +167,27 @@ POB_D v3 qseg_point(const float *LT, const int l, const v3 x, const q4 q, const 
 }
 
 // face items of the lane's bodies: M[l] bit 8 w + f for every face f of a wall w that the
-// face cull keeps for body l, over the (body, wall) pairs of wm (bit 8 l + w), one pair per lane
-// per iteration (the per-body broadphase leaves few)
-POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, uint32_t wm, const QMesh &ms,
+// face cull keeps for body l, over the walls of wm (bit 8 l + w: body l's walls; walls walked
+// per lane in increasing order)
+POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, const uint32_t wm, const QMesh &ms,
                        uint64_t (&M)[QNB]) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) M[l] = 0ull;
   const float cz = S.wall_cz, hz = S.wall_hz;
-  while (__any(wm != 0u)) {
-    const bool on = wm != 0u;
-    const int bit = on ? __builtin_ctz(wm) : 0;
-    wm &= wm - 1u;
-    const int l = bit >> 3, w = bit & 7;
+  uint32_t m = (wm | (wm >> 8) | (wm >> 16)) & 0xFFu;
+  while (__any(m != 0u)) {
+    const bool on = m != 0u;
+    const int w = on ? __builtin_ctz(m) : 0;
+    m &= m - 1u;
     const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
-    const float R = (l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1]) + POB_MESH_MARGIN;
-    const v3 A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
-    const v3 B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
-    const v3 La = mwall_local(W, cz, A);
-    const v3 Lb = l == 0 ? La : mwall_local(W, cz, B);
-    const uint64_t fm = on ? (uint64_t)mesh_face_mask(La, Lb, W.hx, W.hy, hz, R) << (8 * w) : 0ull;
-    M[0] |= l == 0 ? fm : 0ull;
-    M[1] |= l == 1 ? fm : 0ull;
-    M[2] |= l == 2 ? fm : 0ull;
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      const float R = (l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1]) + POB_MESH_MARGIN;
+      const v3 La = mwall_local(W, cz, ms.a[l]);
+      const v3 Lb = l == 0 ? La : mwall_local(W, cz, ms.b[l]);
+      const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, R);
+      M[l] |= (on && ((wm >> (8 * l + w)) & 1u)) ? (uint64_t)fm << (8 * w) : 0ull;
+    }
   }
 }
 
@@ -261,7 +241,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
   uint64_t M[QNB];
   {
     const uint32_t lw = qwall_mask(S, b);
-    qmesh_items(S, LT, WT, __any(lw != 0u) ? qbody_walls(S, ms, lw) : 0u, ms, M);
+    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
@@ -359,7 +339,7 @@ POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const 
   uint64_t M[QNB];
   {
     const uint32_t lw = qwall_mask(S, b);
-    qmesh_items(S, LT, WT, __any(lw != 0u) ? qbody_walls(S, ms, lw) : 0u, ms, M);
+    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
   mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
