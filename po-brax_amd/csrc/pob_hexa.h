@@ -43,7 +43,6 @@
 #define HT_ISHIP 34    // 1.0 for a hip joint
 #define HT_FLOATS POB_HEX_FLOATS
 #define HT_TAB_FLOATS (16 * HT_FLOATS + POB_MAXW * POB_WALL_FLOATS)  // + the wall rows
-static_assert(HT_TAB_FLOATS % 4 == 0, "the wall boxes after the wall rows are read as float4");
 #define HTV(T, f) V((T)[(f)], (T)[(f) + 1], (T)[(f) + 2])
 
 // lane r <-> 7 - r (half row): a joint's two sides
@@ -125,7 +124,6 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   ms.b = vsub(b.x, rv);
   const float R = HT[HT_R] + POB_MESH_MARGIN;
   uint64_t M = 0ull;
-  m = hbody_walls<MW>(WT + POB_MAXW * POB_WALL_FLOATS + HW_BBOX, ms.a, ms.b, m);  // the segment's own walls
   while (__any(m != 0u)) {
     const bool on = m != 0u;
     const int w = on ? __builtin_ctz(m) : 0;

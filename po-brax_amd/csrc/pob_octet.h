@@ -100,11 +100,8 @@ POB_D void ocap_points(const float *OT, const OBody &b, int s, v3 &p0, v3 &p1) {
 // substep re-issued ~20 scalar loads and waited for them (SQ_WAIT_ANY was 42 % of a wave's
 // cycles at HH B = 4 096 on the sixteen-lane kernel).
 #define HW_BOX 0                      // LDS wall table: lo.x lo.y hi.x hi.y per wall,
-#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls,
-#define HW_BBOX (4 * POB_MAXW + 8)    // then the per-body boxes (pob_sys wall_blo / wall_bhi)
-#define HW_FLOATS (8 * POB_MAXW + 8)
-static_assert(HW_FLOATS <= 128, "hwalls_stage writes two entries per lane");
-static_assert(HW_BBOX % 4 == 0, "the per-body boxes are read as float4");
+#define HW_CZ (4 * POB_MAXW)          // then wall_cz, wall_hz, s_pos, friction, n_walls
+#define HW_FLOATS (4 * POB_MAXW + 5)
 template <int MW>
 struct HWalls {
   float lx[MW > 0 ? MW : 1], ly[MW > 0 ? MW : 1], hx[MW > 0 ? MW : 1], hy[MW > 0 ? MW : 1];
@@ -117,32 +114,13 @@ struct HWalls {
 // Fill the wall table's HW_FLOATS entries (lanes 0 .. HW_FLOATS - 1 of the block's first wave
 // write one each) and, after the caller's LDS sync, read it into registers.
 POB_D void hwalls_stage(csys_t &S, float *tab, const int lane) {
-#pragma unroll
-  for (int i = lane; i < HW_FLOATS; i += 64) {
-    const int w = (i >> 2) & (POB_MAXW - 1), c = i & 3;
-    const int e = i - HW_CZ;
-    const int wb = (i - HW_BBOX) >> 2, cb = (i - HW_BBOX) & 3;
-    float v = 0.0f;
-    if (i >= HW_BBOX) v = cb < 2 ? S.wall_blo[wb][cb] : S.wall_bhi[wb][cb - 2];
-    else if (e >= 0) v = e == 0 ? S.wall_cz : e == 1 ? S.wall_hz : e == 2 ? S.s_pos : e == 3 ? S.friction
-                                                                                 : __int_as_float(S.n_walls);
-    else v = c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2];
-    tab[i] = v;
+  if (lane < HW_FLOATS) {
+    const int w = lane >> 2, c = lane & 3;
+    const int e = lane - HW_CZ;
+    tab[lane] = e >= 0 ? (e == 0 ? S.wall_cz : e == 1 ? S.wall_hz : e == 2 ? S.s_pos : e == 3 ? S.friction
+                                                                                  : __int_as_float(S.n_walls))
+                       : (c < 2 ? S.wall_lo[w][c] : S.wall_hi[w][c - 2]);
   }
-}
-// bit w when the segment [A, B]'s xy AABB meets wall w's per-body box (LDS table WB = the
-// HW_BBOX entries), for the walls of m
-template <int MW>
-POB_D uint32_t hbody_walls(const float *WB, const v3 A, const v3 B, const uint32_t m) {
-  const float mnx = fminf(A.x, B.x), mxx = fmaxf(A.x, B.x), mny = fminf(A.y, B.y), mxy = fmaxf(A.y, B.y);
-  uint32_t r = 0u;
-#pragma unroll
-  for (int w = 0; w < MW; ++w) {
-    const float4 bx = *reinterpret_cast<const float4 *>(WB + 4 * w);
-    const bool near = (mnx <= bx.z) & (mxx >= bx.x) & (mny <= bx.w) & (mxy >= bx.y) & (((m >> w) & 1u) != 0u);
-    r |= near ? 1u << w : 0u;
-  }
-  return r;
 }
 template <int MW>
 POB_D void hwalls_load(const float *tab, HWalls<MW> &HW) {
@@ -215,23 +193,22 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
     }
   }
   uint64_t M[ONB] = {0ull, 0ull};
-  if (__any(lane_mask != 0u)) {
-    // per slot: the walls its segment's box meets, then the face cull per (slot, wall) pair
-    const float *WBB = WT + POB_MAXW * POB_WALL_FLOATS + HW_BBOX;
-    uint32_t m = hbody_walls<MW>(WBB, ms.a[0], ms.b[0], lane_mask) | (hbody_walls<MW>(WBB, ms.a[1], ms.b[1], lane_mask) << 8);
+  {
+    const float R0 = OT[OT_B(0) + 1] + POB_MESH_MARGIN, R1 = OT[OT_B(1) + 1] + POB_MESH_MARGIN;
+    uint32_t m = lane_mask;
     while (__any(m != 0u)) {
       const bool on = m != 0u;
-      const int bit = on ? __builtin_ctz(m) : 0;
+      const int w = on ? __builtin_ctz(m) : 0;
       m &= m - 1u;
-      const int s = bit >> 3, w = bit & 7;
       const MWall W = mwall_row(WT + POB_WALL_FLOATS * w);
-      const bool seg = !(isA && s == 0);
-      const v3 La = mwall_local(W, HW.cz, vsel3(s == 0, ms.a[0], ms.a[1]));
-      const v3 Lb = seg ? mwall_local(W, HW.cz, vsel3(s == 0, ms.b[0], ms.b[1])) : La;
-      const float R = (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) + POB_MESH_MARGIN;
-      const uint64_t fm = on ? (uint64_t)mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, R) << (8 * w) : 0ull;
-      M[0] |= s == 0 ? fm : 0ull;
-      M[1] |= s == 1 ? fm : 0ull;
+#pragma unroll
+      for (int s = 0; s < ONB; ++s) {
+        const bool seg = !(isA && s == 0);
+        const v3 La = mwall_local(W, HW.cz, ms.a[s]);
+        const v3 Lb = seg ? mwall_local(W, HW.cz, ms.b[s]) : La;
+        const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, s == 0 ? R0 : R1);
+        M[s] |= on ? (uint64_t)fm << (8 * w) : 0ull;
+      }
     }
   }
 #ifdef POB_EXP_NO_WALK

@@ -56,10 +56,6 @@ struct pob_sys {
   // lane skips a wall when none of its body centres falls inside it (exact: every triangle of
   // a culled wall is farther than r from the capsule, no contact)
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
-  // per-body broadphase: world AABB of each wall grown by (largest capsule radius + 2e-3); a
-  // body whose segment's xy AABB misses it is farther than r + 1e-3 from the wall: no face of
-  // it is walked (the face cull would keep none that can penetrate)
-  float wall_blo[POB_MAXW][2], wall_bhi[POB_MAXW][2];
   float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
   float friction, s_pos, half_s_ang;
   // legacy spring dynamics (pob_params.legacy_spring; brax <= 0.0.12): joint stiffness, spring

@@ -266,8 +266,6 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
       reach = fmax(reach, sqrt((double)e[0] * e[0] + (double)e[1] * e[1] + (double)e[2] * e[2]) + s.cap_r[i]);
     }
   reach += 1e-3;
-  double rmax = 0.0;
-  for (int i = 0; i < POB_NDYN; ++i) rmax = fmax(rmax, (double)s.cap_r[i]);
   for (int w = 0; w < s.n_walls; ++w) {
     const double c = fabs((double)s.wall_cos[w]), sn = fabs((double)s.wall_sin[w]);
     const double ex[3] = {c * s.wall_h[w][0] + sn * s.wall_h[w][1], sn * s.wall_h[w][0] + c * s.wall_h[w][1],
@@ -275,10 +273,6 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     for (int k = 0; k < 3; ++k) {
       s.wall_lo[w][k] = (float)(s.wall_c[w][k] - ex[k] - reach);
       s.wall_hi[w][k] = (float)(s.wall_c[w][k] + ex[k] + reach);
-    }
-    for (int k = 0; k < 2; ++k) {
-      s.wall_blo[w][k] = (float)(s.wall_c[w][k] - ex[k] - (rmax + 2e-3));
-      s.wall_bhi[w][k] = (float)(s.wall_c[w][k] + ex[k] + (rmax + 2e-3));
     }
   }
   // joint frames the step kernel specialises (pob_quad.h qjoint_position): every offset lies in
