@@ -178,30 +178,42 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
   const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
   const float e_d = FMA(hb2, hb2, ha2 * ha2), i_d = g.rcp(e_d);
   MCand c[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) { c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f; }
+  // Exact skips: a candidate provably farther than R = r + 1e-3 from the triangle has a computed
+  // d2 above T (coordinate errors here are ~1e-6), so it can neither win with a contact nor
+  // change a winner without one -- the face cull's argument, per candidate: an end point at
+  // |w - w0| >= R from the face plane, an edge whose line the segment's box misses by >= R
+  // along one of the two axes across it.  (A NaN bound never skips.)
+  const float R = r + POB_MESH_MARGIN;
   // end point A (and B) against each triangle
-  {
+  if (!(fabsf(S.aw - w0) >= R)) {
     float qa[2], qb[2];
     mtri_closest2(ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa[0], qb[0], qa[1], qb[1]);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f;
-      mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0);
-    }
+    for (int t = 0; t < 2; ++t) mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0);
   }
   if (seg) {
-    float qa[2], qb[2];
-    mtri_closest2(ha, hb, ha2, hb2, i_d, Ba, Bb, qa[0], qb[0], qa[1], qb[1]);
+    if (!(fabsf(Bw - w0) >= R)) {
+      float qa[2], qb[2];
+      mtri_closest2(ha, hb, ha2, hb2, i_d, Ba, Bb, qa[0], qb[0], qa[1], qb[1]);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0);
+      for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0);
+    }
     S.Da = Ba - S.aa_; S.Db = Bb - S.ab; S.Dw = Bw - S.aw;
     S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
     S.inv_aa = g.rcp(S.aa);
     const float e_a = ha2 * ha2, e_b = hb2 * hb2;
     const float i_a = g.rcp(e_a), i_b = g.rcp(e_b);
+    // the segment's box across the edges: gaps to a = +-ha, b = +-hb and to the plane
+    const float amn = fminf(S.aa_, Ba), amx = fmaxf(S.aa_, Ba), bmn = fminf(S.ab, Bb), bmx = fmaxf(S.ab, Bb);
+    const float gw = fmaxf(fminf(S.aw, Bw) - w0, w0 - fmaxf(S.aw, Bw));
+    const bool bottom = !(fmaxf(fmaxf(bmn + hb, -hb - bmx), gw) >= R), top = !(fmaxf(fmaxf(bmn - hb, hb - bmx), gw) >= R);
+    const bool right = !(fmaxf(fmaxf(amn - ha, ha - amx), gw) >= R), left = !(fmaxf(fmaxf(amn + ha, -ha - amx), gw) >= R);
     // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (the diagonal's
     // candidate is the same closest pair for both: evaluated once, taken in each order)
-    mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);
-    mseg_edge(g, c[0], S, ha, -hb, w0, 0.0f, hb2, e_b, i_b);
+    if (bottom) mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);
+    if (right) mseg_edge(g, c[0], S, ha, -hb, w0, 0.0f, hb2, e_b, i_b);
     MCand dg;
     dg.d2 = __builtin_inff(); dg.u = 0.0f; dg.da = 0.0f; dg.db = 0.0f; dg.dw = 0.0f;
     mseg_edge(g, dg, S, -ha, -hb, w0, ha2, hb2, e_d, i_d);
@@ -210,8 +222,8 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       if (dg.d2 < c[t].d2) c[t] = dg;
-    mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a);
-    mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);
+    if (top) mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a);
+    if (left) mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);
     // the segment crossing the face plane inside the triangle
     const float aw = S.aw - w0, bw = Bw - w0;
     if (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f))) {
