@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, final pass on the HEAD build: the GPU suite, smoke(), the bench lines of every
+# Round 4, final pass on the HEAD build: the GPU suite, smoke(), the candidate-skip A/B, the bench lines of every
 # BASELINE config and of the per-GPU batches of the 1/2/4/8-GPU sweep, and PMC profiles of the
 # eight- / sixteen-lane configs (the four-lane kernel is unchanged since profiles/r4m).
 set -o pipefail
@@ -11,6 +11,10 @@ fatal() { case $1 in 124|134|137|139) echo "fatal exit $1 in $2"; exit $1;; esac
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; fatal $rc pytest
 tail -2 $OUT/pytest_gpu.log; grep -E "FAILED|Error" $OUT/pytest_gpu.log | head -20
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?; fatal $rc smoke; tail -4 $OUT/smoke.log
+# A/B: the exact candidate skips (libpob) against the build before them (build_variants/noskip.so)
+rm -rf gpurun_out/ab
+R=2 BS="65536 4096" ENVS="ant_heavenhell ant_tag" timeout -k 10 400 bash scripts/ab_bench.sh > $OUT/ab_skip.txt 2>&1; rc=$?; fatal $rc ab
+cat $OUT/ab_skip.txt
 for spec in "default:" "legacy:--legacy-spring" "hh_32768:--batch 32768" "hh_16384:--batch 16384" "hh_8192:--batch 8192" "hh_4096:--global-batch 4096" \
             "tag_65536:--env ant_tag" "tag_32768:--env ant_tag --batch 32768" "tag_16384:--env ant_tag --batch 16384" "tag_8192:--env ant_tag --global-batch 8192" \
             "ga_16384:--env ant_gather --global-batch 16384" "mixed_f16_32768:--env mixed --qp-dtype f16 --global-batch 32768" "gym_hh:--gym"; do
