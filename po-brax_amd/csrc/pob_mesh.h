@@ -104,11 +104,10 @@ POB_D void mtri_closest2(const float ha, const float hb, const float ha2, const 
 // running closest candidate: squared distance, segment parameter, S - P (face coordinates)
 struct MCand {
   float d2, u, da, db, dw;
-  int k;  // the candidate's kind (mface_cand's numbering; mesh_face records it for the velocity pass)
 };
-POB_D void mcand_take(MCand &c, const float u, const float da, const float db, const float dw, const int k = 0) {
+POB_D void mcand_take(MCand &c, const float u, const float da, const float db, const float dw) {
   const float d2 = FMA(dw, dw, FMA(db, db, da * da));
-  if (d2 < c.d2) { c.d2 = d2; c.u = u; c.da = da; c.db = db; c.dw = dw; c.k = k; }
+  if (d2 < c.d2) { c.d2 = d2; c.u = u; c.da = da; c.db = db; c.dw = dw; }
 }
 
 // closest point of face triangle t to the plane point (pa, pb) (oracle tri_closest): the point
@@ -143,7 +142,7 @@ struct MSeg {
 };
 template <class G>
 POB_D void mseg_edge(G &g, MCand &c, const MSeg &S, const float e0a, const float e0b, const float w0, const float fa,
-                     const float fb, const float ee, const float inv_ee, const int kind = 0) {
+                     const float fb, const float ee, const float inv_ee) {
   const float ra = S.aa_ - e0a, rb = S.ab - e0b, rw = S.aw - w0;
   const float f = FMA(fb, rb, fa * ra);
   const float cc = FMA(S.Dw, rw, FMA(S.Db, rb, S.Da * ra));
@@ -155,13 +154,12 @@ POB_D void mseg_edge(G &g, MCand &c, const MSeg &S, const float e0a, const float
   if (t < 0.0f) { t = 0.0f; u = clamp01(-cc * S.inv_aa); }
   else if (t > 1.0f) { t = 1.0f; u = clamp01((bb - cc) * S.inv_aa); }
   const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
-  mcand_take(c, u, sa - FMA(t, fa, e0a), sb - FMA(t, fb, e0b), sw - w0, kind);
+  mcand_take(c, u, sa - FMA(t, fa, e0a), sb - FMA(t, fb, e0b), sw - w0);
 }
 
 // The contacts of face f (0..5) of a wall with half extents (hx, hy, hz) against the segment
 // [A, B] (wall frame; seg = false: the point A, the torso sphere), radius r, T = r^2 (1 + 2^-20):
-// emit(tau, n_local, pen, t, kind) for triangle 0 then 1 when it penetrates (kind: the winning
-// candidate's, mface_cand's numbering).  tau = 1 - 2u places the
+// emit(tau, n_local, pen) for triangle 0 then 1 when it penetrates.  tau = 1 - 2u places the
 // contact on the capsule's segment x + tau rotate(e0, q) (A = x + rotate(e0), B = x - rotate(e0)).
 // A triangle with d2 >= T has sqrt_rn(d2) >= r (no contact): its square root is skipped.
 template <class G, class F>
@@ -181,7 +179,7 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
   const float e_d = FMA(hb2, hb2, ha2 * ha2), i_d = g.rcp(e_d);
   MCand c[2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) { c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f; c[t].k = 0; }
+  for (int t = 0; t < 2; ++t) { c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f; }
   // Exact skips: a candidate provably farther than R = r + 1e-3 from the triangle has a computed
   // d2 above T (coordinate errors here are ~1e-6), so it can neither win with a contact nor
   // change a winner without one -- the face cull's argument, per candidate: an end point at
@@ -193,14 +191,14 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
     float qa[2], qb[2];
     mtri_closest2(ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa[0], qb[0], qa[1], qb[1]);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0, 0);
+    for (int t = 0; t < 2; ++t) mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0);
   }
   if (seg) {
     if (!(fabsf(Bw - w0) >= R)) {
       float qa[2], qb[2];
       mtri_closest2(ha, hb, ha2, hb2, i_d, Ba, Bb, qa[0], qb[0], qa[1], qb[1]);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0, 1);
+      for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0);
     }
     S.Da = Ba - S.aa_; S.Db = Bb - S.ab; S.Dw = Bw - S.aw;
     S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
@@ -214,18 +212,18 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
     const bool right = !(fmaxf(fmaxf(amn - ha, ha - amx), gw) >= R), left = !(fmaxf(fmaxf(amn + ha, -ha - amx), gw) >= R);
     // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (the diagonal's
     // candidate is the same closest pair for both: evaluated once, taken in each order)
-    if (bottom) mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a, 2);
-    if (right) mseg_edge(g, c[0], S, ha, -hb, w0, 0.0f, hb2, e_b, i_b, 3);
+    if (bottom) mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);
+    if (right) mseg_edge(g, c[0], S, ha, -hb, w0, 0.0f, hb2, e_b, i_b);
     MCand dg;
-    dg.d2 = __builtin_inff(); dg.u = 0.0f; dg.da = 0.0f; dg.db = 0.0f; dg.dw = 0.0f; dg.k = 0;
+    dg.d2 = __builtin_inff(); dg.u = 0.0f; dg.da = 0.0f; dg.db = 0.0f; dg.dw = 0.0f;
     mseg_edge(g, dg, S, -ha, -hb, w0, ha2, hb2, e_d, i_d);
     // (taken on its own squared distance: an untaken dg -- a NaN or overflowing candidate,
     // which the oracle never takes -- keeps d2 = inf, not the 0 of its cleared fields)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
-      if (dg.d2 < c[t].d2) { c[t] = dg; c[t].k = t == 0 ? 4 : 2; }
-    if (top) mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a, 3);
-    if (left) mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b, 4);
+      if (dg.d2 < c[t].d2) c[t] = dg;
+    if (top) mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a);
+    if (left) mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);
     // the segment crossing the face plane inside the triangle
     const float aw = S.aw - w0, bw = Bw - w0;
     if (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f))) {
@@ -233,7 +231,7 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
       const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        if (mtri_inside(t == 1, ha, hb, sa, sb)) mcand_take(c[t], u, 0.0f, 0.0f, sw - w0, 5);
+        if (mtri_inside(t == 1, ha, hb, sa, sb)) mcand_take(c[t], u, 0.0f, 0.0f, sw - w0);
     }
   }
 #pragma unroll
@@ -251,7 +249,7 @@ POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, 
         else { na = 0.0f; nb = 0.0f; nw = sg; }
         // face -> wall frame
         const v3 nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
-        emit(1.0f - 2.0f * c[t].u, nl, pen, t, c[t].k);
+        emit(1.0f - 2.0f * c[t].u, nl, pen);
       }
     }
   }
@@ -300,7 +298,7 @@ POB_D MFace mface(G &g, const int f, const v3 A, const v3 B, const float hx, con
 template <class G>
 POB_D MCand mface_cand(G &g, const MFace &F, const bool seg, const int t, const int kk) {
   MCand c;
-  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f; c.k = kk;
+  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
   if (kk == 0 || (kk == 1 && seg)) {
     const float pa = kk == 0 ? F.pa : F.qa, pb = kk == 0 ? F.pb : F.qb, pw = kk == 0 ? F.pw : F.qw;
     float qa, qb;
@@ -355,26 +353,6 @@ POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, co
   return true;
 }
 
-// The contacts of face f that mesh_face found with winning candidates kb (one byte of
-// mesh_lane_walk's kinds): each recorded triangle's winner recomputed alone (mface_cand: the
-// same operations on the same operands as mesh_face's), its contact emitted -- the contacts
-// of mesh_face in order, without its other candidates.
-template <class G, class F>
-POB_D void mesh_face_kinds(G &g, const int f, const v3 A, const v3 B, const bool seg, const float hx, const float hy,
-                           const float hz, const float r, const float T, const uint32_t kb, F &&emit) {
-  const MFace Fc = mface(g, f, A, B, hx, hy, hz);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const uint32_t kt = kb >> (4 * t);
-    if (kt & 8u) {
-      const MCand c = mface_cand(g, Fc, seg, t, (int)(kt & 7u));
-      float tau, pen;
-      v3 nl;
-      if (mface_contact(g, Fc, c, r, T, tau, nl, pen)) emit(tau, nl, pen);
-    }
-  }
-}
-
 #ifndef POB_MESH_HOST
 // ---------------------------------------------------------------- the wave's face walk
 // Walk the lanes' face items (M[s]: bit 8 w + f for face f of wall w of the lane's body slot
@@ -407,17 +385,9 @@ POB_D void mlexmin_dpp(float &d, int &kk) {
 }
 
 // each lane walks its own items, one face per iteration (mesh_face)
-// kinds (optional): per slot, byte i = the i-th face with contacts (in walk order, i < 4):
-// bits 0-2 / 4-6 the winning candidate kinds of triangles 0 / 1, bits 3 / 7 set when the
-// triangle has a contact (mesh_face_kinds re-derives exactly those contacts)
 template <int NB, class G, class SegOf, class Apply>
 POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
-                          Apply &&apply, uint32_t (*kinds)[NB] = nullptr) {
-  uint32_t nf = 0u;  // faces with contacts so far, 4 bits per slot
-  if (kinds) {
-#pragma unroll
-    for (int q = 0; q < NB; ++q) (*kinds)[q] = 0u;
-  }
+                          Apply &&apply) {
   while (true) {
     bool has = false;
     int s = 0;
@@ -442,64 +412,9 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
       const v3 La = mwall_local(W, cz, A);
       const v3 Lb = seg ? mwall_local(W, cz, B) : La;
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      const uint32_t fi = (nf >> (4 * s)) & 15u;
-      bool hitf = false;
-      mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T,
-                [&](const float tau, const v3 nl, const float pen, const int t, const int kind) {
-        if (kinds && fi < 4u) {
-          const uint32_t v = (uint32_t)(kind | 8) << (8 * fi + 4 * t);
-#pragma unroll
-          for (int q = 0; q < NB; ++q) (*kinds)[q] |= s == q ? v : 0u;
-        }
-        hitf = true;
+      mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
         apply(s, bit, tau, mwall_world_n(W, nl), pen);
       });
-      nf += hitf ? 1u << (4 * s) : 0u;
-    }
-  }
-}
-
-// The velocity pass's walk over the faces that had contacts (M: per slot, the face bits in
-// order): faces with recorded kinds re-derive only their winning candidates, the rest (a
-// slot's fifth contact face and later) run mesh_face again -- the same contacts either way.
-template <int NB, class G, class SegOf, class Apply>
-POB_D void mesh_kinds_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB],
-                           const uint32_t (&kinds)[NB], SegOf &&seg_of, Apply &&apply) {
-  uint32_t nf = 0u;
-  while (true) {
-    bool has = false;
-    int s = 0;
-    uint64_t ml = 0ull;
-#pragma unroll
-    for (int q = NB - 1; q >= 0; --q) {
-      const bool h = M[q] != 0ull;
-      s = h ? q : s;
-      ml = h ? M[q] : ml;
-      has = has | h;
-    }
-    if (!__any(has)) break;
-    const int bit = has ? __builtin_ctzll(ml) : 0;
-#pragma unroll
-    for (int q = 0; q < NB; ++q) M[q] = (has && s == q) ? (M[q] & (M[q] - 1ull)) : M[q];
-    if (has) {
-      v3 A, B;
-      float r;
-      bool seg;
-      seg_of(s, A, B, r, seg);
-      const MWall W = mwall_row(WT + POB_WALL_FLOATS * (bit >> 3));
-      const v3 La = mwall_local(W, cz, A);
-      const v3 Lb = seg ? mwall_local(W, cz, B) : La;
-      const float T = (r * r) * 1.00000095367431640625f;
-      const uint32_t fi = (nf >> (4 * s)) & 15u;
-      nf += 1u << (4 * s);
-      uint32_t ks = 0u;
-#pragma unroll
-      for (int q = 0; q < NB; ++q) ks = s == q ? kinds[q] : ks;
-      const auto em = [&](const float tau, const v3 nl, const float pen) { apply(s, bit, tau, mwall_world_n(W, nl), pen); };
-      if (fi < 4u) mesh_face_kinds(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T, (ks >> (8 * fi)) & 0xFFu, em);
-      else
-        mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T,
-                  [&](const float tau, const v3 nl, const float pen, const int, const int) { em(tau, nl, pen); });
     }
   }
 }

@@ -114,8 +114,7 @@ struct QGround {
 // contact in registers.
 struct QMesh {
   v3 a[QNB], b[QNB];
-  uint64_t mc[QNB];     // per body: the faces that produced a contact (bit 8 w + f)
-  uint32_t kinds[QNB];  // per body: those faces' winning candidates (pob_mesh.h mesh_lane_walk)
+  uint64_t mc[QNB];  // per body: the faces that produced a contact (bit 8 w + f)
 };
 
 // The Ant's capsules (checked by pob_system.cpp) have opposite end points +-e0 in the body
@@ -264,7 +263,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
     ms.mc[0] |= l == 0 ? 1ull << bit : 0ull;
     ms.mc[1] |= l == 1 ? 1ull << bit : 0ull;
     ms.mc[2] |= l == 2 ? 1ull << bit : 0ull;
-  }, &ms.kinds);
+  });
 }
 
 // Velocity pass: ground contacts, then the wall contacts re-derived from the stored segments
@@ -293,10 +292,9 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
   POB_FENCE();
   uint64_t M[QNB];
   M[0] = ms.mc[0]; M[1] = ms.mc[1]; M[2] = ms.mc[2];
-  // (the winning candidates recorded by the position pass: each contact recomputed alone)
-  mesh_kinds_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M, ms.kinds,
-                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                       [&](const int l, const int, const float tau, const v3 n, const float pen) {
+  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+                      [&](const int l, const int, const float tau, const v3 n, const float pen) {
     const v3 x = qpick3(l, b.x);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
     v3 dv = qpick3(l, dV), dw = qpick3(l, dW);

@@ -49,7 +49,7 @@ extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    mesh_face(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float pen, int, int) {
+    mesh_face(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float pen) {
       const v3 nw = mwall_world_n(W, nl);
       out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
       ++n;
@@ -87,32 +87,6 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
   }
   return n;
 }
-// the velocity pass's form: mesh_face recording each contact's winning candidate kind, then
-// mesh_face_kinds re-deriving the contacts from those kinds alone (must give the same contacts)
-extern "C" int host_mesh_contacts_kinds(const float *w, const float *a, const float *b, int seg, float r, float *out) {
-  MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
-  const float cz = w[2], hz = w[7];
-  const v3 La = mwall_local(W, cz, V(a[0], a[1], a[2]));
-  const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
-  const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
-  const float T = (r * r) * 1.00000095367431640625f;
-  HostGuard g;
-  int n = 0;
-  for (int f = 0; f < 6; ++f) {
-    if (!((fm >> f) & 1u)) continue;
-    uint32_t kb = 0u;
-    mesh_face(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, [&](float, v3, float, int t, int kind) {
-      kb |= (uint32_t)(kind | 8) << (4 * t);
-    });
-    if (!kb) continue;
-    mesh_face_kinds(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, kb, [&](float tau, v3 nl, float pen) {
-      const v3 nw = mwall_world_n(W, nl);
-      out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
-      ++n;
-    });
-  }
-  return n;
-}
 """
 
 
@@ -129,7 +103,6 @@ def host_mesh(tmp_path_factory):
     FP = C.POINTER(C.c_float)
     lib.host_mesh_contacts.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     lib.host_mesh_contacts_split.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
-    lib.host_mesh_contacts_kinds.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     return lib
 
 
@@ -166,8 +139,6 @@ def test_kernel_mesh_code_equals_oracle_bitwise(host_mesh):
         out2 = np.zeros((12, 5), np.float32)
         n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
         assert n2 == n and np.array_equal(out2[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split", out2[:n2], ref)
-        n3 = host_mesh.host_mesh_contacts_kinds(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
-        assert n3 == n and np.array_equal(out2[:n3].view(np.uint32), ref.view(np.uint32)), (it, "kinds", out2[:n3], ref)
         n_cases += 1
         n_contacts += n
     assert n_contacts > 2000, n_contacts
