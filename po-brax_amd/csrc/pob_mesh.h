@@ -334,6 +334,99 @@ POB_D MCand mface_cand(G &g, const MFace &F, const bool seg, const int t, const 
   return c;
 }
 
+// mface_cand without branches (the cooperative walk: a wave's lanes hold different kinds, so
+// a kind's branch would be executed by the whole wave anyway): every form -- the end point, the
+// edge, the crossing -- computed, the lane's kind selected.  The same operations on the same
+// operands as mface_cand where its branches are taken; the forms a lane does not need run on
+// substituted operands (1 under a reciprocal) that keep the range guards quiet.
+template <class G>
+POB_D MCand mface_cand_bf(G &g, const MFace &F, const bool seg, const int t, const int kk) {
+  const bool t1 = t == 1;
+  // end point kk (A for 0, B for 1)
+  const bool ep = kk == 0 || (kk == 1 && seg);
+  const bool isb = kk == 1;
+  const float pa = isb ? F.qa : F.pa, pb = isb ? F.qb : F.pb, pw = isb ? F.qw : F.pw;
+  float qa, qb;
+  {
+    const float ha = F.ha, hb = F.hb;
+    const float cr = FMA(pa + ha, hb, -((pb + hb) * ha));
+    const bool in = t1 ? ((pb <= hb) & (pa >= -ha) & (cr <= 0.0f)) : ((pb >= -hb) & (pa <= ha) & (cr >= 0.0f));
+    const float s_ = clamp01(FMA(pb + hb, F.hb2, (pa + ha) * F.ha2) * F.i_d);
+    const float s2 = 2.0f * s_;
+    const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
+    const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
+    const float e0a = t1 ? da : ca, e0b = t1 ? db : -hb;
+    const float e1a = t1 ? ca : ha, e1b = t1 ? hb : cb;
+    const float e2a = t1 ? -ha : da, e2b = t1 ? cb : db;
+    const float g0 = pa - e0a, h0 = pb - e0b;
+    float best = FMA(h0, h0, g0 * g0);
+    float ra = e0a, rb = e0b;
+    const float g1 = pa - e1a, h1 = pb - e1b;
+    const float d1 = FMA(h1, h1, g1 * g1);
+    const bool b1 = d1 < best;
+    best = b1 ? d1 : best; ra = b1 ? e1a : ra; rb = b1 ? e1b : rb;
+    const float g2 = pa - e2a, h2 = pb - e2b;
+    const float d2 = FMA(h2, h2, g2 * g2);
+    const bool b2 = d2 < best;
+    ra = b2 ? e2a : ra; rb = b2 ? e2b : rb;
+    qa = in ? pa : ra; qb = in ? pb : rb;
+  }
+  const float ea_ = pa - qa, eb_ = pb - qb, ew_ = pw - F.w0;
+  const float e_d2 = FMA(ew_, ew_, FMA(eb_, eb_, ea_ * ea_));
+  // edge kk (2..4) of triangle t
+  MSeg S;
+  S.aa_ = F.pa; S.ab = F.pb; S.aw = F.pw;
+  S.Da = F.qa - F.pa; S.Db = F.qb - F.pb; S.Dw = F.qw - F.pw;
+  const bool ed = seg && kk >= 2 && kk <= 4;
+  S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
+  S.inv_aa = g.rcp(ed ? S.aa : 1.0f);
+  const bool diag = t == 0 ? kk == 4 : kk == 2;
+  const bool first = t == 0 ? kk == 2 : kk == 3;
+  const float ha = F.ha, hb = F.hb, ha2 = F.ha2, hb2 = F.hb2;
+  const float e0a = diag ? -ha : (t == 0 ? (first ? -ha : ha) : (first ? ha : -ha));
+  const float e0b = diag ? -hb : (t == 0 ? -hb : hb);
+  const float fa = diag ? ha2 : (first ? (t == 0 ? ha2 : -ha2) : 0.0f);
+  const float fb = diag ? hb2 : (first ? 0.0f : (t == 0 ? hb2 : -hb2));
+  const float ee = diag ? FMA(hb2, hb2, ha2 * ha2) : (first ? ha2 * ha2 : hb2 * hb2);
+  const float inv_ee = diag ? F.i_d : g.rcp(ed ? ee : 1.0f);
+  float su, sda, sdb, sdw;
+  {
+    const float ra = S.aa_ - e0a, rb = S.ab - e0b, rw = S.aw - F.w0;
+    const float f = FMA(fb, rb, fa * ra);
+    const float cc = FMA(S.Dw, rw, FMA(S.Db, rb, S.Da * ra));
+    const float bb = FMA(S.Db, fb, S.Da * fa);
+    const float den = FMA(S.aa, ee, -(bb * bb));
+    const bool dp = den > 0.0f;
+    const float u0 = dp ? clamp01(FMA(bb, f, -(cc * ee)) * g.rcp(ed && dp ? den : 1.0f)) : 0.0f;
+    const float t0 = FMA(bb, u0, f) * inv_ee;
+    const bool tl = t0 < 0.0f, tg = !tl && (t0 > 1.0f);
+    const float u = tl ? clamp01(-cc * S.inv_aa) : (tg ? clamp01((bb - cc) * S.inv_aa) : u0);
+    const float tt = tl ? 0.0f : (tg ? 1.0f : t0);
+    const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
+    su = u; sda = sa - FMA(tt, fa, e0a); sdb = sb - FMA(tt, fb, e0b); sdw = sw - F.w0;
+  }
+  const float s_d2 = FMA(sdw, sdw, FMA(sdb, sdb, sda * sda));
+  // the crossing (kk 5)
+  const float aw = F.pw - F.w0, bw = F.qw - F.w0;
+  const bool cr = seg && kk == 5 && (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f)));
+  const float cu = aw * g.rcp(cr ? aw - bw : 1.0f);
+  const float csa = FMA(cu, S.Da, S.aa_), csb = FMA(cu, S.Db, S.ab), csw = FMA(cu, S.Dw, S.aw);
+  const bool cin = cr && (t1 ? ((csb <= hb) & (csa >= -ha) & (FMA(csa + ha, hb, -((csb + hb) * ha)) <= 0.0f))
+                             : ((csb >= -hb) & (csa <= ha) & (FMA(csa + ha, hb, -((csb + hb) * ha)) >= 0.0f)));
+  const float cdw = csw - F.w0;
+  const float c_d2 = FMA(cdw, cdw, FMA(0.0f, 0.0f, 0.0f * 0.0f));
+  // the lane's kind (mcand_take's rule: a NaN or +inf d2 is not taken: d2 stays +inf, fields 0)
+  MCand c;
+  const float d2 = ep ? e_d2 : (ed ? s_d2 : (cin ? c_d2 : __builtin_inff()));
+  const bool take = d2 < __builtin_inff();
+  c.d2 = take ? d2 : __builtin_inff();
+  c.u = take ? (ep ? (isb ? 1.0f : 0.0f) : (ed ? su : cu)) : 0.0f;
+  c.da = take ? (ep ? ea_ : (ed ? sda : 0.0f)) : 0.0f;
+  c.db = take ? (ep ? eb_ : (ed ? sdb : 0.0f)) : 0.0f;
+  c.dw = take ? (ep ? ew_ : (ed ? sdw : cdw)) : 0.0f;
+  return c;
+}
+
 // the contact of a triangle whose winning candidate is c (mesh_face's emission): tau, the
 // wall-frame normal and the penetration; false when the triangle does not penetrate
 template <class G>
@@ -491,7 +584,7 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     const v3 La = mwall_local(W, cz, Ao);
     const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
     const MFace F = mface(g, mo & 7, La, Lb, W.hx, W.hy, hz);
-    const MCand c = mface_cand(g, F, sego, tri, gv ? kk : 7);
+    const MCand c = mface_cand_bf(g, F, sego, tri, gv ? kk : 7);
     // each triangle's winner over its eight lanes
     float dmin = c.d2;
     int kmin = kk;

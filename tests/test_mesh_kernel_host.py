@@ -87,6 +87,37 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
   }
   return n;
 }
+// the same with the branch-free candidates of the cooperative walk (mface_cand_bf)
+extern "C" int host_mesh_contacts_split_bf(const float *w, const float *a, const float *b, int seg, float r, float *out) {
+  MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
+  const float cz = w[2], hz = w[7];
+  const v3 La = mwall_local(W, cz, V(a[0], a[1], a[2]));
+  const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
+  const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
+  const float T = (r * r) * 1.00000095367431640625f;
+  HostGuard g;
+  int n = 0;
+  for (int f = 0; f < 6; ++f) {
+    if (!((fm >> f) & 1u)) continue;
+    const MFace F = mface(g, f, La, Lb, W.hx, W.hy, hz);
+    for (int t = 0; t < 2; ++t) {
+      MCand best; int kb = 0;
+      for (int kk = 0; kk < 8; ++kk) {
+        const MCand c = mface_cand_bf(g, F, seg != 0, t, kk);
+        const MCand c0 = mface_cand(g, F, seg != 0, t, kk);
+        if (memcmp(&c, &c0, sizeof(MCand)) != 0) return -1000 - kk;  // the forms disagree
+        if (kk == 0 || c.d2 < best.d2 || (c.d2 == best.d2 && kk < kb)) { best = c; kb = kk; }
+      }
+      float tau, pen; v3 nl;
+      if (mface_contact(g, F, best, r, T, tau, nl, pen)) {
+        const v3 nw = mwall_world_n(W, nl);
+        out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
+        ++n;
+      }
+    }
+  }
+  return n;
+}
 """
 
 
@@ -103,6 +134,7 @@ def host_mesh(tmp_path_factory):
     FP = C.POINTER(C.c_float)
     lib.host_mesh_contacts.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     lib.host_mesh_contacts_split.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
+    lib.host_mesh_contacts_split_bf.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     return lib
 
 
@@ -139,6 +171,8 @@ def test_kernel_mesh_code_equals_oracle_bitwise(host_mesh):
         out2 = np.zeros((12, 5), np.float32)
         n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
         assert n2 == n and np.array_equal(out2[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split", out2[:n2], ref)
+        n3 = host_mesh.host_mesh_contacts_split_bf(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
+        assert n3 == n and np.array_equal(out2[:n3].view(np.uint32), ref.view(np.uint32)), (it, "split_bf", n3, ref)
         n_cases += 1
         n_contacts += n
     assert n_contacts > 2000, n_contacts
@@ -166,5 +200,7 @@ def test_kernel_mesh_code_non_finite_segments(host_mesh):
         assert n == len(ref) and np.array_equal(out[:n].view(np.uint32), ref.view(np.uint32)), (it, pa, pb, n, ref)
         n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
         assert n2 == len(ref) and np.array_equal(out[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split", pa, pb)
+        n3 = host_mesh.host_mesh_contacts_split_bf(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
+        assert n3 == len(ref) and np.array_equal(out[:n3].view(np.uint32), ref.view(np.uint32)), (it, "split_bf", n3)
         n_cases += 1
     assert n_cases == 3000
