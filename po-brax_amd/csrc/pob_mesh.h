@@ -477,34 +477,6 @@ POB_D void mlexmin_dpp(float &d, int &kk) {
   kk = take ? ok : kk;
 }
 
-// mesh_face's contacts returned as a value, compiled out of line (POB_MESH_OUTLINE): the
-// per-lane walk's face evaluation then lives in its own function, whose registers do not
-// count against the caller's substep loop (the four-lane kernel spills at 128 VGPRs)
-template <class G>
-struct MFaceOut {
-  float tau0, pen0, tau1, pen1;
-  v3 n0, n1;
-  uint32_t hit;
-  G g;
-};
-template <class G>
-__device__ __attribute__((noinline)) MFaceOut<G> mesh_face_out(G g, const int f, const v3 A, const v3 B, const bool seg,
-                                                               const float hx, const float hy, const float hz,
-                                                               const float r, const float T) {
-  MFaceOut<G> o;
-  o.hit = 0u;
-  o.tau0 = o.pen0 = o.tau1 = o.pen1 = 0.0f;
-  o.n0 = o.n1 = V(0.0f, 0.0f, 0.0f);
-  mesh_face(g, f, A, B, seg, hx, hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
-    const bool second = o.hit != 0u;
-    o.tau1 = second ? tau : o.tau1; o.pen1 = second ? pen : o.pen1; o.n1 = second ? nl : o.n1;
-    o.tau0 = second ? o.tau0 : tau; o.pen0 = second ? o.pen0 : pen; o.n0 = second ? o.n0 : nl;
-    o.hit = second ? 3u : 1u;
-  });
-  o.g = g;
-  return o;
-}
-
 // each lane walks its own items, one face per iteration (mesh_face)
 template <int NB, class G, class SegOf, class Apply>
 POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
@@ -533,16 +505,9 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
       const v3 La = mwall_local(W, cz, A);
       const v3 Lb = seg ? mwall_local(W, cz, B) : La;
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-#ifdef POB_MESH_OUTLINE
-      const MFaceOut<G> o = mesh_face_out<G>(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T);
-      g = o.g;
-      if (o.hit & 1u) apply(s, bit, o.tau0, mwall_world_n(W, o.n0), o.pen0);
-      if (o.hit & 2u) apply(s, bit, o.tau1, mwall_world_n(W, o.n1), o.pen1);
-#else
       mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
         apply(s, bit, tau, mwall_world_n(W, nl), pen);
       });
-#endif
     }
   }
 }
