@@ -114,6 +114,8 @@ def _declare(_lib):
         _lib.orc_math_check.argtypes = [C.c_int, C.c_int, _FP, _FP, _FP]
         _lib.orc_contact_stats.argtypes = [C.POINTER(C.c_longlong)]
         _lib.orc_set_face_cull.argtypes = [C.c_int]
+        _lib.orc_set_mesh_variant.argtypes = [C.c_int]
+        _lib.orc_get_mesh_variant.restype = C.c_int
         _lib.orc_contact_stats_enable.argtypes = [C.c_int]
         _lib.orc_mesh_contacts.argtypes = [_FP, _FP, _FP, C.c_int, C.c_float, _FP]
     return _lib
@@ -268,11 +270,12 @@ def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_E
 def mesh_contacts(wall, a, b, seg: bool, r: float) -> np.ndarray:
     """The oracle's capsule x TriangulatedBox contacts of one capsule (world end points a, b;
     seg False: the sphere at a) against one wall box (cx, cy, cz, cos, sin, hx, hy, hz):
-    rows (tau, nx, ny, nz, pen) in (face, triangle) order."""
+    rows (tau, nx, ny, nz, pen, cd) in (face, triangle) order; cd: the contact position is the
+    segment point moved by -cd n (the triangle point)."""
     w = np.ascontiguousarray(wall, np.float32)
     pa = np.ascontiguousarray(a, np.float32)
     pb = np.ascontiguousarray(b, np.float32)
-    out = np.zeros((12, 5), np.float32)
+    out = np.zeros((12, 6), np.float32)
     n = lib().orc_mesh_contacts(_p(w), _p(pa), _p(pb), int(bool(seg)), float(r), _p(out))
     return out[:n].copy()
 

@@ -765,6 +765,202 @@ static cand_t seg_tri(int t, float ha, float hb, float w0, f3 A, f3 B, int seg, 
   return c;
 }
 
+/* ---- brax v1's own spelling of capsule_mesh [ext, recalled] (deviation table).
+ * The exact form above computes the closest points exactly (up to rounding); brax v1 spells
+ * them with regularised divisions and another candidate set.  g_mesh_variant selects, per
+ * deviation, brax's form (oracle/brax_mesh_study.py measures each one's effect on a step);
+ * the restatement adopts all three (the default):
+ *   MV_EPS_NORMAL  normal = (S - P) / (1e-6 + dist)  (capsule_mesh), so a touching or
+ *                  piercing segment (S == P) gives the zero normal, a nearly touching one a
+ *                  short normal (the exact form: the unit normal, the face's outward normal
+ *                  at S == P).  dist = |S - P| (capsule_mesh's jp.safe_norm(penetration_vec,
+ *                  axis=1) tests jnp.allclose over all twelve triangles at once, which a box
+ *                  never meets: the plain norm)
+ *   MV_POS_TRI     the contact position is the triangle point P = S - (1e-6 + dist) n
+ *                  (capsule_mesh: pos = triangle_p; the exact form: the capsule's surface point
+ *                  S - r n)
+ *   MV_FORM        the closest points by brax's _closest_segment_triangle_points: three
+ *                  segment-segment pairs (_closest_segment_to_segment_points: directions
+ *                  d / (len + 1e-6), mid-point parameters, the (denom + 1e-6) line solution,
+ *                  both clipped, then each re-projected onto the other segment by
+ *                  _closest_segment_point with (d.d + 1e-6)), the segment-plane point
+ *                  (_closest_segment_point_plane: (d - n.a) / (n.(b - a) + 1e-6), clipped) and
+ *                  its barycentric closest triangle point (_closest_triangle_point), the
+ *                  minimum of the four squared distances, ties averaged.
+ * Frames and shared terms: the capsule's segment quantities (length, direction, mid point,
+ * 1 / (d.d + 1e-6)) are formed once per wall in the wall frame (x, y, z order) and permuted
+ * into face coordinates; a face's edges are exact constants of its half extents.  Triangles
+ * (p0, p1, p2): t0 = (V0, V1, V2), t1 = (V0, V2, V3) of the face rectangle V0 = (-ha, -hb),
+ * V1 = (ha, -hb), V2 = (ha, hb), V3 = (-ha, hb) (the restatement's triangulation; brax's
+ * TriangulatedBox vertex order is not recoverable here).  Divisions are a * (1 / b) (the
+ * spec's rule; brax divides: <= 1 ulp apart). */
+#define MV_EPS_NORMAL 1
+#define MV_POS_TRI 4
+#define MV_FORM 8
+#define MV_BRAX (MV_EPS_NORMAL | MV_POS_TRI | MV_FORM)
+static int g_mesh_variant = 0;
+void orc_set_mesh_variant(int v) { g_mesh_variant = v; }
+int orc_get_mesh_variant(void) { return g_mesh_variant; }
+
+static inline f3 F3(float a, float b, float w) { f3 r = {a, b, w}; return r; }
+static inline f3 f3sub(f3 x, f3 y) { FL(3); return F3(x.a - y.a, x.b - y.b, x.w - y.w); }
+static inline float f3dot(f3 x, f3 y) { FL(5); return fmaf(x.w, y.w, fmaf(x.b, y.b, x.a * y.a)); }
+/* p + d s, fused per component */
+static inline f3 f3fma(f3 d, float s, f3 p) { FL(6); return F3(fmaf(d.a, s, p.a), fmaf(d.b, s, p.b), fmaf(d.w, s, p.w)); }
+static inline float bdist2(f3 x, f3 y) { const f3 d = f3sub(x, y); return f3dot(d, d); }
+
+/* a segment p0 -> p0 + d with brax's derived quantities: len = jp.safe_norm(d) (0 when every
+ * |d_i| <= 1e-8), il = 1 / (len + 1e-6), dir = d il, hl = len 0.5, mid = p0 + dir hl,
+ * idd = 1 / (d.d + 1e-6) */
+typedef struct { f3 p0, d, dir, mid; float hl, il, idd; } bseg_t;
+static bseg_t bseg_make(f3 p0, f3 d) {
+  bseg_t s;
+  s.p0 = p0; s.d = d;
+  const float dd = f3dot(d, d);
+  FL(1 + 2 + 3 + 1 + 2);
+  const float len = (fabsf(d.a) <= 1e-8f && fabsf(d.b) <= 1e-8f && fabsf(d.w) <= 1e-8f) ? 0.0f : sqrtf(dd);
+  s.il = 1.0f / (len + 1e-6f);
+  s.dir = F3(d.a * s.il, d.b * s.il, d.w * s.il);
+  s.hl = len * 0.5f;
+  s.mid = f3fma(s.dir, s.hl, p0);
+  s.idd = 1.0f / (dd + 1e-6f);
+  return s;
+}
+/* wall-frame (x, y, z) -> face coordinates (a, b, w) of axis k */
+static inline f3 fperm(f3 v, int k) { return k == 0 ? F3(v.b, v.w, v.a) : (k == 1 ? F3(v.a, v.w, v.b) : v); }
+static inline bseg_t bseg_perm(const bseg_t *s, int k) {
+  bseg_t r = *s;
+  r.p0 = fperm(s->p0, k); r.d = fperm(s->d, k); r.dir = fperm(s->dir, k); r.mid = fperm(s->mid, k);
+  return r;
+}
+/* _closest_segment_point(p0, p0 + d, pt): t = clip((pt - p0).d / (d.d + 1e-6), 0, 1) */
+static inline f3 bseg_point(const bseg_t *s, f3 pt, float *tp) {
+  FL(1);
+  const float t = clamp01(f3dot(f3sub(pt, s->p0), s->d) * s->idd);
+  *tp = t;
+  return f3fma(s->d, t, s->p0);
+}
+/* _closest_segment_to_segment_points(A, E) -> (best_a, best_b); *u = best_a's parameter on A */
+static float bseg_seg(const bseg_t *A, const bseg_t *E, f3 *pa, f3 *pb, float *u) {
+  const f3 trans = f3sub(A->mid, E->mid);
+  const float dd = f3dot(A->dir, E->dir), dat = f3dot(A->dir, trans), dbt = f3dot(E->dir, trans);
+  FL(2 + 1 + 3 + 2 + 4 + 2);
+  const float denom = fmaf(-dd, dd, 1.0f);
+  const float ota = fmaf(dd, dbt, -dat) * (1.0f / (denom + 1e-6f));
+  const float otb = fmaf(ota, dd, dbt);
+  const float ta = fminf(fmaxf(ota, -A->hl), A->hl), tb = fminf(fmaxf(otb, -E->hl), E->hl);
+  f3 best_a = f3fma(A->dir, ta, A->mid), best_b = f3fma(E->dir, tb, E->mid);
+  float s1, s2;
+  const f3 new_a = bseg_point(A, best_b, &s1);
+  const float d1 = bdist2(best_b, new_a);
+  const f3 new_b = bseg_point(E, best_a, &s2);
+  const float d2 = bdist2(best_a, new_b);
+  float ua = (A->hl + ta) * A->il;
+  if (d1 < d2) { best_a = new_a; ua = s1; }
+  else best_b = new_b;
+  *pa = best_a; *pb = best_b; *u = ua;
+  return bdist2(best_a, best_b);
+}
+/* _closest_triangle_point(p0, p0 + e0, p0 + e1, pt): barycentric (u, v) with the triangle's
+ * constants a = e0.e0, b = e0.e1, c = e1.e1, idet = 1 / (a c - b b); else the edges' closest
+ * points (p0 p1, p1 p2, p2 p0 given as segments) */
+typedef struct { f3 p0, e0, e1; float a, b, c, idet; bseg_t s01, s12, s20; } btri_t;
+static f3 btri_point(const btri_t *T, f3 pt) {
+  const f3 d = f3sub(pt, T->p0);
+  const float e0d = f3dot(T->e0, d), e1d = f3dot(T->e1, d);
+  FL(3 + 3 + 1);
+  const float u = fmaf(T->c, e0d, -(T->b * e1d)) * T->idet, v = fmaf(T->a, e1d, -(T->b * e0d)) * T->idet;
+  const int inside = 0.0f <= u && u <= 1.0f && 0.0f <= v && v <= 1.0f && u + v <= 1.0f;
+  f3 cp = f3fma(T->e1, v, f3fma(T->e0, u, T->p0));
+  const float d0 = bdist2(cp, pt);
+  float t;
+  const f3 c1 = bseg_point(&T->s01, pt, &t);
+  const float d1 = bdist2(pt, c1);
+  float md = d0;
+  if (!(d0 < d1 && inside)) { cp = c1; md = d1; }
+  const f3 c2 = bseg_point(&T->s12, pt, &t);
+  const float d2 = bdist2(pt, c2);
+  FL(2);
+  if (d2 < md) cp = c2;
+  md = fminf(md, d2);
+  const f3 c3 = bseg_point(&T->s20, pt, &t);
+  const float d3 = bdist2(pt, c3);
+  if (d3 < md) cp = c3;
+  return cp;
+}
+static btri_t btri_make(f3 p0, f3 p1, f3 p2) {
+  btri_t T;
+  T.p0 = p0; T.e0 = f3sub(p1, p0); T.e1 = f3sub(p2, p0);
+  T.a = f3dot(T.e0, T.e0); T.b = f3dot(T.e0, T.e1); T.c = f3dot(T.e1, T.e1);
+  FL(3 + 1);
+  T.idet = 1.0f / fmaf(T.a, T.c, -(T.b * T.b));
+  T.s01 = bseg_make(p0, f3sub(p1, p0)); T.s12 = bseg_make(p1, f3sub(p2, p1)); T.s20 = bseg_make(p2, f3sub(p0, p2));
+  return T;
+}
+/* the minimum of the four squared distances, ties averaged (jp.amin, mask, sum / sum(mask)); a
+ * triangle whose distances are all NaN has no candidate (d2 = +inf: the exact form's rule) */
+static cand_t bpick(const f3 sp[4], const f3 tp[4], const float u[4], const float d2[4]) {
+  FL(3);
+  const float mn = fminf(fminf(d2[0], d2[1]), fminf(d2[2], d2[3]));
+  f3 S = F3(0.0f, 0.0f, 0.0f), P = S;
+  float us = 0.0f, cnt = 0.0f;
+  int first = -1;
+  for (int k = 0; k < 4; ++k)
+    if (d2[k] == mn) {
+      if (first < 0) first = k;
+      FL(7);
+      S = F3(S.a + sp[k].a, S.b + sp[k].b, S.w + sp[k].w);
+      P = F3(P.a + tp[k].a, P.b + tp[k].b, P.w + tp[k].w);
+      us += u[k]; cnt += 1.0f;
+    }
+  cand_t c; c.d2 = INFINITY; c.u = 0.0f; c.d.a = c.d.b = c.d.w = 0.0f;
+  if (first < 0) return c;
+  if (cnt > 1.0f) {
+    FL(7);
+    S = F3(S.a / cnt, S.b / cnt, S.w / cnt); P = F3(P.a / cnt, P.b / cnt, P.w / cnt); us /= cnt;
+    c.d = f3sub(S, P); c.d2 = f3dot(c.d, c.d);
+  } else {
+    c.d = f3sub(sp[first], tp[first]); c.d2 = d2[first];
+  }
+  c.u = us;
+  return c;
+}
+/* both triangles of face (axis k, outward sign sg, plane w = w0, half extents ha, hb) against
+ * the capsule segment A (face coordinates): _closest_segment_triangle_points per triangle */
+static void bface(float ha, float hb, float w0, float sg, const bseg_t *A, cand_t c[2]) {
+  const f3 V0 = F3(-ha, -hb, w0), V1 = F3(ha, -hb, w0), V2 = F3(ha, hb, w0), V3 = F3(-ha, hb, w0);
+  /* the segment-plane point (both triangles: p0 = V0, n = (0, 0, sg); n's zero products drop
+   * out exactly) */
+  FL(1 + 1 + 1 + 1 + 2);
+  const float tt = clamp01((sg * w0 - sg * A->p0.w) * (1.0f / (sg * A->d.w + 1e-6f)));
+  const f3 sp4 = f3fma(A->d, tt, A->p0);
+  /* the edges as segments: t0 (V0 V1), (V1 V2), (V0 V2); t1 (V0 V2), (V2 V3), (V0 V3) */
+  const bseg_t E01 = bseg_make(V0, f3sub(V1, V0)), E12 = bseg_make(V1, f3sub(V2, V1));
+  const bseg_t E02 = bseg_make(V0, f3sub(V2, V0)), E23 = bseg_make(V2, f3sub(V3, V2));
+  const bseg_t E03 = bseg_make(V0, f3sub(V3, V0));
+  f3 sp[4], tp[4];
+  float u[4], d2[4];
+  f3 sdg, tdg;
+  float udg;
+  const float ddg = bseg_seg(A, &E02, &sdg, &tdg, &udg);
+  for (int t = 0; t < 2; ++t) {
+    if (t == 0) {
+      d2[0] = bseg_seg(A, &E01, &sp[0], &tp[0], &u[0]);
+      d2[1] = bseg_seg(A, &E12, &sp[1], &tp[1], &u[1]);
+      sp[2] = sdg; tp[2] = tdg; u[2] = udg; d2[2] = ddg;
+    } else {
+      sp[0] = sdg; tp[0] = tdg; u[0] = udg; d2[0] = ddg;
+      d2[1] = bseg_seg(A, &E23, &sp[1], &tp[1], &u[1]);
+      d2[2] = bseg_seg(A, &E03, &sp[2], &tp[2], &u[2]);
+    }
+    const btri_t T = t == 0 ? btri_make(V0, V1, V2) : btri_make(V0, V2, V3);
+    sp[3] = sp4; u[3] = tt;
+    tp[3] = btri_point(&T, sp4);
+    d2[3] = bdist2(sp4, tp[3]);
+    c[t] = bpick(sp, tp, u, d2);
+  }
+}
+
 /* component k of the wall-local vector (x, y, z) */
 static inline float comp(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
@@ -781,6 +977,10 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
   v3 Lb = La;
   if (seg) { const v3 db = vsub(pb, e->wall_c[w]); Lb = V(fmaf(db.y, s, db.x * c), fmaf(db.y, c, -(db.x * s)), db.z); }
   const float R = r + WALL_CULL_MARGIN;
+  const int mv = g_mesh_variant;
+  /* brax form: the capsule's segment quantities once per wall, in the wall frame (x, y, z) */
+  bseg_t capw;
+  if (mv & MV_FORM) capw = bseg_make(F3(La.x, La.y, La.z), f3sub(F3(Lb.x, Lb.y, Lb.z), F3(La.x, La.y, La.z)));
   CST(0, 1);
   int n_hit = 0;
   for (int f = 0; f < 6; ++f) {
@@ -802,28 +1002,42 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
       if (gw >= R || ga >= R || gb >= R) continue;
     }
     CST(1, 1);
-    f3 D = {0.0f, 0.0f, 0.0f};
-    float aa = 0.0f, inv_aa = 0.0f;
-    if (seg) {
-      FL(3 + 5 + 1);
-      D.a = B.a - A.a; D.b = B.b - A.b; D.w = B.w - A.w;
-      aa = fmaf(D.w, D.w, fmaf(D.b, D.b, D.a * D.a));
-      inv_aa = 1.0f / aa;
+    cand_t cds[2];
+    if (mv & MV_FORM) {
+      const bseg_t capf = bseg_perm(&capw, k);
+      bface(ha, hb, w0, sg, &capf, cds);
+    } else {
+      f3 D = {0.0f, 0.0f, 0.0f};
+      float aa = 0.0f, inv_aa = 0.0f;
+      if (seg) {
+        FL(3 + 5 + 1);
+        D.a = B.a - A.a; D.b = B.b - A.b; D.w = B.w - A.w;
+        aa = fmaf(D.w, D.w, fmaf(D.b, D.b, D.a * D.a));
+        inv_aa = 1.0f / aa;
+      }
+      for (int t = 0; t < 2; ++t) cds[t] = seg_tri(t, ha, hb, w0, A, B, seg, D, aa, inv_aa);
     }
     for (int t = 0; t < 2; ++t) {
-      const cand_t cd = seg_tri(t, ha, hb, w0, A, B, seg, D, aa, inv_aa);
+      const cand_t cd = cds[t];
       FL(1);
       const float dist = sqrtf(cd.d2);
       const float pen = r - dist;
       if (!(pen > 0.0f)) continue;
       f3 nf;
-      if (cd.d2 > 0.0f) { FL(4); const float inv = 1.0f / dist; nf.a = cd.d.a * inv; nf.b = cd.d.b * inv; nf.w = cd.d.w * inv; }
-      else { nf.a = 0.0f; nf.b = 0.0f; nf.w = sg; CST(6, 1); }
+      float cdist; /* |S - P| + 1e-6 (or |S - P|): the contact position's offset from S along -n */
+      if (mv & MV_EPS_NORMAL) {
+        FL(5);
+        cdist = 1e-6f + dist;
+        const float inv = 1.0f / cdist;
+        nf.a = cd.d.a * inv; nf.b = cd.d.b * inv; nf.w = cd.d.w * inv;
+        if (!(cd.d2 > 0.0f)) CST(6, 1);
+      } else if (cd.d2 > 0.0f) { FL(4); cdist = dist; const float inv = 1.0f / dist; nf.a = cd.d.a * inv; nf.b = cd.d.b * inv; nf.w = cd.d.w * inv; }
+      else { cdist = 0.0f; nf.a = 0.0f; nf.b = 0.0f; nf.w = sg; CST(6, 1); }
       /* back to wall-local (x, y, z), then to the world */
       float nl[3]; nl[ka] = nf.a; nl[kb] = nf.b; nl[k] = nf.w;
       FL(6 + 1);
       const int m = ct->count++;
-      ct->body[m] = i; ct->ground[m] = 0; ct->pen[m] = pen; ct->r[m] = r;
+      ct->body[m] = i; ct->ground[m] = 0; ct->pen[m] = pen; ct->r[m] = (mv & MV_POS_TRI) ? cdist : r;
       ct->tau[m] = 1.0f - 2.0f * cd.u;
       ct->n[m] = V(fmaf(-nl[1], s, nl[0] * c), fmaf(nl[1], c, nl[0] * s), nl[2]);
       ct->e[m] = V(0.0f, 0.0f, 0.0f);
@@ -841,8 +1055,9 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
 
 /* Test hook (tests/test_contact_mesh.py): the mesh contacts of one capsule against one wall
  * box.  wall = (cx, cy, cz, cos, sin, hx, hy, hz), the capsule's world end points a, b (seg = 0:
- * the sphere at a) and radius r; out[5 k ..] = (tau, nx, ny, nz, pen) of contact k in
- * (face, triangle) order; returns the count (<= 12). */
+ * the sphere at a) and radius r; out[6 k ..] = (tau, nx, ny, nz, pen, cd) of contact k in
+ * (face, triangle) order, cd = the contact position's offset from the segment point along -n;
+ * returns the count (<= 12). */
 int orc_mesh_contacts(const float *wall, const float *a, const float *b, int seg, float r, float *out) {
   orc_env *e = (orc_env *)calloc(1, sizeof(orc_env));
   e->n_walls = 1;
@@ -854,8 +1069,8 @@ int orc_mesh_contacts(const float *wall, const float *a, const float *b, int seg
   ct->count = 0;
   capsule_wall_mesh(e, 0, 0, V(a[0], a[1], a[2]), V(b[0], b[1], b[2]), ct);
   for (int k = 0; k < ct->count; ++k) {
-    out[5 * k] = ct->tau[k]; out[5 * k + 1] = ct->n[k].x; out[5 * k + 2] = ct->n[k].y;
-    out[5 * k + 3] = ct->n[k].z; out[5 * k + 4] = ct->pen[k];
+    out[6 * k] = ct->tau[k]; out[6 * k + 1] = ct->n[k].x; out[6 * k + 2] = ct->n[k].y;
+    out[6 * k + 3] = ct->n[k].z; out[6 * k + 4] = ct->pen[k]; out[6 * k + 5] = ct->r[k];
   }
   const int n = ct->count;
   free(ct); free(e);

@@ -89,11 +89,15 @@ int orc_flops_set_mode(int mode);
 void orc_contact_stats(long long out[16]);
 void orc_contact_stats_enable(int on);
 /* test hook: mesh contacts of one capsule (world end points a, b; seg 0 = sphere at a, radius r)
- * against one wall box (cx, cy, cz, cos, sin, hx, hy, hz): out (tau, nx, ny, nz, pen) x count */
+ * against one wall box (cx, cy, cz, cos, sin, hx, hy, hz): out (tau, nx, ny, nz, pen, cd) x count */
 int orc_mesh_contacts(const float *wall, const float *a, const float *b, int seg, float r, float *out);
 /* 0: evaluate every face of every wall (no face cull; the FLOP counter's reference mode does
  * this too) -- results must be identical to the default (1) */
 void orc_set_face_cull(int on);
+/* capsule x TriangulatedBox spelling: bit 1 eps-regularised normal, 2 safe_norm, 4 contact at the
+ * triangle point, 8 brax's closest-point forms (pob_oracle.c MV_*) */
+void orc_set_mesh_variant(int v);
+int orc_get_mesh_variant(void);
 /* test hook: op 0 atan2f(a, b); op 1 substep quaternion normalisation of a (n x 4) */
 void orc_math_check(int op, int n, const float *a, const float *b, float *out);
 
