@@ -798,7 +798,7 @@ static cand_t seg_tri(int t, float ha, float hb, float w0, f3 A, f3 B, int seg, 
 #define MV_POS_TRI 4
 #define MV_FORM 8
 #define MV_BRAX (MV_EPS_NORMAL | MV_POS_TRI | MV_FORM)
-static int g_mesh_variant = 0;
+static int g_mesh_variant = MV_BRAX;
 void orc_set_mesh_variant(int v) { g_mesh_variant = v; }
 int orc_get_mesh_variant(void) { return g_mesh_variant; }
 
@@ -808,6 +808,10 @@ static inline float f3dot(f3 x, f3 y) { FL(5); return fmaf(x.w, y.w, fmaf(x.b, y
 /* p + d s, fused per component */
 static inline f3 f3fma(f3 d, float s, f3 p) { FL(6); return F3(fmaf(d.a, s, p.a), fmaf(d.b, s, p.b), fmaf(d.w, s, p.w)); }
 static inline float bdist2(f3 x, f3 y) { const f3 d = f3sub(x, y); return f3dot(d, d); }
+/* jp.clip as selects (the same bits on every target, -0 and NaN included: NaN clips to the
+ * lower bound, -0 to +0 / -h) */
+static inline float bclamp01(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+static inline float bclamps(float x, float h) { return x > -h ? (x < h ? x : h) : -h; }
 
 /* a segment p0 -> p0 + d with brax's derived quantities: len = jp.safe_norm(d) (0 when every
  * |d_i| <= 1e-8), il = 1 / (len + 1e-6), dir = d il, hl = len 0.5, mid = p0 + dir hl,
@@ -836,7 +840,7 @@ static inline bseg_t bseg_perm(const bseg_t *s, int k) {
 /* _closest_segment_point(p0, p0 + d, pt): t = clip((pt - p0).d / (d.d + 1e-6), 0, 1) */
 static inline f3 bseg_point(const bseg_t *s, f3 pt, float *tp) {
   FL(1);
-  const float t = clamp01(f3dot(f3sub(pt, s->p0), s->d) * s->idd);
+  const float t = bclamp01(f3dot(f3sub(pt, s->p0), s->d) * s->idd);
   *tp = t;
   return f3fma(s->d, t, s->p0);
 }
@@ -848,7 +852,7 @@ static float bseg_seg(const bseg_t *A, const bseg_t *E, f3 *pa, f3 *pb, float *u
   const float denom = fmaf(-dd, dd, 1.0f);
   const float ota = fmaf(dd, dbt, -dat) * (1.0f / (denom + 1e-6f));
   const float otb = fmaf(ota, dd, dbt);
-  const float ta = fminf(fmaxf(ota, -A->hl), A->hl), tb = fminf(fmaxf(otb, -E->hl), E->hl);
+  const float ta = bclamps(ota, A->hl), tb = bclamps(otb, E->hl);
   f3 best_a = f3fma(A->dir, ta, A->mid), best_b = f3fma(E->dir, tb, E->mid);
   float s1, s2;
   const f3 new_a = bseg_point(A, best_b, &s1);
@@ -932,7 +936,7 @@ static void bface(float ha, float hb, float w0, float sg, const bseg_t *A, cand_
   /* the segment-plane point (both triangles: p0 = V0, n = (0, 0, sg); n's zero products drop
    * out exactly) */
   FL(1 + 1 + 1 + 1 + 2);
-  const float tt = clamp01((sg * w0 - sg * A->p0.w) * (1.0f / (sg * A->d.w + 1e-6f)));
+  const float tt = bclamp01((sg * w0 - sg * A->p0.w) * (1.0f / (sg * A->d.w + 1e-6f)));
   const f3 sp4 = f3fma(A->d, tt, A->p0);
   /* the edges as segments: t0 (V0 V1), (V1 V2), (V0 V2); t1 (V0 V2), (V2 V3), (V0 V3) */
   const bseg_t E01 = bseg_make(V0, f3sub(V1, V0)), E12 = bseg_make(V1, f3sub(V2, V1));

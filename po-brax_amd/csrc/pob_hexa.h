@@ -140,12 +140,13 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   uint64_t Ms[1] = {M};
   mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
-                    [&](const int, const int bit, const float tau, const v3 n, const float pen) {
-    owall_position(g, SC, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.q, pq, px, DX, DA);
+                    [&](const int, const int bit, const float tau, const v3 n, const float dist) {
+    // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
+    owall_position(g, SC, HT[HT_R] - dist, vfma(rv, tau, b.x), n, 1e-6f + dist, im, b.x, b.q, pq, px, DX, DA);
     ms.mc |= 1ull << bit;
     if (ms.nct < HMAXC) {
       float *c = CS + 64 * 5 * ms.nct;
-      c[0] = tau; c[64] = n.x; c[128] = n.y; c[192] = n.z; c[256] = pen;
+      c[0] = tau; c[64] = n.x; c[128] = n.y; c[192] = n.z; c[256] = dist;
     }
     ++ms.nct;
   });
@@ -167,16 +168,16 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
     if (!__any(i < n)) break;
     if (i < n) {
       const float *c = CS + 64 * 5 * i;
-      ocontact_vel_pe(g, SC, false, c[256], vfma(rv, c[0], b.x), V(c[64], c[128], c[192]), HT[HT_R], im, b.x, b.v, b.w,
-                      dV, dW);
+      ocontact_vel_pe(g, SC, false, HT[HT_R] - c[256], vfma(rv, c[0], b.x), V(c[64], c[128], c[192]), 1e-6f + c[256], im,
+                      b.x, b.v, b.w, dV, dW);
     }
   }
   if (!__any(ovf)) return;
   uint64_t Ms[1] = {ovf ? ms.mc : 0ull};
   mesh_wave_walk<1>(g, WT, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
-                    [&](const int, const int, const float tau, const v3 n, const float pen) {
-    ocontact_vel_pe(g, SC, false, pen, vfma(rv, tau, b.x), n, HT[HT_R], im, b.x, b.v, b.w, dV, dW);
+                    [&](const int, const int, const float tau, const v3 n, const float dist) {
+    ocontact_vel_pe(g, SC, false, HT[HT_R] - dist, vfma(rv, tau, b.x), n, 1e-6f + dist, im, b.x, b.v, b.w, dV, dW);
   });
 }
 

@@ -261,6 +261,7 @@ POB_D float pob_atan2f_g(G &g, float y, float x) {
 // kernels' basic blocks; the accumulator is one or two VALU operations off the chain.
 struct GuardBranch {
   POB_D float rcp(float x) { return pob_rcp(x); }
+  POB_D float sqrt(float x) { return pob_sqrt(x); }
   POB_D void sqrt_rcp(float x, float &s, float &i) { pob_sqrt_rcp(x, s, i); }
   POB_D q4 qnorm(q4 q) { return qnormalize(q); }
 };
@@ -272,6 +273,7 @@ struct GuardAcc {
   }
   POB_D bool bad() const { return m > 0xC0000000u; }
   POB_D float rcp(float x) { note(x); return pob_rcp_fast(x); }
+  POB_D float sqrt(float x) { note(x); return pob_sqrt_fast(x); }
   POB_D void sqrt_rcp(float x, float &s, float &i) {
     note(x);
     s = pob_sqrt_fast(x);

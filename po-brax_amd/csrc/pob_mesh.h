@@ -3,9 +3,10 @@
 //
 // Every arena wall is a box collider of the frozen Arena body (po_brax/envs/utils.py:6-28,
 // add_box_wall_to_body; ant x Arena in collide_include, ant_heavenhell.py:33-34).  brax v1
-// meshes a box into 12 triangles and, for every triangle, takes the closest points of the
-// capsule's segment and the triangle; a triangle closer than the capsule radius is one contact
-// (penetration r - |S - P|, normal along S - P), and every such contact is applied.  The
+// meshes a box into 12 triangles and, for every triangle, takes the closest points S (on the
+// capsule's segment) and P (on the triangle) by _closest_segment_triangle_points; a triangle
+// with |S - P| below the capsule radius is one contact (penetration r - |S - P|, normal
+// (S - P) / (1e-6 + |S - P|), position P), and every such contact is applied.  The
 // computation runs in the wall's frame (world -> R_z(-theta)(p - c)); a face is the plane
 // w = sigma h_k of axis k with face coordinates (a, b, w) = (y, z, x) / (x, z, y) / (x, y, z)
 // for k = x / y / z, its rectangle split along the diagonal (-ha, -hb) -> (ha, hb).
@@ -64,194 +65,352 @@ POB_D uint32_t mesh_face_mask(const v3 A, const v3 B, const float hx, const floa
   return m;
 }
 
-POB_D float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
+// ---------------------------------------------------------------- brax's closest-point forms
+// brax v1's _closest_segment_triangle_points and capsule_mesh as the restatement spells them
+// (oracle/pob_oracle.c bseg_make / bseg_seg / btri_point / bpick / bface): three
+// segment-segment pairs, the segment-plane point with its closest triangle point, the minimum
+// of the four squared distances (ties averaged), the normal (S - P) / (1e-6 + |S - P|), the
+// contact at the triangle point.  The same operations on the same operands as the oracle;
+// jp.clip as selects (bclamp01 / bclamps: the same bits for -0 and NaN on both sides).
+POB_D float bclamp01(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+POB_D float bclamps(float x, float h) { return x > -h ? (x < h ? x : h) : -h; }
 
-// is (pa, pb) in face triangle t (boundary included)?  (oracle tri_inside)
-POB_D bool mtri_inside(const bool t1, const float ha, const float hb, const float pa, const float pb) {
-  const float cr = FMA(pa + ha, hb, -((pb + hb) * ha));
-  return t1 ? ((pb <= hb) & (pa >= -ha) & (cr <= 0.0f)) : ((pb >= -hb) & (pa <= ha) & (cr >= 0.0f));
+struct F3 {
+  float a, b, w;  // face coordinates (a, b in the face plane, w along its normal)
+};
+POB_D F3 f3(const float a, const float b, const float w) { F3 r; r.a = a; r.b = b; r.w = w; return r; }
+POB_D F3 f3sub(const F3 x, const F3 y) { return f3(x.a - y.a, x.b - y.b, x.w - y.w); }
+POB_D float f3dot(const F3 x, const F3 y) { return FMA(x.w, y.w, FMA(x.b, y.b, x.a * y.a)); }
+POB_D F3 f3fma(const F3 d, const float s, const F3 p) { return f3(FMA(d.a, s, p.a), FMA(d.b, s, p.b), FMA(d.w, s, p.w)); }
+POB_D float f3d2(const F3 x, const F3 y) { const F3 d = f3sub(x, y); return f3dot(d, d); }
+POB_D F3 f3sel(const bool c, const F3 x, const F3 y) { return f3(c ? x.a : y.a, c ? x.b : y.b, c ? x.w : y.w); }
+// wall frame (x, y, z) -> face coordinates of axis k: (y, z, x) / (x, z, y) / (x, y, z)
+POB_D F3 fperm(const F3 v, const int k) {
+  return f3(k == 0 ? v.b : v.a, k == 2 ? v.b : v.w, k == 0 ? v.a : (k == 1 ? v.b : v.w));
 }
 
-// mtri_closest for both triangles of the face at once (mesh_face): the inside tests share the
-// diagonal's cross term, the edge points their clamps and the diagonal's closest point -- the
-// same operations on the same operands as two mtri_closest calls, each computed once
-POB_D void mtri_closest2(const float ha, const float hb, const float ha2, const float hb2, const float inv_dd,
-                         const float pa, const float pb, float &qa0, float &qb0, float &qa1, float &qb1) {
-  const float cr = FMA(pa + ha, hb, -((pb + hb) * ha));
-  const bool in0 = (pb >= -hb) & (pa <= ha) & (cr >= 0.0f);
-  const bool in1 = (pb <= hb) & (pa >= -ha) & (cr <= 0.0f);
-  const float s = clamp01(FMA(pb + hb, hb2, (pa + ha) * ha2) * inv_dd);
-  const float s2 = 2.0f * s;
-  const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
-  const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
-  // squared distances to the edge points: bottom (ca, -hb), right (ha, cb), diagonal (da, db),
-  // top (ca, hb), left (-ha, cb)
-  const float gc = pa - ca, gd = pa - da, gr = pa - ha, gl = pa - -ha;
-  const float hbt = pb - -hb, hd = pb - db, hcb = pb - cb, htp = pb - hb;
-  const float dbot = FMA(hbt, hbt, gc * gc), drt = FMA(hcb, hcb, gr * gr), ddg = FMA(hd, hd, gd * gd);
-  const float dtop = FMA(htp, htp, gc * gc), dlf = FMA(hcb, hcb, gl * gl);
-  // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (first strict minimum)
-  float b0 = dbot, a0 = ca, c0 = -hb;
-  if (drt < b0) { b0 = drt; a0 = ha; c0 = cb; }
-  if (ddg < b0) { a0 = da; c0 = db; }
-  float b1 = ddg, a1 = da, c1 = db;
-  if (dtop < b1) { b1 = dtop; a1 = ca; c1 = hb; }
-  if (dlf < b1) { a1 = -ha; c1 = cb; }
-  qa0 = in0 ? pa : a0; qb0 = in0 ? pb : c0;
-  qa1 = in1 ? pa : a1; qb1 = in1 ? pb : c1;
+// a segment p0 -> p0 + d with brax's derived quantities: len = safe_norm(d), il = 1 / (len +
+// 1e-6), dir = d il, hl = len 0.5, mid = p0 + dir hl, idd = 1 / (d.d + 1e-6)
+struct BSeg {
+  F3 p0, d, dir, mid;
+  float hl, il, idd;
+};
+template <class G>
+POB_D BSeg bseg_make(G &g, const F3 p0, const F3 d) {
+  BSeg s;
+  s.p0 = p0;
+  s.d = d;
+  const float dd = f3dot(d, d);
+  const bool z = (int)(fabsf(d.a) <= 1e-8f) & (int)(fabsf(d.b) <= 1e-8f) & (int)(fabsf(d.w) <= 1e-8f);
+  const float len = z ? 0.0f : g.sqrt(z ? 1.0f : dd);
+  s.il = g.rcp(len + 1e-6f);
+  s.dir = f3(d.a * s.il, d.b * s.il, d.w * s.il);
+  s.hl = len * 0.5f;
+  s.mid = f3fma(s.dir, s.hl, p0);
+  s.idd = g.rcp(dd + 1e-6f);
+  return s;
 }
-
-// running closest candidate: squared distance, segment parameter, S - P (face coordinates)
+POB_D BSeg bseg_perm(const BSeg &s, const int k) {
+  BSeg r = s;
+  r.p0 = fperm(s.p0, k); r.d = fperm(s.d, k); r.dir = fperm(s.dir, k); r.mid = fperm(s.mid, k);
+  return r;
+}
+// _closest_segment_point(p0, p0 + d, pt)
+POB_D F3 bseg_point(const BSeg &s, const F3 pt, float &t) {
+  t = bclamp01(f3dot(f3sub(pt, s.p0), s.d) * s.idd);
+  return f3fma(s.d, t, s.p0);
+}
+// _closest_segment_to_segment_points(A, E): S on A (parameter u), P on E; returns |S - P|^2
+// and S - P (the candidate's fields)
 struct MCand {
   float d2, u, da, db, dw;
 };
-POB_D void mcand_take(MCand &c, const float u, const float da, const float db, const float dw) {
-  const float d2 = FMA(dw, dw, FMA(db, db, da * da));
-  if (d2 < c.d2) { c.d2 = d2; c.u = u; c.da = da; c.db = db; c.dw = dw; }
-}
-
-// closest point of face triangle t to the plane point (pa, pb) (oracle tri_closest): the point
-// if inside, else the first strict minimum over the triangle's edges' nearest points;
-// the diagonal D = (2ha, 2hb), inv_dd = 1 / (D . D)
-POB_D void mtri_closest(const bool t1, const float ha, const float hb, const float ha2, const float hb2,
-                        const float inv_dd, const float pa, const float pb, float &qa, float &qb) {
-  if (mtri_inside(t1, ha, hb, pa, pb)) { qa = pa; qb = pb; return; }
-  const float s = clamp01(FMA(pb + hb, hb2, (pa + ha) * ha2) * inv_dd);
-  const float s2 = 2.0f * s;
-  const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
-  const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
-  // triangle 0: bottom (ca, -hb), right (ha, cb), diagonal; triangle 1: diagonal, top (ca, hb), left (-ha, cb)
-  const float e0a = t1 ? da : ca, e0b = t1 ? db : -hb;
-  const float e1a = t1 ? ca : ha, e1b = t1 ? hb : cb;
-  const float e2a = t1 ? -ha : da, e2b = t1 ? cb : db;
-  float g0 = pa - e0a, h0 = pb - e0b;
-  float best = FMA(h0, h0, g0 * g0);
-  qa = e0a; qb = e0b;
-  const float g1 = pa - e1a, h1 = pb - e1b;
-  const float d1 = FMA(h1, h1, g1 * g1);
-  if (d1 < best) { best = d1; qa = e1a; qb = e1b; }
-  const float g2 = pa - e2a, h2 = pb - e2b;
-  const float d2 = FMA(h2, h2, g2 * g2);
-  if (d2 < best) { qa = e2a; qb = e2b; }
-}
-
-// closest points of the segment A + u D and the edge E0 + t F (in the face plane w = w0):
-// the oracle's seg_edge (Ericson's clamped form) as a candidate update
-struct MSeg {
-  float aa_, ab, aw, Da, Db, Dw, aa, inv_aa;  // A (face coordinates), D = B - A, D . D, 1 / D . D
-};
 template <class G>
-POB_D void mseg_edge(G &g, MCand &c, const MSeg &S, const float e0a, const float e0b, const float w0, const float fa,
-                     const float fb, const float ee, const float inv_ee) {
-  const float ra = S.aa_ - e0a, rb = S.ab - e0b, rw = S.aw - w0;
-  const float f = FMA(fb, rb, fa * ra);
-  const float cc = FMA(S.Dw, rw, FMA(S.Db, rb, S.Da * ra));
-  const float bb = FMA(S.Db, fb, S.Da * fa);
-  const float den = FMA(S.aa, ee, -(bb * bb));
-  float u = 0.0f;
-  if (den > 0.0f) u = clamp01(FMA(bb, f, -(cc * ee)) * g.rcp(den));
-  float t = FMA(bb, u, f) * inv_ee;
-  if (t < 0.0f) { t = 0.0f; u = clamp01(-cc * S.inv_aa); }
-  else if (t > 1.0f) { t = 1.0f; u = clamp01((bb - cc) * S.inv_aa); }
-  const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
-  mcand_take(c, u, sa - FMA(t, fa, e0a), sb - FMA(t, fb, e0b), sw - w0);
+POB_D void bseg_seg(G &g, const BSeg &A, const BSeg &E, F3 &S, F3 &P, float &u) {
+  const F3 trans = f3sub(A.mid, E.mid);
+  const float dd = f3dot(A.dir, E.dir), dat = f3dot(A.dir, trans), dbt = f3dot(E.dir, trans);
+  const float denom = FMA(-dd, dd, 1.0f);
+  const float ota = FMA(dd, dbt, -dat) * g.rcp(denom + 1e-6f);
+  const float otb = FMA(ota, dd, dbt);
+  const float ta = bclamps(ota, A.hl), tb = bclamps(otb, E.hl);
+  const F3 best_a = f3fma(A.dir, ta, A.mid), best_b = f3fma(E.dir, tb, E.mid);
+  float s1, s2;
+  const F3 new_a = bseg_point(A, best_b, s1);
+  const float d1 = f3d2(best_b, new_a);
+  const F3 new_b = bseg_point(E, best_a, s2);
+  const float d2 = f3d2(best_a, new_b);
+  const bool na = d1 < d2;
+  S = f3sel(na, new_a, best_a);
+  P = f3sel(na, best_b, new_b);
+  u = na ? s1 : (A.hl + ta) * A.il;
+}
+POB_D MCand bcand(const F3 S, const F3 P, const float u) {
+  MCand c;
+  c.da = S.a - P.a; c.db = S.b - P.b; c.dw = S.w - P.w;
+  c.d2 = FMA(c.dw, c.dw, FMA(c.db, c.db, c.da * c.da));
+  c.u = u;
+  return c;
+}
+// _closest_triangle_point(V0, V0 + e0, V0 + e1, pt) with the triangle's constants; edges
+// s01, s12, s20
+struct BTri {
+  F3 p0, e0, e1;
+  float a, b, c, idet;
+  BSeg s01, s12, s20;
+};
+POB_D F3 btri_point(const BTri &T, const F3 pt) {
+  const F3 d = f3sub(pt, T.p0);
+  const float e0d = f3dot(T.e0, d), e1d = f3dot(T.e1, d);
+  const float u = FMA(T.c, e0d, -(T.b * e1d)) * T.idet, v = FMA(T.a, e1d, -(T.b * e0d)) * T.idet;
+  const bool inside = (0.0f <= u) & (u <= 1.0f) & (0.0f <= v) & (v <= 1.0f) & (u + v <= 1.0f);
+  F3 cp = f3fma(T.e1, v, f3fma(T.e0, u, T.p0));
+  const float d0 = f3d2(cp, pt);
+  float t;
+  const F3 c1 = bseg_point(T.s01, pt, t);
+  const float d1 = f3d2(pt, c1);
+  const bool k0 = (d0 < d1) & inside;
+  cp = f3sel(k0, cp, c1);
+  float md = k0 ? d0 : d1;
+  const F3 c2 = bseg_point(T.s12, pt, t);
+  const float d2 = f3d2(pt, c2);
+  cp = f3sel(d2 < md, c2, cp);
+  md = fminf(md, d2);
+  const F3 c3 = bseg_point(T.s20, pt, t);
+  const float d3 = f3d2(pt, c3);
+  return f3sel(d3 < md, c3, cp);
 }
 
-// The contacts of face f (0..5) of a wall with half extents (hx, hy, hz) against the segment
-// [A, B] (wall frame; seg = false: the point A, the torso sphere), radius r, T = r^2 (1 + 2^-20):
-// emit(tau, n_local, pen) for triangle 0 then 1 when it penetrates.  tau = 1 - 2u places the
-// contact on the capsule's segment x + tau rotate(e0, q) (A = x + rotate(e0), B = x - rotate(e0)).
-// A triangle with d2 >= T has sqrt_rn(d2) >= r (no contact): its square root is skipped.
-template <class G, class F>
-POB_D void mesh_face(G &g, const int f, const v3 A, const v3 B, const bool seg, const float hx, const float hy,
-                     const float hz, const float r, const float T, F &&emit) {
+// A face (axis k, outward sign sg, plane w = w0, half extents ha, hb) with the capsule's
+// segment in face coordinates: its edges as segments (exact constants of ha, hb: every
+// derived quantity equals bseg_make's), its two triangles, and the segment-plane point.
+// Edges V0 V1 (a), V1 V2 (b), V0 V2 (diagonal), V2 V3 (a), V0 V3 (b); triangle t0 = (V0, V1,
+// V2), t1 = (V0, V2, V3) (oracle bface).
+struct MFace {
+  int k;
+  float sg, ha, hb, w0, ha2, hb2;
+  BSeg A;                        // the capsule's segment
+  float ilA, hlA, iddA, ilB, hlB, iddB, ilD, hlD, iddD, e_d;  // a / b / diagonal edge terms
+  float tt;                      // the segment-plane point's parameter
+};
+// the capsule's segment in the wall frame (once per wall; oracle capsule_wall_mesh capw)
+template <class G>
+POB_D BSeg mcap_seg(G &g, const v3 La, const v3 Lb) {
+  return bseg_make(g, f3(La.x, La.y, La.z), f3(Lb.x - La.x, Lb.y - La.y, Lb.z - La.z));
+}
+template <class G>
+POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const float hy, const float hz) {
+  MFace F;
   const int k = f >> 1;
-  const float sg = (f & 1) ? 1.0f : -1.0f;
-  // face coordinates (a, b, w): k = 0 (y, z, x), 1 (x, z, y), 2 (x, y, z)
-  const float ha = k == 0 ? hy : hx, hb = k == 2 ? hy : hz, hw = k == 0 ? hx : (k == 1 ? hy : hz);
-  const float w0 = sg * hw;
-  MSeg S;
-  S.aa_ = k == 0 ? A.y : A.x;
-  S.ab = k == 2 ? A.y : A.z;
-  S.aw = k == 0 ? A.x : (k == 1 ? A.y : A.z);
-  const float Ba = k == 0 ? B.y : B.x, Bb = k == 2 ? B.y : B.z, Bw = k == 0 ? B.x : (k == 1 ? B.y : B.z);
-  const float ha2 = 2.0f * ha, hb2 = 2.0f * hb;
-  const float e_d = FMA(hb2, hb2, ha2 * ha2), i_d = g.rcp(e_d);
+  F.k = k;
+  F.sg = (f & 1) ? 1.0f : -1.0f;
+  F.ha = k == 0 ? hy : hx;
+  F.hb = k == 2 ? hy : hz;
+  F.w0 = F.sg * (k == 0 ? hx : (k == 1 ? hy : hz));
+  F.A = bseg_perm(capw, k);
+  F.ha2 = F.ha + F.ha;  // V1 - V0 = (ha - (-ha), ..): exact
+  F.hb2 = F.hb + F.hb;
+  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2;
+  F.e_d = FMA(F.hb2, F.hb2, F.ha2 * F.ha2);
+  const float lA = g.sqrt(dA), lB = g.sqrt(dB), lD = g.sqrt(F.e_d);  // (half extents > 1e-8: pob_system.cpp)
+  F.ilA = g.rcp(lA + 1e-6f); F.hlA = lA * 0.5f; F.iddA = g.rcp(dA + 1e-6f);
+  F.ilB = g.rcp(lB + 1e-6f); F.hlB = lB * 0.5f; F.iddB = g.rcp(dB + 1e-6f);
+  F.ilD = g.rcp(lD + 1e-6f); F.hlD = lD * 0.5f; F.iddD = g.rcp(F.e_d + 1e-6f);
+  F.tt = bclamp01((F.sg * F.w0 - F.sg * F.A.p0.w) * g.rcp(F.sg * F.A.d.w + 1e-6f));
+  return F;
+}
+// edge e of the face as a segment: 0 V0 V1, 1 V1 V2, 2 V0 V2, 3 V2 V3, 4 V0 V3, 5 V2 V0, 6 V3 V0
+POB_D BSeg medge(const MFace &F, const int e) {
+  const float ha = F.ha, hb = F.hb, w0 = F.w0;
+  BSeg s;
+  const bool ea = e == 0 || e == 3, eb = e == 1 || e == 4 || e == 6, ed = e == 2 || e == 5;
+  const bool neg = e >= 3;  // direction -a (3), -b (6), -diagonal (5); 4 is +b
+  const float da = ea ? (e == 3 ? -F.ha2 : F.ha2) : (ed ? (e == 5 ? -F.ha2 : F.ha2) : 0.0f);
+  const float db = eb ? (e == 6 ? -F.hb2 : F.hb2) : (ed ? (e == 5 ? -F.hb2 : F.hb2) : 0.0f);
+  (void)neg;
+  const float pa = (e == 1) ? ha : ((e == 3 || e == 5) ? ha : -ha);
+  const float pb = (e == 3 || e == 5 || e == 6) ? hb : -hb;
+  s.p0 = f3(pa, pb, w0);
+  s.d = f3(da, db, 0.0f);
+  s.il = ea ? F.ilA : (eb ? F.ilB : F.ilD);
+  s.hl = ea ? F.hlA : (eb ? F.hlB : F.hlD);
+  s.idd = ea ? F.iddA : (eb ? F.iddB : F.iddD);
+  s.dir = f3(da * s.il, db * s.il, 0.0f);
+  s.mid = f3(FMA(s.dir.a, s.hl, pa), FMA(s.dir.b, s.hl, pb), w0);
+  return s;
+}
+// triangle t of the face (oracle btri_make)
+POB_D BTri mtri(const MFace &F, const int t) {
+  BTri T;
+  T.p0 = f3(-F.ha, -F.hb, F.w0);
+  T.e0 = t == 0 ? f3(F.ha2, 0.0f, 0.0f) : f3(F.ha2, F.hb2, 0.0f);
+  T.e1 = t == 0 ? f3(F.ha2, F.hb2, 0.0f) : f3(0.0f, F.hb2, 0.0f);
+  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2;
+  // a = e0.e0, b = e0.e1, c = e1.e1 with the zero products dropped (exact: +0 terms)
+  T.a = t == 0 ? dA : F.e_d;
+  T.b = t == 0 ? dA : dB;
+  T.c = t == 0 ? F.e_d : dB;
+  T.idet = 1.0f;  // set by the caller (one reciprocal per triangle, in the guard's policy)
+  T.s01 = medge(F, t == 0 ? 0 : 2);
+  T.s12 = medge(F, t == 0 ? 1 : 3);
+  T.s20 = medge(F, t == 0 ? 5 : 6);
+  return T;
+}
+// candidate kk of triangle t (oracle bface order): 0..2 the triangle's edges (t0: V0 V1, V1 V2,
+// V0 V2; t1: V0 V2, V2 V3, V0 V3) against the segment, 3 the segment-plane point and its
+// closest triangle point; any other kk: none (d2 = +inf)
+template <class G>
+POB_D MCand mface_cand(G &g, const MFace &F, const int t, const int kk) {
+  MCand c;
+  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
+  if (kk < 3) {
+    const int e = t == 0 ? kk : (kk == 0 ? 2 : kk + 2);
+    F3 S, P;
+    float u;
+    bseg_seg(g, F.A, medge(F, e), S, P, u);
+    c = bcand(S, P, u);
+  } else if (kk == 3) {
+    BTri T = mtri(F, t);
+    T.idet = g.rcp(FMA(T.a, T.c, -(T.b * T.b)));
+    const F3 sp = f3fma(F.A.d, F.tt, F.A.p0);
+    c = bcand(sp, btri_point(T, sp), F.tt);
+  }
+  return c;
+}
+// the triangle's pick with brax's tie rule (oracle bpick): all four candidates, the minimum,
+// ties averaged in candidate order (the slow path of a tie: the fast forms take the first
+// strict minimum and call this only when two candidates tie at a distance below the radius)
+template <class G>
+POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
+  F3 sp[4], tp[4];
+  float u[4], d2[4];
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const int e = t == 0 ? kk : (kk == 0 ? 2 : kk + 2);
+    bseg_seg(g, F.A, medge(F, e), sp[kk], tp[kk], u[kk]);
+    d2[kk] = f3d2(sp[kk], tp[kk]);
+  }
+  {
+    BTri T = mtri(F, t);
+    T.idet = g.rcp(FMA(T.a, T.c, -(T.b * T.b)));
+    sp[3] = f3fma(F.A.d, F.tt, F.A.p0);
+    tp[3] = btri_point(T, sp[3]);
+    u[3] = F.tt;
+    d2[3] = f3d2(sp[3], tp[3]);
+  }
+  const float mn = fminf(fminf(d2[0], d2[1]), fminf(d2[2], d2[3]));
+  F3 S = f3(0.0f, 0.0f, 0.0f), P = S;
+  float us = 0.0f, cnt = 0.0f;
+  int first = -1;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    if (d2[kk] == mn) {
+      if (first < 0) first = kk;
+      S = f3(S.a + sp[kk].a, S.b + sp[kk].b, S.w + sp[kk].w);
+      P = f3(P.a + tp[kk].a, P.b + tp[kk].b, P.w + tp[kk].w);
+      us += u[kk];
+      cnt += 1.0f;
+    }
+  MCand c;
+  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
+  if (first < 0) return c;
+  if (cnt > 1.0f) {
+    S = f3(S.a / cnt, S.b / cnt, S.w / cnt);
+    P = f3(P.a / cnt, P.b / cnt, P.w / cnt);
+    c = bcand(S, P, us / cnt);
+  } else {
+    F3 s1 = sp[0], p1 = tp[0];
+#pragma unroll
+    for (int kk = 1; kk < 4; ++kk) if (first == kk) { s1 = sp[kk]; p1 = tp[kk]; }
+    c = bcand(s1, p1, us);
+  }
+  return c;
+}
+
+// the contact of a triangle whose pick is c (oracle capsule_wall_mesh's emission): tau, the
+// wall-frame normal (S - P) / (1e-6 + dist) and dist = |S - P| (the caller's penetration is
+// r - dist, the contact's offset from the segment point along -n is 1e-6 + dist: the triangle
+// point -- both recomputed from dist by the same operations); false when the triangle does
+// not penetrate (r - dist <= 0).  d2 = 0 (a segment touching or piercing the triangle: its
+// distance is 0 exactly) takes no square root -- kept out of the range guards.
+template <class G>
+POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, const float T, float &tau, v3 &nl,
+                         float &dist) {
+  if (!(c.d2 < T)) return false;
+  dist = c.d2 > 0.0f ? g.sqrt(c.d2 > 0.0f ? c.d2 : 1.0f) : 0.0f;
+  if (!(r - dist > 0.0f)) return false;
+  const float inv = g.rcp(1e-6f + dist);
+  const float na = c.da * inv, nb = c.db * inv, nw = c.dw * inv;
+  const int k = F.k;
+  nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
+  tau = 1.0f - 2.0f * c.u;
+  return true;
+}
+
+// a candidate's distance as the reduction's key: NaN as +inf (the oracle's fminf skips NaN and
+// its tie mask excludes it; with every distance NaN or +inf there is no contact either way)
+POB_D float mcand_key(const float d2) { return d2 < __builtin_inff() ? d2 : __builtin_inff(); }
+
+// first strict minimum over a triangle's candidates, with the tie flag: tie when a later
+// candidate equals the running minimum (NaN never enters; +inf ties are below nothing)
+POB_D void mpick(MCand &best, bool &tie, const MCand &c) {
+  const bool lt = c.d2 < best.d2, eq = c.d2 == best.d2;
+  tie = lt ? false : (tie | eq);
+  if (lt) best = c;
+}
+
+// The contacts of face f (0..5) of a wall with half extents (hx, hy, hz) against the capsule's
+// segment (capw: mcap_seg of its wall-frame end points; a sphere has A == B), radius r,
+// T = r^2 (1 + 2^-20): emit(tau, n_local, dist) for triangle 0 then 1 when it penetrates.
+// tau = 1 - 2u places the segment point on the capsule's segment x + tau rotate(e0, q).
+// Exact skips (a candidate whose computed d2 is provably >= T can neither win with a contact
+// nor change a winner or a tie below T): an edge whose line the segment's box misses by
+// >= R = r + 1e-3 across it, the segment-plane candidate when its point is >= R off the plane
+// (its triangle points lie in the plane: w = w0 exactly).  (A NaN bound never skips.)
+template <class G, class Fn>
+POB_D void mesh_face(G &g, const int f, const BSeg &capw, const float hx, const float hy, const float hz,
+                     const float r, const float T, Fn &&emit) {
+  const MFace F = mface(g, f, capw, hx, hy, hz);
+  const float R = r + POB_MESH_MARGIN;
+  const F3 A = F.A.p0, B = f3(F.A.p0.a + F.A.d.a, F.A.p0.b + F.A.d.b, F.A.p0.w + F.A.d.w);
+  (void)B;
+  const float ha = F.ha, hb = F.hb, w0 = F.w0;
+  // the segment's box (its end points A and A + d; the same bound as the exact form's)
+  const float e_a = A.a + F.A.d.a, e_b = A.b + F.A.d.b, e_w = A.w + F.A.d.w;
+  const float amn = fminf(A.a, e_a), amx = fmaxf(A.a, e_a), bmn = fminf(A.b, e_b), bmx = fmaxf(A.b, e_b);
+  const float gw = fmaxf(fminf(A.w, e_w) - w0, w0 - fmaxf(A.w, e_w));
+  const bool bottom = !(fmaxf(fmaxf(bmn + hb, -hb - bmx), gw) >= R), top = !(fmaxf(fmaxf(bmn - hb, hb - bmx), gw) >= R);
+  const bool right = !(fmaxf(fmaxf(amn - ha, ha - amx), gw) >= R), left = !(fmaxf(fmaxf(amn + ha, -ha - amx), gw) >= R);
   MCand c[2];
+  bool tie[2] = {false, false};
 #pragma unroll
   for (int t = 0; t < 2; ++t) { c[t].d2 = __builtin_inff(); c[t].u = 0.0f; c[t].da = 0.0f; c[t].db = 0.0f; c[t].dw = 0.0f; }
-  // Exact skips: a candidate provably farther than R = r + 1e-3 from the triangle has a computed
-  // d2 above T (coordinate errors here are ~1e-6), so it can neither win with a contact nor
-  // change a winner without one -- the face cull's argument, per candidate: an end point at
-  // |w - w0| >= R from the face plane, an edge whose line the segment's box misses by >= R
-  // along one of the two axes across it.  (A NaN bound never skips.)
-  const float R = r + POB_MESH_MARGIN;
-  // end point A (and B) against each triangle
-  if (!(fabsf(S.aw - w0) >= R)) {
-    float qa[2], qb[2];
-    mtri_closest2(ha, hb, ha2, hb2, i_d, S.aa_, S.ab, qa[0], qb[0], qa[1], qb[1]);
+  F3 S, P;
+  float u;
+  // t0: V0 V1 (bottom), V1 V2 (right), diagonal; t1: diagonal, V2 V3 (top), V0 V3 (left)
+  if (bottom) { bseg_seg(g, F.A, medge(F, 0), S, P, u); mpick(c[0], tie[0], bcand(S, P, u)); }
+  if (right) { bseg_seg(g, F.A, medge(F, 1), S, P, u); mpick(c[0], tie[0], bcand(S, P, u)); }
+  bseg_seg(g, F.A, medge(F, 2), S, P, u);
+  const MCand dg = bcand(S, P, u);
+  mpick(c[0], tie[0], dg);
+  mpick(c[1], tie[1], dg);
+  if (top) { bseg_seg(g, F.A, medge(F, 3), S, P, u); mpick(c[1], tie[1], bcand(S, P, u)); }
+  if (left) { bseg_seg(g, F.A, medge(F, 4), S, P, u); mpick(c[1], tie[1], bcand(S, P, u)); }
+  const F3 sp = f3fma(F.A.d, F.tt, F.A.p0);
+  if (!(fabsf(sp.w - w0) >= R)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) mcand_take(c[t], 0.0f, S.aa_ - qa[t], S.ab - qb[t], S.aw - w0);
-  }
-  if (seg) {
-    if (!(fabsf(Bw - w0) >= R)) {
-      float qa[2], qb[2];
-      mtri_closest2(ha, hb, ha2, hb2, i_d, Ba, Bb, qa[0], qb[0], qa[1], qb[1]);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) mcand_take(c[t], 1.0f, Ba - qa[t], Bb - qb[t], Bw - w0);
-    }
-    S.Da = Ba - S.aa_; S.Db = Bb - S.ab; S.Dw = Bw - S.aw;
-    S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
-    S.inv_aa = g.rcp(S.aa);
-    const float e_a = ha2 * ha2, e_b = hb2 * hb2;
-    const float i_a = g.rcp(e_a), i_b = g.rcp(e_b);
-    // the segment's box across the edges: gaps to a = +-ha, b = +-hb and to the plane
-    const float amn = fminf(S.aa_, Ba), amx = fmaxf(S.aa_, Ba), bmn = fminf(S.ab, Bb), bmx = fmaxf(S.ab, Bb);
-    const float gw = fmaxf(fminf(S.aw, Bw) - w0, w0 - fmaxf(S.aw, Bw));
-    const bool bottom = !(fmaxf(fmaxf(bmn + hb, -hb - bmx), gw) >= R), top = !(fmaxf(fmaxf(bmn - hb, hb - bmx), gw) >= R);
-    const bool right = !(fmaxf(fmaxf(amn - ha, ha - amx), gw) >= R), left = !(fmaxf(fmaxf(amn + ha, -ha - amx), gw) >= R);
-    // triangle 0: bottom, right, diagonal; triangle 1: diagonal, top, left (the diagonal's
-    // candidate is the same closest pair for both: evaluated once, taken in each order)
-    if (bottom) mseg_edge(g, c[0], S, -ha, -hb, w0, ha2, 0.0f, e_a, i_a);
-    if (right) mseg_edge(g, c[0], S, ha, -hb, w0, 0.0f, hb2, e_b, i_b);
-    MCand dg;
-    dg.d2 = __builtin_inff(); dg.u = 0.0f; dg.da = 0.0f; dg.db = 0.0f; dg.dw = 0.0f;
-    mseg_edge(g, dg, S, -ha, -hb, w0, ha2, hb2, e_d, i_d);
-    // (taken on its own squared distance: an untaken dg -- a NaN or overflowing candidate,
-    // which the oracle never takes -- keeps d2 = inf, not the 0 of its cleared fields)
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-      if (dg.d2 < c[t].d2) c[t] = dg;
-    if (top) mseg_edge(g, c[1], S, ha, hb, w0, -ha2, 0.0f, e_a, i_a);
-    if (left) mseg_edge(g, c[1], S, -ha, hb, w0, 0.0f, -hb2, e_b, i_b);
-    // the segment crossing the face plane inside the triangle
-    const float aw = S.aw - w0, bw = Bw - w0;
-    if (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f))) {
-      const float u = aw * g.rcp(aw - bw);
-      const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        if (mtri_inside(t == 1, ha, hb, sa, sb)) mcand_take(c[t], u, 0.0f, 0.0f, sw - w0);
+    for (int t = 0; t < 2; ++t) {
+      BTri Tr = mtri(F, t);
+      Tr.idet = g.rcp(FMA(Tr.a, Tr.c, -(Tr.b * Tr.b)));
+      mpick(c[t], tie[t], bcand(sp, btri_point(Tr, sp), F.tt));
     }
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    if (c[t].d2 < T) {
-      // (d2 = 0: the segment touches or pierces the triangle -- common when a leg goes through
-      // a wall -- has distance 0 exactly and uses no reciprocal; kept out of the range guards,
-      // whose rerun (GuardAcc) would double the wave's step)
-      float dist = 0.0f, inv = 0.0f;
-      if (c[t].d2 > 0.0f) g.sqrt_rcp(c[t].d2, dist, inv);
-      const float pen = r - dist;
-      if (pen > 0.0f) {
-        float na, nb, nw;
-        if (c[t].d2 > 0.0f) { na = c[t].da * inv; nb = c[t].db * inv; nw = c[t].dw * inv; }
-        else { na = 0.0f; nb = 0.0f; nw = sg; }
-        // face -> wall frame
-        const v3 nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
-        emit(1.0f - 2.0f * c[t].u, nl, pen);
-      }
-    }
+    MCand ct = c[t];
+    if (tie[t] && ct.d2 < T) ct = mtri_pick_ties(g, F, t);  // (rare: two candidates at one distance)
+    float tau, dist;
+    v3 nl;
+    if (mface_contact(g, F, ct, r, T, tau, nl, dist)) emit(tau, nl, dist);
   }
 }
 
@@ -260,210 +419,28 @@ POB_D v3 mwall_world_n(const MWall &W, const v3 nl) {
   return V(FMA(-nl.y, W.s, nl.x * W.c), FMA(nl.y, W.c, nl.x * W.s), nl.z);
 }
 
-// ---------------------------------------------------------------- one candidate at a time
-// mesh_face's work split into independent pieces, so that the lanes of a wave can evaluate a
-// face's candidates side by side (mesh_wave_walk): the face frame, each candidate on its own,
-// and the contact of a triangle's winner.  The first strict minimum of mesh_face's sequential
-// candidate order is the lexicographic minimum of (d2, position in that order) over the
-// candidates (mcand_take never stores a NaN; a candidate it does not take keeps d2 = +inf), so
-// the winner, and with it every bit of the contact, is mesh_face's.
-struct MFace {
-  int k;
-  float sg, ha, hb, w0, ha2, hb2, i_d;
-  float pa, pb, pw, qa, qb, qw;  // end points A and B in face coordinates (a, b, w)
-};
-template <class G>
-POB_D MFace mface(G &g, const int f, const v3 A, const v3 B, const float hx, const float hy, const float hz) {
-  MFace F;
-  const int k = f >> 1;
-  F.k = k;
-  F.sg = (f & 1) ? 1.0f : -1.0f;
-  F.ha = k == 0 ? hy : hx;
-  F.hb = k == 2 ? hy : hz;
-  F.w0 = F.sg * (k == 0 ? hx : (k == 1 ? hy : hz));
-  F.pa = k == 0 ? A.y : A.x; F.pb = k == 2 ? A.y : A.z; F.pw = k == 0 ? A.x : (k == 1 ? A.y : A.z);
-  F.qa = k == 0 ? B.y : B.x; F.qb = k == 2 ? B.y : B.z; F.qw = k == 0 ? B.x : (k == 1 ? B.y : B.z);
-  F.ha2 = 2.0f * F.ha;
-  F.hb2 = 2.0f * F.hb;
-  F.i_d = g.rcp(FMA(F.hb2, F.hb2, F.ha2 * F.ha2));
-  return F;
-}
-
-// Candidate kk of triangle t, in mesh_face's order: 0 / 1 the end point A / B, 2..4 the
-// triangle's edges (t = 0: bottom, right, diagonal; t = 1: diagonal, top, left), 5 the segment
-// crossing the face plane inside the triangle.  Any other kk, or a candidate that does not
-// apply (a sphere has its point only; no crossing), stays at d2 = +inf.  The same operations
-// on the same operands as mesh_face (its reciprocals 1 / e_a, 1 / e_b, 1 / (D . D) are taken
-// here only by the candidates that use them: the same values).
-template <class G>
-POB_D MCand mface_cand(G &g, const MFace &F, const bool seg, const int t, const int kk) {
-  MCand c;
-  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
-  if (kk == 0 || (kk == 1 && seg)) {
-    const float pa = kk == 0 ? F.pa : F.qa, pb = kk == 0 ? F.pb : F.qb, pw = kk == 0 ? F.pw : F.qw;
-    float qa, qb;
-    mtri_closest(t == 1, F.ha, F.hb, F.ha2, F.hb2, F.i_d, pa, pb, qa, qb);
-    mcand_take(c, kk == 0 ? 0.0f : 1.0f, pa - qa, pb - qb, pw - F.w0);
-  } else if (seg && kk >= 2 && kk <= 5) {
-    MSeg S;
-    S.aa_ = F.pa; S.ab = F.pb; S.aw = F.pw;
-    S.Da = F.qa - F.pa; S.Db = F.qb - F.pb; S.Dw = F.qw - F.pw;
-    if (kk < 5) {
-      S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
-      S.inv_aa = g.rcp(S.aa);
-      const bool diag = t == 0 ? kk == 4 : kk == 2;
-      const bool first = t == 0 ? kk == 2 : kk == 3;  // bottom (t = 0) / top (t = 1): along a
-      const float ha = F.ha, hb = F.hb, ha2 = F.ha2, hb2 = F.hb2;
-      // edges: bottom (-ha, -hb) + (2ha, 0), right (ha, -hb) + (0, 2hb), diagonal (-ha, -hb) +
-      // (2ha, 2hb), top (ha, hb) + (-2ha, 0), left (-ha, hb) + (0, -2hb)
-      const float e0a = diag ? -ha : (t == 0 ? (first ? -ha : ha) : (first ? ha : -ha));
-      const float e0b = diag ? -hb : (t == 0 ? -hb : hb);
-      const float fa = diag ? ha2 : (first ? (t == 0 ? ha2 : -ha2) : 0.0f);
-      const float fb = diag ? hb2 : (first ? 0.0f : (t == 0 ? hb2 : -hb2));
-      const float ee = diag ? FMA(hb2, hb2, ha2 * ha2) : (first ? ha2 * ha2 : hb2 * hb2);
-      mseg_edge(g, c, S, e0a, e0b, F.w0, fa, fb, ee, diag ? F.i_d : g.rcp(ee));
-    } else {
-      const float aw = F.pw - F.w0, bw = F.qw - F.w0;
-      if (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f))) {
-        const float u = aw * g.rcp(aw - bw);
-        const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
-        if (mtri_inside(t == 1, F.ha, F.hb, sa, sb)) mcand_take(c, u, 0.0f, 0.0f, sw - F.w0);
-      }
-    }
-  }
-  return c;
-}
-
-// mface_cand without branches (the cooperative walk: a wave's lanes hold different kinds, so
-// a kind's branch would be executed by the whole wave anyway): every form -- the end point, the
-// edge, the crossing -- computed, the lane's kind selected.  The same operations on the same
-// operands as mface_cand where its branches are taken; the forms a lane does not need run on
-// substituted operands (1 under a reciprocal) that keep the range guards quiet.
-template <class G>
-POB_D MCand mface_cand_bf(G &g, const MFace &F, const bool seg, const int t, const int kk) {
-  const bool t1 = t == 1;
-  // end point kk (A for 0, B for 1)
-  const bool ep = kk == 0 || (kk == 1 && seg);
-  const bool isb = kk == 1;
-  const float pa = isb ? F.qa : F.pa, pb = isb ? F.qb : F.pb, pw = isb ? F.qw : F.pw;
-  float qa, qb;
-  {
-    const float ha = F.ha, hb = F.hb;
-    const float cr = FMA(pa + ha, hb, -((pb + hb) * ha));
-    const bool in = t1 ? ((pb <= hb) & (pa >= -ha) & (cr <= 0.0f)) : ((pb >= -hb) & (pa <= ha) & (cr >= 0.0f));
-    const float s_ = clamp01(FMA(pb + hb, F.hb2, (pa + ha) * F.ha2) * F.i_d);
-    const float s2 = 2.0f * s_;
-    const float da = FMA(s2, ha, -ha), db = FMA(s2, hb, -hb);
-    const float ca = clamp_sym(pa, ha), cb = clamp_sym(pb, hb);
-    const float e0a = t1 ? da : ca, e0b = t1 ? db : -hb;
-    const float e1a = t1 ? ca : ha, e1b = t1 ? hb : cb;
-    const float e2a = t1 ? -ha : da, e2b = t1 ? cb : db;
-    const float g0 = pa - e0a, h0 = pb - e0b;
-    float best = FMA(h0, h0, g0 * g0);
-    float ra = e0a, rb = e0b;
-    const float g1 = pa - e1a, h1 = pb - e1b;
-    const float d1 = FMA(h1, h1, g1 * g1);
-    const bool b1 = d1 < best;
-    best = b1 ? d1 : best; ra = b1 ? e1a : ra; rb = b1 ? e1b : rb;
-    const float g2 = pa - e2a, h2 = pb - e2b;
-    const float d2 = FMA(h2, h2, g2 * g2);
-    const bool b2 = d2 < best;
-    ra = b2 ? e2a : ra; rb = b2 ? e2b : rb;
-    qa = in ? pa : ra; qb = in ? pb : rb;
-  }
-  const float ea_ = pa - qa, eb_ = pb - qb, ew_ = pw - F.w0;
-  const float e_d2 = FMA(ew_, ew_, FMA(eb_, eb_, ea_ * ea_));
-  // edge kk (2..4) of triangle t
-  MSeg S;
-  S.aa_ = F.pa; S.ab = F.pb; S.aw = F.pw;
-  S.Da = F.qa - F.pa; S.Db = F.qb - F.pb; S.Dw = F.qw - F.pw;
-  const bool ed = seg && kk >= 2 && kk <= 4;
-  S.aa = FMA(S.Dw, S.Dw, FMA(S.Db, S.Db, S.Da * S.Da));
-  S.inv_aa = g.rcp(ed ? S.aa : 1.0f);
-  const bool diag = t == 0 ? kk == 4 : kk == 2;
-  const bool first = t == 0 ? kk == 2 : kk == 3;
-  const float ha = F.ha, hb = F.hb, ha2 = F.ha2, hb2 = F.hb2;
-  const float e0a = diag ? -ha : (t == 0 ? (first ? -ha : ha) : (first ? ha : -ha));
-  const float e0b = diag ? -hb : (t == 0 ? -hb : hb);
-  const float fa = diag ? ha2 : (first ? (t == 0 ? ha2 : -ha2) : 0.0f);
-  const float fb = diag ? hb2 : (first ? 0.0f : (t == 0 ? hb2 : -hb2));
-  const float ee = diag ? FMA(hb2, hb2, ha2 * ha2) : (first ? ha2 * ha2 : hb2 * hb2);
-  const float inv_ee = diag ? F.i_d : g.rcp(ed ? ee : 1.0f);
-  float su, sda, sdb, sdw;
-  {
-    const float ra = S.aa_ - e0a, rb = S.ab - e0b, rw = S.aw - F.w0;
-    const float f = FMA(fb, rb, fa * ra);
-    const float cc = FMA(S.Dw, rw, FMA(S.Db, rb, S.Da * ra));
-    const float bb = FMA(S.Db, fb, S.Da * fa);
-    const float den = FMA(S.aa, ee, -(bb * bb));
-    const bool dp = den > 0.0f;
-    const float u0 = dp ? clamp01(FMA(bb, f, -(cc * ee)) * g.rcp(ed && dp ? den : 1.0f)) : 0.0f;
-    const float t0 = FMA(bb, u0, f) * inv_ee;
-    const bool tl = t0 < 0.0f, tg = !tl && (t0 > 1.0f);
-    const float u = tl ? clamp01(-cc * S.inv_aa) : (tg ? clamp01((bb - cc) * S.inv_aa) : u0);
-    const float tt = tl ? 0.0f : (tg ? 1.0f : t0);
-    const float sa = FMA(u, S.Da, S.aa_), sb = FMA(u, S.Db, S.ab), sw = FMA(u, S.Dw, S.aw);
-    su = u; sda = sa - FMA(tt, fa, e0a); sdb = sb - FMA(tt, fb, e0b); sdw = sw - F.w0;
-  }
-  const float s_d2 = FMA(sdw, sdw, FMA(sdb, sdb, sda * sda));
-  // the crossing (kk 5)
-  const float aw = F.pw - F.w0, bw = F.qw - F.w0;
-  const bool cr = seg && kk == 5 && (((aw < 0.0f) & (bw > 0.0f)) | ((aw > 0.0f) & (bw < 0.0f)));
-  const float cu = aw * g.rcp(cr ? aw - bw : 1.0f);
-  const float csa = FMA(cu, S.Da, S.aa_), csb = FMA(cu, S.Db, S.ab), csw = FMA(cu, S.Dw, S.aw);
-  const bool cin = cr && (t1 ? ((csb <= hb) & (csa >= -ha) & (FMA(csa + ha, hb, -((csb + hb) * ha)) <= 0.0f))
-                             : ((csb >= -hb) & (csa <= ha) & (FMA(csa + ha, hb, -((csb + hb) * ha)) >= 0.0f)));
-  const float cdw = csw - F.w0;
-  const float c_d2 = FMA(cdw, cdw, FMA(0.0f, 0.0f, 0.0f * 0.0f));
-  // the lane's kind (mcand_take's rule: a NaN or +inf d2 is not taken: d2 stays +inf, fields 0)
-  MCand c;
-  const float d2 = ep ? e_d2 : (ed ? s_d2 : (cin ? c_d2 : __builtin_inff()));
-  const bool take = d2 < __builtin_inff();
-  c.d2 = take ? d2 : __builtin_inff();
-  c.u = take ? (ep ? (isb ? 1.0f : 0.0f) : (ed ? su : cu)) : 0.0f;
-  c.da = take ? (ep ? ea_ : (ed ? sda : 0.0f)) : 0.0f;
-  c.db = take ? (ep ? eb_ : (ed ? sdb : 0.0f)) : 0.0f;
-  c.dw = take ? (ep ? ew_ : (ed ? sdw : cdw)) : 0.0f;
-  return c;
-}
-
-// the contact of a triangle whose winning candidate is c (mesh_face's emission): tau, the
-// wall-frame normal and the penetration; false when the triangle does not penetrate
-template <class G>
-POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, const float T, float &tau, v3 &nl,
-                         float &pen) {
-  if (!(c.d2 < T)) return false;
-  float dist = 0.0f, inv = 0.0f;
-  if (c.d2 > 0.0f) g.sqrt_rcp(c.d2, dist, inv);  // (d2 = 0: mesh_face)
-  pen = r - dist;
-  if (!(pen > 0.0f)) return false;
-  float na, nb, nw;
-  if (c.d2 > 0.0f) { na = c.da * inv; nb = c.db * inv; nw = c.dw * inv; }
-  else { na = 0.0f; nb = 0.0f; nw = F.sg; }
-  const int k = F.k;
-  nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
-  tau = 1.0f - 2.0f * c.u;
-  return true;
-}
-
 #ifndef POB_MESH_HOST
 // ---------------------------------------------------------------- the wave's face walk
 // Walk the lanes' face items (M[s]: bit 8 w + f for face f of wall w of the lane's body slot
 // s; slots, then bits, in increasing order: the oracle's contact order per body) and call
-// apply(s, bit, tau, n_world, pen) on the owning lane for every penetrating triangle, in
+// apply(s, bit, tau, n_world, dist) on the owning lane for every penetrating triangle, in
 // order.  seg_of(s, A, B, r, seg) gives a slot's segment (world end points), radius and
 // whether it is a capsule (false: the torso sphere at A).
 //
-// A face costs ~1 000 instructions evaluated on one lane (its twelve candidates and two
-// emissions one after another) and few lanes of a wave hold one at a time (0.7 items on the
-// busiest lane per wave and collide substep on HH rollouts, scripts/wall_walk_stats.py), so
-// the wave shares them out: each round takes the next items of up to four lanes (a lane's
-// next two of one body when fewer lanes have one) and gives each of those faces sixteen lanes -- lane 8 t + kk of the group computes candidate kk of
-// triangle t -- reduces the candidates to each triangle's winner (DPP, lexicographic (d2, kk)
-// minimum over the eight lanes), lets the winner lane compute the contact, and hands it to
-// the owner (ds_bpermute), which applies its triangles in order.  Needs all 64 lanes active
-// (the DPP reduction reads every lane of a group); with lanes masked off -- the batch's last
-// wave, a masked reset -- each lane walks its own items (mesh_lane_walk).
+// A face evaluated on one lane is a few hundred instructions (its ten candidates, both
+// triangles' picks and emissions, one after another) and few lanes of a wave hold one at a
+// time (0.7 items on the busiest lane per wave and collide substep on HH rollouts,
+// scripts/wall_walk_stats.py), so the wave shares them out: each round takes the next items
+// of up to eight lanes (a lane's next two of one body when fewer lanes have one) and gives
+// each of those faces eight lanes -- lane 4 t + kk of the group computes candidate kk of
+// triangle t (mface_cand: the triangle's three edges, the segment-plane point) -- reduces
+// each triangle's four candidates to the first strict minimum (DPP over the quad,
+// lexicographic (d2, kk), with a tie count: a tie below the radius takes brax's averaging on
+// the winner lane), lets the winner compute the contact and hands it to the owner
+// (ds_bpermute), which applies its triangles in order.  Needs all 64 lanes active (the DPP
+// reduction reads every lane of a quad); with lanes masked off -- the batch's last wave, a
+// masked reset -- each lane walks its own items (mesh_lane_walk).
+static_assert(POB_MAXW <= 8, "face items pack wall w and face f as bit 8 w + f of a uint64_t");
 POB_D float mlane_read(const float v, const int src) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
 }
@@ -476,6 +453,8 @@ POB_D void mlexmin_dpp(float &d, int &kk) {
   d = take ? od : d;
   kk = take ? ok : kk;
 }
+template <int CTRL>
+POB_D int msum_dpp(const int v) { return v + __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true); }
 
 // each lane walks its own items, one face per iteration (mesh_face)
 template <int NB, class G, class SegOf, class Apply>
@@ -505,8 +484,10 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
       const v3 La = mwall_local(W, cz, A);
       const v3 Lb = seg ? mwall_local(W, cz, B) : La;
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      mesh_face(g, bit & 7, La, Lb, seg, W.hx, W.hy, hz, r, T, [&](const float tau, const v3 nl, const float pen) {
-        apply(s, bit, tau, mwall_world_n(W, nl), pen);
+      const BSeg capw = mcap_seg(g, La, Lb);
+      mesh_face(g, bit & 7, capw, W.hx, W.hy, hz, r, T,
+                [&](const float tau, const v3 nl, const float dist) {
+        apply(s, bit, tau, mwall_world_n(W, nl), dist);
       });
     }
   }
@@ -524,7 +505,7 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     return;
   }
   const int lane = (int)__lane_id();
-  const int grp = lane >> 4, tri = (lane >> 3) & 1, kk = lane & 7;
+  const int grp = lane >> 3, tri = (lane >> 2) & 1, kk = lane & 3;
   while (true) {
     // the lane's next item (slot s, face bit b1) and the one after it in the same slot (b2)
     bool has = false;
@@ -543,30 +524,30 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     const bool has2 = has && rest != 0ull;
     const uint64_t req2 = __ballot(has2);
     const int b1 = has ? __builtin_ctzll(ml) : 0, b2 = has2 ? __builtin_ctzll(rest) : 0;
-    // a round's four groups: the first items of the first four lanes with one, then (when
+    // a round's eight groups: the first items of the first eight lanes with one, then (when
     // fewer) the second items of lanes with two -- each lane's items in its order
     const int n1 = __builtin_popcountll(req1), n2 = __builtin_popcountll(req2);
     const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(req1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req1, 0u));
     const uint32_t r2 = (uint32_t)n1 +
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(req2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req2, 0u));
-    const bool own1 = has && r1 < 4u, own2 = has2 && r2 < 4u;  // (own2 implies own1: n1 < 4)
+    const bool own1 = has && r1 < 8u, own2 = has2 && r2 < 8u;  // (own2 implies own1: n1 < 8)
     const uint64_t pop = (own1 ? 1ull << b1 : 0ull) | (own2 ? 1ull << b2 : 0ull);
 #pragma unroll
     for (int q = 0; q < NB; ++q) M[q] = s == q ? (M[q] & ~pop) : M[q];
-    // group owners (wave-uniform): lane and item of each of the four groups
-    int og[4];
+    // group owners (wave-uniform): the lane of each of the eight groups
+    int ol = 0;
     {
       uint64_t m1 = req1, m2 = req2;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 8; ++q) {
         const bool first = q < n1;
         const uint64_t m = first ? m1 : m2;
-        og[q] = m != 0ull ? __builtin_ctzll(m) : 0;
+        const int o = m != 0ull ? __builtin_ctzll(m) : 0;
+        ol = grp == q ? o : ol;
         m1 = first ? (m1 & (m1 - 1ull)) : m1;
         m2 = first ? m2 : (m2 & (m2 - 1ull));
       }
     }
-    const int ol = grp == 0 ? og[0] : (grp == 1 ? og[1] : (grp == 2 ? og[2] : og[3]));
     const bool gv = grp < n1 + n2;
     const bool second = grp >= n1;
     v3 A, B;
@@ -583,35 +564,39 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     const MWall W = mwall_row(WT + POB_WALL_FLOATS * ((mo >> 3) & 7));
     const v3 La = mwall_local(W, cz, Ao);
     const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
-    const MFace F = mface(g, mo & 7, La, Lb, W.hx, W.hy, hz);
-    const MCand c = mface_cand_bf(g, F, sego, tri, gv ? kk : 7);
-    // each triangle's winner over its eight lanes
+    const MFace F = mface(g, mo & 7, mcap_seg(g, La, Lb), W.hx, W.hy, hz);
+    MCand c = mface_cand(g, F, tri, gv ? kk : 7);
+    c.d2 = mcand_key(c.d2);
+    // each triangle's first strict minimum over its quad, and the number of candidates at it
     float dmin = c.d2;
     int kmin = kk;
-    mlexmin_dpp<0xB1>(dmin, kmin);   // quad_perm [1, 0, 3, 2]
-    mlexmin_dpp<0x4E>(dmin, kmin);   // quad_perm [2, 3, 0, 1]
-    mlexmin_dpp<0x141>(dmin, kmin);  // row_half_mirror: the other quad of the eight
-    float tau = 0.0f, pen = 0.0f;
+    mlexmin_dpp<0xB1>(dmin, kmin);  // quad_perm [1, 0, 3, 2]
+    mlexmin_dpp<0x4E>(dmin, kmin);  // quad_perm [2, 3, 0, 1]
+    const int neq = msum_dpp<0x4E>(msum_dpp<0xB1>(c.d2 == dmin ? 1 : 0));
+    float tau = 0.0f, dst = 0.0f;
     v3 nw = V(0.0f, 0.0f, 0.0f);
     bool hit = false;
     if (gv && kk == kmin) {
+      const float T = (ro * ro) * 1.00000095367431640625f;
+      MCand ct = c;
+      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties(g, F, tri);  // (rare: brax's tie average)
       v3 nl;
-      hit = mface_contact(g, F, c, ro, (ro * ro) * 1.00000095367431640625f, tau, nl, pen);
+      hit = mface_contact(g, F, ct, ro, T, tau, nl, dst);
       if (hit) nw = mwall_world_n(W, nl);
     }
     // the owners take their items' triangles in order: the winners' lanes first (all four
     // fetches in flight), then each contact
-    const int g1 = 16 * (int)r1, g2 = 16 * (int)r2;
-    const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 8 + mlane_read_i(kmin, g1 + 8);
-    const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 8 + mlane_read_i(kmin, g2 + 8);
+    const int g1 = 8 * (int)r1, g2 = 8 * (int)r2;
+    const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 4 + mlane_read_i(kmin, g1 + 4);
+    const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 4 + mlane_read_i(kmin, g2 + 4);
     const int nt = __any(own2) ? 4 : 2;
 #pragma nounroll
     for (int t = 0; t < nt; ++t) {
       const int wl = t == 0 ? w10 : (t == 1 ? w11 : (t == 2 ? w20 : w21));
       const int h = mlane_read_i(hit ? 1 : 0, wl);
-      const float tw = mlane_read(tau, wl), pw = mlane_read(pen, wl);
+      const float tw = mlane_read(tau, wl), dw = mlane_read(dst, wl);
       const v3 nn = V(mlane_read(nw.x, wl), mlane_read(nw.y, wl), mlane_read(nw.z, wl));
-      if ((t < 2 ? own1 : own2) && h != 0) apply(s, t < 2 ? b1 : b2, tw, nn, pw);
+      if ((t < 2 ? own1 : own2) && h != 0) apply(s, t < 2 ? b1 : b2, tw, nn, dw);
     }
   }
 }

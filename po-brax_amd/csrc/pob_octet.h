@@ -77,7 +77,7 @@ struct OMesh {
   uint64_t mc[ONB];
   int nct;  // wall contacts of the position pass (the first OMAXC kept in the lane's LDS store)
 };
-// The position pass's wall contacts (slot, tau, n, pen), kept in the lane's LDS store
+// The position pass's wall contacts (slot, tau, n, dist), kept in the lane's LDS store
 // (lane-minor: element e at CS[64 e]) so that the velocity pass applies them without evaluating
 // their faces again; a lane with more re-walks its contact faces (ms.mc) from its segments,
 // which it then leaves in the store too (elements OCS_SEG.., off the registers of the velocity
@@ -216,20 +216,22 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
 #endif
   mesh_wave_walk<ONB>(g, WT, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
-                      [&](const int s, const int bit, const float tau, const v3 n, const float pen) {
+                      [&](const int s, const int bit, const float tau, const v3 n, const float dist) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
     const q4 q = qsel(s == 0, b.q[0], b.q[1]);
     const v3 pe = vfma(vsel3(s == 0, rv[0], rv[1]), tau, x);
     v3 dx = vsel3(s == 0, DX[0], DX[1]), da = vsel3(s == 0, DA[0], DA[1]);
-    owall_position(g, SC, pen, pe, n, s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1], s == 0 ? OT[OT_B(0)] : OT[OT_B(1)],
-                   x, q, qsel(s == 0, pqs[0], pqs[1]), vsel3(s == 0, pxs[0], pxs[1]), dx, da);
+    // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
+    owall_position(g, SC, (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) - dist, pe, n, 1e-6f + dist,
+                   s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, q, qsel(s == 0, pqs[0], pqs[1]), vsel3(s == 0, pxs[0], pxs[1]),
+                   dx, da);
     DX[0] = vsel3(s == 0, dx, DX[0]); DX[1] = vsel3(s == 1, dx, DX[1]);
     DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
     ms.mc[0] |= s == 0 ? 1ull << bit : 0ull;
     ms.mc[1] |= s == 1 ? 1ull << bit : 0ull;
     if (ms.nct < OMAXC) {
       float *c = CS + 64 * 6 * ms.nct;
-      c[0] = (float)s; c[64] = tau; c[128] = n.x; c[192] = n.y; c[256] = n.z; c[320] = pen;
+      c[0] = (float)s; c[64] = tau; c[128] = n.x; c[192] = n.y; c[256] = n.z; c[320] = dist;
     }
     ++ms.nct;
   });
@@ -267,8 +269,8 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
       const q4 q = qsel(s == 0, b.q[0], b.q[1]);
       const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), c[64], x);
       v3 dv = vsel3(s == 0, dV[0], dV[1]), dw = vsel3(s == 0, dW[0], dW[1]);
-      ocontact_vel_pe(g, SC, false, c[320], pe, V(c[128], c[192], c[256]), s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1],
-                      s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]),
+      ocontact_vel_pe(g, SC, false, (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) - c[320], pe, V(c[128], c[192], c[256]),
+                      1e-6f + c[320], s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]),
                       vsel3(s == 0, b.w[0], b.w[1]), dv, dw);
       dV[0] = vsel3(s == 0, dv, dV[0]); dV[1] = vsel3(s == 1, dv, dV[1]);
       dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
@@ -284,12 +286,12 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
                         r = s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1];
                         seg = !(isA && s == 0);
                       },
-                      [&](const int s, const int, const float tau, const v3 n, const float pen) {
+                      [&](const int s, const int, const float tau, const v3 n, const float dist) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
     const q4 q = qsel(s == 0, b.q[0], b.q[1]);
     const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), tau, x);
     v3 dv = vsel3(s == 0, dV[0], dV[1]), dw = vsel3(s == 0, dW[0], dW[1]);
-    ocontact_vel_pe(g, SC, false, pen, pe, n, s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1],
+    ocontact_vel_pe(g, SC, false, (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) - dist, pe, n, 1e-6f + dist,
                     s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]), vsel3(s == 0, b.w[0], b.w[1]),
                     dv, dw);
     dV[0] = vsel3(s == 0, dv, dV[0]); dV[1] = vsel3(s == 1, dv, dV[1]);

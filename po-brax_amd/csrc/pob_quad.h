@@ -107,11 +107,10 @@ struct QGround {
 };
 // The lane's wall contacts (pob_mesh.h, brax capsule x TriangulatedBox) of a collide substep:
 // the bodies' capsule segments at detection -- a = x + rotate(e0, q), b = x - rotate(e0, q)
-// (torso: the sphere centre a) -- and, per body, the (wall, face) items that produced a
-// contact: wall w of body l = bit 8 l + w of mc.  The velocity pass re-derives the face items
-// of exactly those walls from the stored segments and re-evaluates them (the same operations
-// on the same operands: the same contacts in the same order) instead of keeping every
-// contact in registers.
+// (torso: the sphere centre a) -- and, per body, the faces that produced a contact (mc[l]
+// bit 8 w + f: face f of wall w).  The velocity pass re-walks exactly those faces from the
+// stored segments (the same operations on the same operands: the same contacts in the same
+// order) instead of keeping every contact in registers.
 struct QMesh {
   v3 a[QNB], b[QNB];
   uint64_t mc[QNB];  // per body: the faces that produced a contact (bit 8 w + f)
@@ -251,13 +250,14 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
 #endif
   mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                      [&](const int l, const int bit, const float tau, const v3 n, const float pen) {
+                      [&](const int l, const int bit, const float tau, const v3 n, const float dist) {
     const v3 x = qpick3(l, b.x);
     const q4 q = qpick4(l, b.q);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, q, tau);
     v3 dx = qpick3(l, DX), da = qpick3(l, DA);
-    owall_position(g, SC, pen, pe, n, q_cap_r(S, LT, l), q_inv_mass(S, LT, l), x, q, L.get4(QL_PQ(0) + 7 * l),
-                   L.get3(QL_PX(0) + 7 * l), dx, da);
+    // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
+    owall_position(g, SC, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), x, q,
+                   L.get4(QL_PQ(0) + 7 * l), L.get3(QL_PX(0) + 7 * l), dx, da);
     qput3(l, DX, dx);
     qput3(l, DA, da);
     ms.mc[0] |= l == 0 ? 1ull << bit : 0ull;
@@ -294,12 +294,12 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
   M[0] = ms.mc[0]; M[1] = ms.mc[1]; M[2] = ms.mc[2];
   mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                      [&](const int l, const int, const float tau, const v3 n, const float pen) {
+                      [&](const int l, const int, const float tau, const v3 n, const float dist) {
     const v3 x = qpick3(l, b.x);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
     v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
-    ocontact_vel_pe(g, SC, false, pen, pe, n, q_cap_r(S, LT, l), q_inv_mass(S, LT, l), x, qpick3(l, b.v),
-                    qpick3(l, b.w), dv, dw);
+    ocontact_vel_pe(g, SC, false, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), x,
+                    qpick3(l, b.v), qpick3(l, b.w), dv, dw);
     qput3(l, dV, dv);
     qput3(l, dW, dw);
   });
@@ -343,13 +343,13 @@ POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const 
   }
   mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                      [&](const int l, const int, const float tau, const v3 n, const float pen) {
+                      [&](const int l, const int, const float tau, const v3 n, const float dist) {
     const v3 x = qpick3(l, b.x);
     const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
-    const float rl = q_cap_r(S, LT, l), iml = q_inv_mass(S, LT, l);
+    const float pen = q_cap_r(S, LT, l) - dist, cd = 1e-6f + dist, iml = q_inv_mass(S, LT, l);
     v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
-    if (LEGACY) olegacy_contact(S, pen, pe, n, rl, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
-    else ocontact_vel_pe(g, SC, false, pen, pe, n, rl, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
+    if (LEGACY) olegacy_contact(S, pen, pe, n, cd, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
+    else ocontact_vel_pe(g, SC, false, pen, pe, n, cd, iml, x, qpick3(l, b.v), qpick3(l, b.w), dv, dw);
     qput3(l, dV, dv);
     qput3(l, dW, dw);
   });

@@ -5,11 +5,13 @@ geometry reference.
 brax is not vendored (parity unpinned at the float level), so the restatement is pinned to
 the geometry it claims to compute: for every one of a box's 12 triangles, the closest points
 of the capsule's segment and the triangle, a contact per triangle closer than the radius with
-penetration r - distance and the normal along (segment point - triangle point).  The reference
-here triangulates the rotated box in world coordinates (the wall frame is not used), samples
-the segment densely and takes the exact point-triangle distance at every sample (Ericson's
-region test, float64), so its minimum is within the sampling step of the true segment-triangle
-distance.
+penetration r - distance, the normal along (segment point - triangle point) and the contact
+at the triangle point.  Both spellings are checked: brax's (the default: regularised forms,
+normal (S - P) / (1e-6 + |S - P|)) and the exact form (orc_set_mesh_variant(0)).  The
+reference here triangulates the rotated box in world coordinates (the wall frame is not
+used), samples the segment densely and takes the exact point-triangle distance at every
+sample (Ericson's region test, float64), so its minimum is within the sampling step of the
+true segment-triangle distance.
 """
 import itertools
 
@@ -114,8 +116,24 @@ def _case(rng, w):
     return centre + half * d, centre - half * d, True, 0.08
 
 
+BRAX, EXACT = 13, 0
+
+
+@pytest.fixture(params=[BRAX, EXACT], ids=["brax", "exact"])
+def spelling(request):
+    L = orc.lib()
+    prev = L.orc_get_mesh_variant()
+    L.orc_set_mesh_variant(request.param)
+    yield request.param
+    L.orc_set_mesh_variant(prev)
+
+
+def test_default_spelling_is_brax():
+    assert orc.lib().orc_get_mesh_variant() == BRAX
+
+
 @pytest.mark.parametrize("wi", range(len(WALLS)))
-def test_mesh_contacts_match_brute_force_geometry(wi):
+def test_mesh_contacts_match_brute_force_geometry(wi, spelling):
     rng = np.random.default_rng(100 + wi)
     w = _wall(*WALLS[wi])
     checked = 0
@@ -125,7 +143,9 @@ def test_mesh_contacts_match_brute_force_geometry(wi):
         got = orc.mesh_contacts(w, pa32, pb32, seg, r)
         ref = _reference(w, pa32.astype(np.float64), pb32.astype(np.float64), seg, r)
         step = (np.linalg.norm(pb - pa) / 4000.0) if seg else 0.0
-        tol = step + 2e-5
+        # brax's regularised forms move a distance by up to ~1e-4 where the segment is nearly
+        # parallel to an edge (the line solution's (denom + 1e-6), denom = sin^2 of the angle)
+        tol = step + (3e-4 if spelling == BRAX else 2e-5)
         expect = [t for t, (d, *_rest) in enumerate(ref) if d < r - tol]
         maybe = [t for t, (d, *_rest) in enumerate(ref) if d < r + tol]
         assert len(expect) <= len(got) <= len(maybe), (wi, len(got), [ref[t][0] for t in maybe])
@@ -136,16 +156,28 @@ def test_mesh_contacts_match_brute_force_geometry(wi):
             if j >= len(got):
                 assert t not in expect
                 continue
-            tau, nx, ny, nz, pen = (float(x) for x in got[j])
+            tau, nx, ny, nz, pen, cd = (float(x) for x in got[j])
             if abs((r - pen) - d) > tol + 1e-6:  # not this triangle: must be a borderline one
                 assert t not in expect, (wi, t, r - pen, d)
                 continue
             j += 1
             checked += 1
-            # the normal points from the triangle point to the segment point (when apart)
+            # the normal points from the triangle point to the segment point (when apart), of
+            # length d / (1e-6 + d) in brax's spelling, where the contact sits at the triangle
+            # point: the segment point moved by cd = 1e-6 + d along -n
             if d > 1e-3:
                 nref = (S - Q) / d
-                assert np.dot(nref, [nx, ny, nz]) > 0.999, (wi, t, nref, (nx, ny, nz))
+                nn = np.linalg.norm([nx, ny, nz])
+                # (brax: the points' up to ~1e-4 shift turns the normal by up to ~1e-4 / d; a
+                # segment nearly parallel to an edge takes a pair that is not the closest one, S - P
+                # then tilts by up to the segment's angle to the face: <= 5e-3 rad on these cases)
+                cos_min = np.cos(min(3e-4 / d + 5e-3, 1.5)) if spelling == BRAX else 0.999
+                assert np.dot(nref, [nx, ny, nz]) / nn > cos_min, (wi, t, nref, (nx, ny, nz))
+                scale = d / (1e-6 + d) if spelling == BRAX else 1.0
+                assert abs(nn - scale) < 2e-6 + (3e-4 / d if spelling == BRAX else 0.0)
+                # (the exact form, variant 0, keeps the round-4 contact position: the capsule
+                # surface point S - r n)
+                assert abs(cd - ((1e-6 + (r - pen)) if spelling == BRAX else r)) < 1e-7
             # the contact sits on the segment: x + tau e0 with tau = 1 - 2 u
             if seg and d > 1e-3:
                 Sg = 0.5 * (pa + pb) + tau * 0.5 * (pa - pb)
@@ -154,36 +186,46 @@ def test_mesh_contacts_match_brute_force_geometry(wi):
     assert checked > 20  # enough penetrating triangles were exercised
 
 
-def test_mesh_face_split_and_order():
+def test_mesh_face_split_and_order(spelling):
     """A leg lying flat against the +y face of an axis-aligned wall, crossing the face's diagonal:
     both triangles of that face report a contact (face order -x, +x, -y, +y, ...: entries of
-    the +y face), each with the face's outward normal and the same depth."""
+    the +y face), each with the face's outward normal (brax: scaled by 0.05 / (1e-6 + 0.05))
+    and the same depth."""
     w = _wall((0.0, 0.0), 0.0, (2.0, 0.5))
     y = 0.5 + 0.05  # segment 0.05 outside the face, radius 0.08: 0.03 deep
     a, b = np.array([-0.2, y, 0.3], np.float32), np.array([0.2, y, 0.7], np.float32)
     got = orc.mesh_contacts(w, a, b, True, 0.08)
     assert len(got) == 2
+    ny_ref = 0.05 / (1e-6 + 0.05) if spelling == BRAX else 1.0
     for row in got:
-        tau, nx, ny, nz, pen = row
-        assert abs(nx) < 1e-6 and abs(ny - 1.0) < 1e-6 and abs(nz) < 1e-6
+        tau, nx, ny, nz, pen, cd = row
+        assert abs(nx) < 1e-5 and abs(ny - ny_ref) < 1e-6 and abs(nz) < 1e-5
         assert abs(pen - 0.03) < 1e-5
 
 
-def test_mesh_deep_segment_crossing_a_face():
-    """A segment piercing a face (distance 0): the face's outward normal and penetration r,
-    the contact on the segment at the crossing point."""
+def test_mesh_deep_segment_crossing_a_face(spelling):
+    """A segment piercing a face.  Exact form: distance 0, the face's outward normal and
+    penetration r, the contact on the segment at the crossing point.  brax's spelling: the
+    segment-plane point's (n.(b - a) + 1e-6) stops it short of the plane on the inner side, so
+    |S - P| is ~1e-6 (its in-plane part rounding noise) and the normal (S - P) / (1e-6 + |S - P|)
+    is a short vector pointing INTO the box -- brax's own result in this regime is set by
+    1e-6-level arithmetic."""
     w = _wall((0.0, 0.0), 0.0, (2.0, 0.5))
     a, b = np.array([0.3, 0.8, 0.4], np.float32), np.array([0.3, 0.2, 0.4], np.float32)
     got = orc.mesh_contacts(w, a, b, True, 0.08)
-    pierced = [g for g in got if abs(g[4] - 0.08) < 1e-7]
+    pierced = [g for g in got if abs(g[4] - 0.08) < 1e-5]
     assert pierced, got
-    for tau, nx, ny, nz, pen in pierced:
-        assert (nx, ny, nz) == (0.0, 1.0, 0.0)
+    for tau, nx, ny, nz, pen, cd in pierced:
         # crossing y = 0.5: u = 0.5 -> tau = 0
-        assert abs(tau) < 1e-6
+        assert abs(tau) < 1e-5
+        if spelling == EXACT:
+            assert (nx, ny, nz) == (0.0, 1.0, 0.0) and pen == np.float32(0.08) and cd == np.float32(0.08)
+        else:
+            assert 0.0 < 0.08 - pen < 1e-5 and ny < 0.0 and np.linalg.norm([nx, ny, nz]) < 0.9
+            assert abs(cd - (1e-6 + (0.08 - pen))) < 1e-9
 
 
-def test_face_cull_is_exact_on_rollouts():
+def test_face_cull_is_exact_on_rollouts(spelling):
     """The face cull (gap >= r + 1e-3) never changes a contact: a mesh-model rollout with the
     cull and one evaluating every face of every wall are bit-identical (HH spawns against the
     T-maze's bottom wall; TAG and GA arenas)."""

@@ -28,16 +28,23 @@ struct v3 { float x, y, z; };
 struct float2 { float x, y; };
 #define FMA(a, b, c) fmaf((a), (b), (c))
 POB_D v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
-POB_D float clamp_sym(float x, float h) { return fminf(fmaxf(x, -h), h); }
-#define __builtin_amdgcn_fmed3f(x, lo, hi) fminf(fmaxf((x), (lo)), (hi))
 #define __builtin_inff() INFINITY
 struct HostGuard {
   float rcp(float x) { return 1.0f / x; }
+  float sqrt(float x) { return sqrtf(x); }
   void sqrt_rcp(float x, float &s, float &i) { s = sqrtf(x); i = 1.0f / s; }
 };
 """
 
 DRIVER = r"""
+static int g_ties = 0;
+extern "C" int host_tie_count(void) { const int n = g_ties; g_ties = 0; return n; }
+// the oracle's row: (tau, n, pen = r - dist, cd = 1e-6 + dist), as the kernels' callers form them
+static void put(float *out, int n, float tau, v3 nw, float r, float dist) {
+  out[6 * n] = tau; out[6 * n + 1] = nw.x; out[6 * n + 2] = nw.y; out[6 * n + 3] = nw.z; out[6 * n + 4] = r - dist;
+  out[6 * n + 5] = 1e-6f + dist;
+}
+// the per-lane form (mesh_face: both triangles, exact candidate skips, tie slow path)
 extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b, int seg, float r, float *out) {
   MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
   const float cz = w[2], hz = w[7];
@@ -46,19 +53,19 @@ extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b
   const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
   const float T = (r * r) * 1.00000095367431640625f;
   HostGuard g;
+  const BSeg capw = mcap_seg(g, La, Lb);
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    mesh_face(g, f, La, Lb, seg != 0, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float pen) {
-      const v3 nw = mwall_world_n(W, nl);
-      out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
+    mesh_face(g, f, capw, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float dist) {
+      put(out, n, tau, mwall_world_n(W, nl), r, dist);
       ++n;
     });
   }
   return n;
 }
 // the same contacts through the wave walk's decomposition: every candidate on its own, the
-// lexicographic (d2, kk) minimum per triangle, the winner's contact
+// lexicographic (d2, kk) minimum per triangle with the tie count, the winner's contact
 extern "C" int host_mesh_contacts_split(const float *w, const float *a, const float *b, int seg, float r, float *out) {
   MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
   const float cz = w[2], hz = w[7];
@@ -70,50 +77,20 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    const MFace F = mface(g, f, La, Lb, W.hx, W.hy, hz);
+    const MFace F = mface(g, f, mcap_seg(g, La, Lb), W.hx, W.hy, hz);
     for (int t = 0; t < 2; ++t) {
-      MCand best; int kb = 0;
-      for (int kk = 0; kk < 8; ++kk) {
-        const MCand c = mface_cand(g, F, seg != 0, t, kk);
-        if (kk == 0 || c.d2 < best.d2 || (c.d2 == best.d2 && kk < kb)) { best = c; kb = kk; }
+      // (the wave walk's reduction: NaN distances enter as +inf, lexicographic (d2, kk) minimum)
+      MCand c[4]; MCand best; int kb = 0;
+      for (int kk = 0; kk < 4; ++kk) {
+        c[kk] = mface_cand(g, F, t, kk);
+        c[kk].d2 = mcand_key(c[kk].d2);
+        if (kk == 0 || c[kk].d2 < best.d2 || (c[kk].d2 == best.d2 && kk < kb)) { best = c[kk]; kb = kk; }
       }
-      float tau, pen; v3 nl;
-      if (mface_contact(g, F, best, r, T, tau, nl, pen)) {
-        const v3 nw = mwall_world_n(W, nl);
-        out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
-        ++n;
-      }
-    }
-  }
-  return n;
-}
-// the same with the branch-free candidates of the cooperative walk (mface_cand_bf)
-extern "C" int host_mesh_contacts_split_bf(const float *w, const float *a, const float *b, int seg, float r, float *out) {
-  MWall W; W.cx = w[0]; W.cy = w[1]; W.c = w[3]; W.s = w[4]; W.hx = w[5]; W.hy = w[6];
-  const float cz = w[2], hz = w[7];
-  const v3 La = mwall_local(W, cz, V(a[0], a[1], a[2]));
-  const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
-  const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
-  const float T = (r * r) * 1.00000095367431640625f;
-  HostGuard g;
-  int n = 0;
-  for (int f = 0; f < 6; ++f) {
-    if (!((fm >> f) & 1u)) continue;
-    const MFace F = mface(g, f, La, Lb, W.hx, W.hy, hz);
-    for (int t = 0; t < 2; ++t) {
-      MCand best; int kb = 0;
-      for (int kk = 0; kk < 8; ++kk) {
-        const MCand c = mface_cand_bf(g, F, seg != 0, t, kk);
-        const MCand c0 = mface_cand(g, F, seg != 0, t, kk);
-        if (memcmp(&c, &c0, sizeof(MCand)) != 0) return -1000 - kk;  // the forms disagree
-        if (kk == 0 || c.d2 < best.d2 || (c.d2 == best.d2 && kk < kb)) { best = c; kb = kk; }
-      }
-      float tau, pen; v3 nl;
-      if (mface_contact(g, F, best, r, T, tau, nl, pen)) {
-        const v3 nw = mwall_world_n(W, nl);
-        out[5 * n] = tau; out[5 * n + 1] = nw.x; out[5 * n + 2] = nw.y; out[5 * n + 3] = nw.z; out[5 * n + 4] = pen;
-        ++n;
-      }
+      int neq = 0;
+      for (int kk = 0; kk < 4; ++kk) neq += c[kk].d2 == best.d2;
+      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties(g, F, t); ++g_ties; }
+      float tau, dist; v3 nl;
+      if (mface_contact(g, F, best, r, T, tau, nl, dist)) { put(out, n, tau, mwall_world_n(W, nl), r, dist); ++n; }
     }
   }
   return n;
@@ -134,7 +111,6 @@ def host_mesh(tmp_path_factory):
     FP = C.POINTER(C.c_float)
     lib.host_mesh_contacts.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     lib.host_mesh_contacts_split.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
-    lib.host_mesh_contacts_split_bf.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
     return lib
 
 
@@ -163,16 +139,14 @@ def test_kernel_mesh_code_equals_oracle_bitwise(host_mesh):
         pa = (centre + half * d).astype(np.float32)
         pb = (centre - half * d).astype(np.float32) if seg else pa.copy()
         ref = orc.mesh_contacts(w, pa, pb, bool(seg), float(r))
-        out = np.zeros((12, 5), np.float32)
+        out = np.zeros((12, 6), np.float32)
         n = host_mesh.host_mesh_contacts(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out))
         got = out[:n]
         assert got.shape == ref.shape and np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
             (it, deg, w, pa, pb, seg, got, ref)
-        out2 = np.zeros((12, 5), np.float32)
+        out2 = np.zeros((12, 6), np.float32)
         n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
         assert n2 == n and np.array_equal(out2[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split", out2[:n2], ref)
-        n3 = host_mesh.host_mesh_contacts_split_bf(_p(w), _p(pa), _p(pb), int(seg), float(r), _p(out2))
-        assert n3 == n and np.array_equal(out2[:n3].view(np.uint32), ref.view(np.uint32)), (it, "split_bf", n3, ref)
         n_cases += 1
         n_contacts += n
     assert n_contacts > 2000, n_contacts
@@ -195,12 +169,44 @@ def test_kernel_mesh_code_non_finite_segments(host_mesh):
                 if rng.uniform() < 0.3:
                     p[k] = np.float32(bad[rng.integers(len(bad))])
         ref = orc.mesh_contacts(w, pa, pb, True, 0.08)
-        out = np.zeros((12, 5), np.float32)
+        out = np.zeros((12, 6), np.float32)
         n = host_mesh.host_mesh_contacts(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
         assert n == len(ref) and np.array_equal(out[:n].view(np.uint32), ref.view(np.uint32)), (it, pa, pb, n, ref)
         n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
         assert n2 == len(ref) and np.array_equal(out[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split", pa, pb)
-        n3 = host_mesh.host_mesh_contacts_split_bf(_p(w), _p(pa), _p(pb), 1, 0.08, _p(out))
-        assert n3 == len(ref) and np.array_equal(out[:n3].view(np.uint32), ref.view(np.uint32)), (it, "split_bf", n3)
         n_cases += 1
     assert n_cases == 3000
+
+
+def test_kernel_mesh_code_grid_cases_with_ties(host_mesh):
+    """Capsules on a 1/16 grid against axis-aligned walls (exact coordinates: segments lying
+    over a face's diagonal or parallel to its edges give candidates at the same distance), so
+    brax's tie rule (the average of the tied candidates' points) runs on both sides and must
+    agree bit for bit."""
+    rng = np.random.default_rng(5)
+    w = np.array([0.0, 0.0, 0.5, 1.0, 0.0, 1.0, 0.5, 0.5], np.float32)
+    host_mesh.host_tie_count()
+    n_contacts = 0
+    for it in range(20000):
+        q = lambda lo, hi: np.float32(rng.integers(int(lo * 16), int(hi * 16) + 1) / 16.0)
+        pa = np.array([q(-1.25, 1.25), q(-0.75, 0.75), q(-0.25, 1.25)], np.float32)
+        if rng.uniform() < 0.5:  # parallel to an axis or to a face diagonal
+            d = np.zeros(3, np.float32)
+            ax = rng.integers(3)
+            d[ax] = q(-0.5, 0.5)
+            if rng.uniform() < 0.5:
+                d[(ax + 1) % 3] = d[ax] * (1 if rng.uniform() < 0.5 else -1)
+            pb = (pa + d).astype(np.float32)
+        else:
+            pb = np.array([q(-1.25, 1.25), q(-0.75, 0.75), q(-0.25, 1.25)], np.float32)
+        seg = rng.uniform() < 0.85
+        r = 0.0625 if seg else 0.25
+        ref = orc.mesh_contacts(w, pa, pb, seg, r)
+        out = np.zeros((12, 6), np.float32)
+        n = host_mesh.host_mesh_contacts(_p(w), _p(pa), _p(pb), int(seg), r, _p(out))
+        assert n == len(ref) and np.array_equal(out[:n].view(np.uint32), ref.view(np.uint32)), (it, pa, pb, out[:n], ref)
+        n2 = host_mesh.host_mesh_contacts_split(_p(w), _p(pa), _p(pb), int(seg), r, _p(out))
+        assert n2 == len(ref) and np.array_equal(out[:n2].view(np.uint32), ref.view(np.uint32)), (it, "split")
+        n_contacts += n
+    assert n_contacts > 1000
+    assert host_mesh.host_tie_count() > 0  # the tie rule was exercised
