@@ -267,6 +267,50 @@ def flops_per_env_step(name: str, B: int = 64, steps: int = 10, flags: int = F_E
         e._L.orc_flops_set_mode(FLOPS_REF_PAIRS)
 
 
+def uniform(key, n: int, lo: float = -1.0, hi: float = 1.0) -> np.ndarray:
+    """jax.random.uniform(key, (n,), lo, hi) in float32 (the C restatement of pob_np.uniform)."""
+    key = np.ascontiguousarray(key, np.uint32)
+    lo_a, hi_a = np.array([lo], np.float32), np.array([hi], np.float32)
+    out = np.zeros(n, np.float32)
+    lib().orc_uniform(_p(key, _UP), n, _p(lo_a), _p(hi_a), 1, _p(out))
+    return out
+
+
+def flops_bench_workload(name: str, total: int, first: int = 0, n: int = 1024, warmup: int = 20, steps: int = 200,
+                         flags: int = F_EPISODE | F_AUTORESET, episode_length: int = 1000, mode: int = FLOPS_EXECUTED,
+                         seed: int = 0, time_budget_s: float = 60.0, **params) -> dict:
+    """Algorithmic FLOPs per env-step on bench.py's own workload: the global envs
+    [first, first + n) of a batch of ``total`` reset from ``split(PRNGKey(seed), total + 1)[1:]``,
+    stepped with the bench's action stream (``key = split(PRNGKey(seed), total + 1)[0]``; per
+    step ``key, k = split(key)``, ``uniform(k, (total, 8), -1, 1)`` rows [first, first + n)),
+    warm-up steps included so that the timed steps see the bench's states.  Per-step means
+    (FLOPs / env) of the timed steps and their spread; single-threaded instrumented build.
+    Stops after ``time_budget_s`` (the count then covers the steps done)."""
+    import time
+    keys = split(np.array([0, seed & 0xFFFFFFFF], np.uint32), total + 1)
+    e = OracleEnv(name, count_flops=True, **params)
+    s = e.reset(np.ascontiguousarray(keys[1 + first:1 + first + n]), first=True)
+    act_key = keys[0].copy()
+    e._L.orc_flops_set_mode(mode)
+    e._L.orc_flops_read_and_reset()
+    per, t0 = [], time.time()
+    try:
+        for t in range(warmup + steps):
+            kk = split(act_key, 2)
+            act_key, k = kk[0].copy(), kk[1].copy()
+            a = np.ascontiguousarray(uniform(k, total * 8).reshape(total, 8)[first:first + n])
+            e.step(s, a, flags=flags, episode_length=episode_length, nthreads=1, inplace=True)
+            per.append(e._L.orc_flops_read_and_reset() / float(n))
+            if time.time() - t0 > time_budget_s:
+                break
+    finally:
+        e._L.orc_flops_set_mode(FLOPS_REF_PAIRS)
+    timed = np.array(per[warmup:] if len(per) > warmup else per, np.float64)
+    return {"mean": float(timed.mean()), "min": float(timed.min()), "median": float(np.median(timed)),
+            "max": float(timed.max()), "warmup_mean": float(np.mean(per[:warmup])) if warmup and per else None,
+            "steps_counted": len(per), "timed_steps_counted": len(timed), "envs": n, "first": first, "total": total}
+
+
 def mesh_contacts(wall, a, b, seg: bool, r: float) -> np.ndarray:
     """The oracle's capsule x TriangulatedBox contacts of one capsule (world end points a, b;
     seg False: the sphere at a) against one wall box (cx, cy, cz, cos, sin, hx, hy, hz):

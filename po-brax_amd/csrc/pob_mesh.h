@@ -17,6 +17,7 @@
 // gap >= r + 1e-3 along some axis between the face rectangle and the segment's bounding box
 // means no triangle of the face is within r).
 #pragma once
+#include <type_traits>
 #include "pob_math.h"
 
 #define POB_MESH_MARGIN 1e-3f
@@ -72,6 +73,11 @@ POB_D uint32_t mesh_face_mask(const v3 A, const v3 B, const float hx, const floa
 // of the four squared distances (ties averaged), the normal (S - P) / (1e-6 + |S - P|), the
 // contact at the triangle point.  The same operations on the same operands as the oracle;
 // jp.clip as selects (bclamp01 / bclamps: the same bits for -0 and NaN on both sides).
+#if defined(POB_MESH_HOST) || defined(POB_MESH_NO_MFENCE)
+#define MFENCE() ((void)0)
+#else
+#define MFENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 POB_D float bclamp01(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
 POB_D float bclamps(float x, float h) { return x > -h ? (x < h ? x : h) : -h; }
 
@@ -326,6 +332,23 @@ POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
   return c;
 }
 
+// the tie path out of line (rare, ~1 400 instructions: inlined, its registers would set the
+// walk's allocation); exact range guards (GuardBranch) whatever the caller's policy -- in range
+// the guard policies give the same bits
+#ifdef POB_MESH_HOST
+POB_D MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
+                               const int t) {
+  HostGuard g;
+  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz), t);
+}
+#else
+__device__ __attribute__((noinline)) MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx,
+                                                           const float hy, const float hz, const int t) {
+  GuardBranch g;
+  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz), t);
+}
+#endif
+
 // the contact of a triangle whose pick is c (oracle capsule_wall_mesh's emission): tau, the
 // wall-frame normal (S - P) / (1e-6 + dist) and dist = |S - P| (the caller's penetration is
 // r - dist, the contact's offset from the segment point along -n is 1e-6 + dist: the triangle
@@ -333,14 +356,13 @@ POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
 // not penetrate (r - dist <= 0).  d2 = 0 (a segment touching or piercing the triangle: its
 // distance is 0 exactly) takes no square root -- kept out of the range guards.
 template <class G>
-POB_D bool mface_contact(G &g, const MFace &F, const MCand &c, const float r, const float T, float &tau, v3 &nl,
+POB_D bool mface_contact(G &g, const int k, const MCand &c, const float r, const float T, float &tau, v3 &nl,
                          float &dist) {
   if (!(c.d2 < T)) return false;
   dist = c.d2 > 0.0f ? g.sqrt(c.d2 > 0.0f ? c.d2 : 1.0f) : 0.0f;
   if (!(r - dist > 0.0f)) return false;
   const float inv = g.rcp(1e-6f + dist);
   const float na = c.da * inv, nb = c.db * inv, nw = c.dw * inv;
-  const int k = F.k;
   nl = V(k == 0 ? nw : na, k == 0 ? na : (k == 1 ? nw : nb), k == 2 ? nw : nb);
   tau = 1.0f - 2.0f * c.u;
   return true;
@@ -360,21 +382,25 @@ POB_D void mpick(MCand &best, bool &tie, const MCand &c) {
 
 // The contacts of face f (0..5) of a wall with half extents (hx, hy, hz) against the capsule's
 // segment (capw: mcap_seg of its wall-frame end points; a sphere has A == B), radius r,
-// T = r^2 (1 + 2^-20): emit(tau, n_local, dist) for triangle 0 then 1 when it penetrates.
-// tau = 1 - 2u places the segment point on the capsule's segment x + tau rotate(e0, q).
+// T = r^2 (1 + 2^-20): for triangle t = 0, 1, hit[t] and its contact (tau, wall-frame normal,
+// dist).  tau = 1 - 2u places the segment point on the capsule's segment x + tau rotate(e0, q).
 // Exact skips (a candidate whose computed d2 is provably >= T can neither win with a contact
 // nor change a winner or a tie below T): an edge whose line the segment's box misses by
 // >= R = r + 1e-3 across it, the segment-plane candidate when its point is >= R off the plane
 // (its triangle points lie in the plane: w = w0 exactly).  (A NaN bound never skips.)
-template <class G, class Fn>
-POB_D void mesh_face(G &g, const int f, const BSeg &capw, const float hx, const float hy, const float hz,
-                     const float r, const float T, Fn &&emit) {
-  const MFace F = mface(g, f, capw, hx, hy, hz);
+struct MFaceOut {
+  bool hit[2];
+  float tau[2], dist[2];
+  v3 nl[2];
+};
+template <class G>
+POB_D MFaceOut mesh_face_contacts(G &g, const int f, const v3 La, const v3 Lb, const float hx, const float hy,
+                                  const float hz, const float r, const float T) {
+  const MFace F = mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz);
   const float R = r + POB_MESH_MARGIN;
-  const F3 A = F.A.p0, B = f3(F.A.p0.a + F.A.d.a, F.A.p0.b + F.A.d.b, F.A.p0.w + F.A.d.w);
-  (void)B;
+  const F3 A = F.A.p0;
   const float ha = F.ha, hb = F.hb, w0 = F.w0;
-  // the segment's box (its end points A and A + d; the same bound as the exact form's)
+  // the segment's box (its end points A and A + d: the points brax's forms produce lie on it)
   const float e_a = A.a + F.A.d.a, e_b = A.b + F.A.d.b, e_w = A.w + F.A.d.w;
   const float amn = fminf(A.a, e_a), amx = fmaxf(A.a, e_a), bmn = fminf(A.b, e_b), bmx = fmaxf(A.b, e_b);
   const float gw = fmaxf(fminf(A.w, e_w) - w0, w0 - fmaxf(A.w, e_w));
@@ -387,14 +413,21 @@ POB_D void mesh_face(G &g, const int f, const BSeg &capw, const float hx, const 
   F3 S, P;
   float u;
   // t0: V0 V1 (bottom), V1 V2 (right), diagonal; t1: diagonal, V2 V3 (top), V0 V3 (left)
+  // (MFENCE: one candidate at a time -- interleaved for ILP they need more registers than the
+  // four-lane kernel's budget leaves)
   if (bottom) { bseg_seg(g, F.A, medge(F, 0), S, P, u); mpick(c[0], tie[0], bcand(S, P, u)); }
+  MFENCE();
   if (right) { bseg_seg(g, F.A, medge(F, 1), S, P, u); mpick(c[0], tie[0], bcand(S, P, u)); }
+  MFENCE();
   bseg_seg(g, F.A, medge(F, 2), S, P, u);
   const MCand dg = bcand(S, P, u);
   mpick(c[0], tie[0], dg);
   mpick(c[1], tie[1], dg);
+  MFENCE();
   if (top) { bseg_seg(g, F.A, medge(F, 3), S, P, u); mpick(c[1], tie[1], bcand(S, P, u)); }
+  MFENCE();
   if (left) { bseg_seg(g, F.A, medge(F, 4), S, P, u); mpick(c[1], tie[1], bcand(S, P, u)); }
+  MFENCE();
   const F3 sp = f3fma(F.A.d, F.tt, F.A.p0);
   if (!(fabsf(sp.w - w0) >= R)) {
 #pragma unroll
@@ -402,16 +435,49 @@ POB_D void mesh_face(G &g, const int f, const BSeg &capw, const float hx, const 
       BTri Tr = mtri(F, t);
       Tr.idet = g.rcp(FMA(Tr.a, Tr.c, -(Tr.b * Tr.b)));
       mpick(c[t], tie[t], bcand(sp, btri_point(Tr, sp), F.tt));
+      MFENCE();
     }
   }
+  MFaceOut o;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     MCand ct = c[t];
-    if (tie[t] && ct.d2 < T) ct = mtri_pick_ties(g, F, t);  // (rare: two candidates at one distance)
-    float tau, dist;
-    v3 nl;
-    if (mface_contact(g, F, ct, r, T, tau, nl, dist)) emit(tau, nl, dist);
+    // (rare: two candidates at one distance; the face is formed again from the end points so
+    // that its terms need not stay live through the candidates)
+    if (tie[t] && ct.d2 < T) ct = mtri_pick_ties_ool(f, La, Lb, hx, hy, hz, t);
+    o.tau[t] = 0.0f; o.dist[t] = 0.0f; o.nl[t] = V(0.0f, 0.0f, 0.0f);
+    o.hit[t] = mface_contact(g, f >> 1, ct, r, T, o.tau[t], o.nl[t], o.dist[t]);
   }
+  return o;
+}
+#ifndef POB_MESH_HOST
+// out of line (GuardBranch only: stateless): the face's working set leaves the caller's
+// register allocation -- the caller saves its live registers around the call, i.e. only when
+// a lane of the wave has a face item (POB_MESH_NOINLINE)
+__device__ __attribute__((noinline)) MFaceOut mesh_face_ool(const int f, const v3 La, const v3 Lb, const float hx,
+                                                         const float hy, const float hz, const float r, const float T) {
+  GuardBranch g;
+  return mesh_face_contacts(g, f, La, Lb, hx, hy, hz, r, T);
+}
+#endif
+#ifndef POB_MESH_NOINLINE
+#define POB_MESH_NOINLINE 0
+#endif
+// emit(tau, n_local, dist) for triangle 0 then 1 when it penetrates
+template <class G, class Fn>
+POB_D void mesh_face(G &g, const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
+                     const float r, const float T, Fn &&emit) {
+#if POB_MESH_NOINLINE && !defined(POB_MESH_HOST)
+  if constexpr (std::is_same<G, GuardBranch>::value) {
+    const MFaceOut o = mesh_face_ool(f, La, Lb, hx, hy, hz, r, T);
+    if (o.hit[0]) emit(o.tau[0], o.nl[0], o.dist[0]);
+    if (o.hit[1]) emit(o.tau[1], o.nl[1], o.dist[1]);
+    return;
+  }
+#endif
+  const MFaceOut o = mesh_face_contacts(g, f, La, Lb, hx, hy, hz, r, T);
+  if (o.hit[0]) emit(o.tau[0], o.nl[0], o.dist[0]);
+  if (o.hit[1]) emit(o.tau[1], o.nl[1], o.dist[1]);
 }
 
 // wall-frame normal -> world (oracle: (nx c - ny s, ny c + nx s, nz) as fmaf(-ny, s, nx c), ..)
@@ -484,8 +550,7 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
       const v3 La = mwall_local(W, cz, A);
       const v3 Lb = seg ? mwall_local(W, cz, B) : La;
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      const BSeg capw = mcap_seg(g, La, Lb);
-      mesh_face(g, bit & 7, capw, W.hx, W.hy, hz, r, T,
+      mesh_face(g, bit & 7, La, Lb, W.hx, W.hy, hz, r, T,
                 [&](const float tau, const v3 nl, const float dist) {
         apply(s, bit, tau, mwall_world_n(W, nl), dist);
       });
@@ -579,9 +644,9 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     if (gv && kk == kmin) {
       const float T = (ro * ro) * 1.00000095367431640625f;
       MCand ct = c;
-      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties(g, F, tri);  // (rare: brax's tie average)
+      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties_ool(mo & 7, La, Lb, W.hx, W.hy, hz, tri);  // (rare: brax's tie average)
       v3 nl;
-      hit = mface_contact(g, F, ct, ro, T, tau, nl, dst);
+      hit = mface_contact(g, F.k, ct, ro, T, tau, nl, dst);
       if (hit) nw = mwall_world_n(W, nl);
     }
     // the owners take their items' triangles in order: the winners' lanes first (all four

@@ -105,16 +105,35 @@ POB_D float qground_r(csys_t &S, const float *LT, int c) {
 struct QGround {
   float pen[2];
 };
-// The lane's wall contacts (pob_mesh.h, brax capsule x TriangulatedBox) of a collide substep:
-// the bodies' capsule segments at detection -- a = x + rotate(e0, q), b = x - rotate(e0, q)
-// (torso: the sphere centre a) -- and, per body, the faces that produced a contact (mc[l]
-// bit 8 w + f: face f of wall w).  The velocity pass re-walks exactly those faces from the
-// stored segments (the same operations on the same operands: the same contacts in the same
-// order) instead of keeping every contact in registers.
+// The lane's bodies' capsule segments at one pose -- a = x + rotate(e0, q), b = x - rotate(e0, q)
+// (torso: the sphere centre a) -- for the face cull and the static (sys.info / legacy) walk.
 struct QMesh {
   v3 a[QNB], b[QNB];
-  uint64_t mc[QNB];  // per body: the faces that produced a contact (bit 8 w + f)
 };
+// The lane's wall contacts of a collide substep (pob_mesh.h, brax capsule x TriangulatedBox):
+// the position pass walks the lane's face items with each segment formed from the detection
+// pose when the walk needs it (x, q: the pose the position pass projects from, unchanged until
+// its end), applies every contact as it is found and keeps the first QK (body, tau, n, dist)
+// in a private array for the velocity pass.  A lane with more keeps its detection-time
+// segments instead (a second private array, written only then) and its velocity pass re-walks
+// every face the cull keeps from them -- the same operations on the same operands: the same
+// contacts in the same order.  Nothing of this is live in registers between the passes but
+// the count, so the walk's working set does not push the substep's state out of the 128-VGPR
+// budget.
+#define QK 8
+struct QWalls {
+  int nct;                // wall contacts of the position pass
+  float c[6 * QK];        // the first QK: body, tau, n, dist
+  float seg[6 * QNB];     // nct > QK only: the segments a, b of the three bodies
+};
+#ifndef POB_QUAD_WAVE_WALK
+#define POB_QUAD_WAVE_WALK 0  // 1: the wave-cooperative face walk (pob_mesh.h mesh_wave_walk)
+#endif
+#if POB_QUAD_WAVE_WALK
+#define QWALK mesh_wave_walk
+#else
+#define QWALK mesh_lane_walk
+#endif
 
 // The Ant's capsules (checked by pob_system.cpp) have opposite end points +-e0 in the body
 // xy-plane, so one rotation rv = rotate(e0, q) serves both (rotate(-e0) = -rv exactly), and a
@@ -211,17 +230,137 @@ POB_D void qput3(const int l, v3 (&a)[QNB], const v3 v) {
   a[0] = vsel3(l == 0, v, a[0]); a[1] = vsel3(l == 1, v, a[1]); a[2] = vsel3(l == 2, v, a[2]);
 }
 
+// body l's segment formed from the pose (x, q): qmesh_segments' operations for one body
+POB_D void qpose_seg(csys_t &S, const float *LT, const QBody &b, const int l, v3 &A, v3 &B, float &r, bool &seg) {
+  const v3 x = qpick3(l, b.x);
+  const v3 rv = qrot_xy(qcap_end(S, LT, l == 0 ? 1 : l, 0), qpick4(l, b.q));
+  A = l == 0 ? x : vadd(x, rv);
+  B = l == 0 ? x : vsub(x, rv);
+  r = l == 0 ? S.cap_r[0] : LT[POB_LEG_BODY(l) + 1];
+  seg = l != 0;
+}
+
+// Wall contact detection of a collide substep, at the pose the position pass projects from
+// (after the kinetic update, before the joint projection: the face walk's working set then
+// meets only the pose -- the velocities are dead until the velocity projection rewrites them,
+// the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
+// order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
+// its segments for the out-of-line re-walks (qwalls_rewalk).
+template <bool WALLS>
+POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws) {
+  ws.nct = 0;
+  if (!WALLS) return;
+  csys_t &S = *launder(Sp);
+  GuardBranch g;
+  const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
+  uint64_t M[QNB];
+  {
+    QMesh ms;
+    qmesh_segments(S, LT, b, rv_leg, ms);
+    const uint32_t lw = qwall_mask(S, b);
+    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
+  }
+#ifdef POB_EXP_NO_WALK
+  return;  // timing experiment only: broadphase and face cull, no face walk
+#endif
+#ifdef POB_EXP_WALK_DEAD
+  if (S.n_walls < 64) return;  // timing experiment only: the walk compiled in, never run
+#endif
+  if (!__any((M[0] | M[1] | M[2]) != 0ull)) return;
+  QWALK<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
+             [&](const int l, const int, const float tau, const v3 n, const float dist) {
+    if (ws.nct < QK) {
+      float *c = ws.c + 6 * ws.nct;
+      c[0] = (float)l; c[1] = tau; c[2] = n.x; c[3] = n.y; c[4] = n.z; c[5] = dist;
+    }
+    ++ws.nct;
+  });
+  if (ws.nct > QK) {  // (rare) the detection-time segments for the re-walks
+    QMesh ms;
+    qmesh_segments(S, LT, b, rv_leg, ms);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      ws.seg[6 * l] = ms.a[l].x; ws.seg[6 * l + 1] = ms.a[l].y; ws.seg[6 * l + 2] = ms.a[l].z;
+      ws.seg[6 * l + 3] = ms.b[l].x; ws.seg[6 * l + 4] = ms.b[l].y; ws.seg[6 * l + 5] = ms.b[l].z;
+    }
+  }
+}
+
+// One wall contact applied at the position level (penetration r - dist, the contact at the
+// triangle point pe - (1e-6 + dist) n) / at the velocity level (at the post-projection pose)
+template <class G>
+POB_D void qwall_pos_one(G &g, csys_t &S, const HCon &SC, const float *LT, const v3 (&x)[QNB], const q4 (&q)[QNB],
+                         const v3 (&px)[QNB], const q4 (&pq)[QNB], const int l, const float tau, const v3 n,
+                         const float dist, v3 (&DX)[QNB], v3 (&DA)[QNB]) {
+  const v3 xl = qpick3(l, x);
+  const q4 ql = qpick4(l, q);
+  const v3 pe = l == 0 ? xl : qseg_point(LT, l, xl, ql, tau);
+  v3 dx = qpick3(l, DX), da = qpick3(l, DA);
+  owall_position(g, SC, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), xl, ql, qpick4(l, pq),
+                 qpick3(l, px), dx, da);
+  qput3(l, DX, dx);
+  qput3(l, DA, da);
+}
+template <class G>
+POB_D void qwall_vel_one(G &g, csys_t &S, const HCon &SC, const float *LT, const v3 (&x)[QNB], const q4 (&q)[QNB],
+                         const v3 (&v)[QNB], const v3 (&w)[QNB], const int l, const float tau, const v3 n,
+                         const float dist, v3 (&dV)[QNB], v3 (&dW)[QNB]) {
+  const v3 xl = qpick3(l, x);
+  const v3 pe = l == 0 ? xl : qseg_point(LT, l, xl, qpick4(l, q), tau);
+  v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
+  ocontact_vel_pe(g, SC, false, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), xl, qpick3(l, v),
+                  qpick3(l, w), dv, dw);
+  qput3(l, dV, dv);
+  qput3(l, dW, dw);
+}
+
+// The re-walk of a lane whose contacts overflowed the store (rare), out of line so that the
+// walk's registers stay out of the position and velocity passes: every face the cull keeps
+// over every wall, from the detection-time segments (the broadphase only skips walls whose
+// faces are all culled), each contact applied in walk order.  State through a private block.
+struct QOvf {
+  v3 x[QNB], px[QNB], v[QNB], w[QNB], a[QNB], b[QNB], d0[QNB], d1[QNB];
+  q4 q[QNB], pq[QNB];
+  float fric;
+  int on;
+};
+template <bool VEL>
+__device__ __attribute__((noinline)) void qwalls_rewalk(csys_t *Sp, const float *LT, const float *WT, QOvf *st) {
+  csys_t &S = *launder(Sp);
+  GuardBranch g;
+  const HCon SC{st->fric, S.inv_h};
+  v3 x[QNB], px[QNB], v[QNB], w[QNB], d0[QNB], d1[QNB];
+  q4 q[QNB], pq[QNB];
+  QMesh ms;
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) {
+    x[l] = st->x[l]; px[l] = st->px[l]; v[l] = st->v[l]; w[l] = st->w[l]; d0[l] = st->d0[l]; d1[l] = st->d1[l];
+    q[l] = st->q[l]; pq[l] = st->pq[l]; ms.a[l] = st->a[l]; ms.b[l] = st->b[l];
+  }
+  const uint32_t wa = st->on ? (1u << S.n_walls) - 1u : 0u;
+  uint64_t M[QNB];
+  qmesh_items(S, LT, WT, wa | (wa << 8) | (wa << 16), ms, M);
+  QWALK<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+             [&](const int l, const int, const float tau, const v3 n, const float dist) {
+    if (VEL) qwall_vel_one(g, S, SC, LT, x, q, v, w, l, tau, n, dist, d0, d1);
+    else qwall_pos_one(g, S, SC, LT, x, q, px, pq, l, tau, n, dist, d0, d1);
+  });
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) { st->d0[l] = d0[l]; st->d1[l] = d1[l]; }
+}
+
 // Position pass of a collide substep: ground contacts (ground first per body, oracle order),
-// then every wall contact as it is detected; the segments and the contact walls are kept in
-// ms for the velocity pass
+// then the wall contacts from the store in detection order
 template <bool WALLS>
 POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const Lds &L, QGround &gc,
-                              QMesh &ms, v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
+                              const QWalls &ws, v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
   GuardBranch g;
-  const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
   {
+    const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
     v3 pe[2];
     qground_detect(S, LT, b, rv_leg, gc, pe);
 #pragma unroll
@@ -233,44 +372,43 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
                          L.get4(QL_PQ(l)), L.get3(QL_PX(l)), DX[l], DA[l]);
     }
   }
-  ms.mc[0] = 0ull; ms.mc[1] = 0ull; ms.mc[2] = 0ull;
-  if (!WALLS) return;
+  if (!WALLS || !__any(ws.nct != 0)) return;
   POB_FENCE();
-  qmesh_segments(S, LT, b, rv_leg, ms);
-  uint64_t M[QNB];
-  {
-    const uint32_t lw = qwall_mask(S, b);
-    qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
+  v3 px[QNB];
+  q4 pq[QNB];
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) { px[l] = L.get3(QL_PX(l)); pq[l] = L.get4(QL_PQ(l)); }
+  const bool ovf = ws.nct > QK;
+  const int nc = ovf ? 0 : ws.nct;
+#pragma unroll 1
+  for (int i = 0; i < QK; ++i) {
+    if (!__any(i < nc)) break;
+    if (i < nc) {
+      const float *c = ws.c + 6 * i;
+      qwall_pos_one(g, S, SC, LT, b.x, b.q, px, pq, (int)c[0], c[1], V(c[2], c[3], c[4]), c[5], DX, DA);
+    }
   }
-#ifdef POB_EXP_NO_WALK
-  return;  // timing experiment only: broadphase and face cull, no face walk
-#endif
-#ifdef POB_EXP_WALK_DEAD
-  if (S.n_walls < 64) return;  // timing experiment only: the walk compiled in, never run
-#endif
-  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
-                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                      [&](const int l, const int bit, const float tau, const v3 n, const float dist) {
-    const v3 x = qpick3(l, b.x);
-    const q4 q = qpick4(l, b.q);
-    const v3 pe = l == 0 ? x : qseg_point(LT, l, x, q, tau);
-    v3 dx = qpick3(l, DX), da = qpick3(l, DA);
-    // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
-    owall_position(g, SC, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), x, q,
-                   L.get4(QL_PQ(0) + 7 * l), L.get3(QL_PX(0) + 7 * l), dx, da);
-    qput3(l, DX, dx);
-    qput3(l, DA, da);
-    ms.mc[0] |= l == 0 ? 1ull << bit : 0ull;
-    ms.mc[1] |= l == 1 ? 1ull << bit : 0ull;
-    ms.mc[2] |= l == 2 ? 1ull << bit : 0ull;
-  });
+  if (__any(ovf)) {
+    QOvf st;
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      st.x[l] = b.x[l]; st.q[l] = b.q[l]; st.px[l] = px[l]; st.pq[l] = pq[l]; st.d0[l] = DX[l]; st.d1[l] = DA[l];
+      st.a[l] = V(ws.seg[6 * l], ws.seg[6 * l + 1], ws.seg[6 * l + 2]);
+      st.b[l] = V(ws.seg[6 * l + 3], ws.seg[6 * l + 4], ws.seg[6 * l + 5]);
+    }
+    st.fric = fric;
+    st.on = ovf ? 1 : 0;
+    qwalls_rewalk<false>(Sp, LT, WT, &st);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { DX[l] = st.d0[l]; DA[l] = st.d1[l]; }
+  }
 }
 
-// Velocity pass: ground contacts, then the wall contacts re-derived from the stored segments
-// (contact points x + tau rotate(e0, q) at the post-projection pose)
+// Velocity pass: ground contacts, then the wall contacts from the store (contact points
+// x + tau rotate(e0, q) at the post-projection pose)
 template <bool WALLS>
 POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const QGround &gc,
-                              const QMesh &ms, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
+                              const QWalls &ws, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
   GuardBranch g;
@@ -285,24 +423,35 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
                       b.v[l], b.w[l], dV[l], dW[l]);
     }
   }
-  if (!WALLS || !__any((ms.mc[0] | ms.mc[1] | ms.mc[2]) != 0ull)) return;
+  if (!WALLS || !__any(ws.nct != 0)) return;
 #ifdef POB_EXP_NO_VWALK
-  return;  // timing experiment only: no velocity-pass re-walk
+  return;  // timing experiment only: no velocity-pass wall contacts
 #endif
   POB_FENCE();
-  uint64_t M[QNB];
-  M[0] = ms.mc[0]; M[1] = ms.mc[1]; M[2] = ms.mc[2];
-  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
-                      [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
-                      [&](const int l, const int, const float tau, const v3 n, const float dist) {
-    const v3 x = qpick3(l, b.x);
-    const v3 pe = l == 0 ? x : qseg_point(LT, l, x, qpick4(l, b.q), tau);
-    v3 dv = qpick3(l, dV), dw = qpick3(l, dW);
-    ocontact_vel_pe(g, SC, false, q_cap_r(S, LT, l) - dist, pe, n, 1e-6f + dist, q_inv_mass(S, LT, l), x,
-                    qpick3(l, b.v), qpick3(l, b.w), dv, dw);
-    qput3(l, dV, dv);
-    qput3(l, dW, dw);
-  });
+  const bool ovf = ws.nct > QK;
+  const int nc = ovf ? 0 : ws.nct;
+#pragma unroll 1
+  for (int i = 0; i < QK; ++i) {
+    if (!__any(i < nc)) break;
+    if (i < nc) {
+      const float *c = ws.c + 6 * i;
+      qwall_vel_one(g, S, SC, LT, b.x, b.q, b.v, b.w, (int)c[0], c[1], V(c[2], c[3], c[4]), c[5], dV, dW);
+    }
+  }
+  if (__any(ovf)) {
+    QOvf st;
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) {
+      st.x[l] = b.x[l]; st.q[l] = b.q[l]; st.v[l] = b.v[l]; st.w[l] = b.w[l]; st.d0[l] = dV[l]; st.d1[l] = dW[l];
+      st.a[l] = V(ws.seg[6 * l], ws.seg[6 * l + 1], ws.seg[6 * l + 2]);
+      st.b[l] = V(ws.seg[6 * l + 3], ws.seg[6 * l + 4], ws.seg[6 * l + 5]);
+    }
+    st.fric = fric;
+    st.on = ovf ? 1 : 0;
+    qwalls_rewalk<true>(Sp, LT, WT, &st);
+#pragma unroll
+    for (int l = 0; l < QNB; ++l) { dV[l] = st.d0[l]; dW[l] = st.d1[l]; }
+  }
 }
 
 // sys.info(qp).contact and the legacy collisions: detection and the velocity-level response
@@ -493,9 +642,12 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
       b.q[l] = qnormalize(q);
     }
   }
+  // 2b. wall contact detection (collide substeps), at the pose the projection starts from
+  QWalls ws;
+  ws.nct = 0;
+  if (COLLIDE) qwalls_detect<WALLS>(Sp, LT, WT, b, ws);
   // 3. position projection
   QGround gc;
-  QMesh ms;
   {
     v3 DX[QNB];
     v3 DA[QNB];
@@ -522,7 +674,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
       qtorso_add<2>(DX[0], DA[0], tq, imp0);
       qtorso_add<3>(DX[0], DA[0], tq, imp0);
     }
-    if (COLLIDE) qcontacts_position<WALLS>(Sp, LT, WT, b, L, gc, ms, DX, DA, fric);
+    if (COLLIDE) qcontacts_position<WALLS>(Sp, LT, WT, b, L, gc, ws, DX, DA, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.x[l] = vadd(b.x[l], DX[l]);
@@ -546,7 +698,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontacts_velocity<WALLS>(Sp, LT, WT, b, gc, ms, dV, dW, fric);
+    qcontacts_velocity<WALLS>(Sp, LT, WT, b, gc, ws, dV, dW, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);

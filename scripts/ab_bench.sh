@@ -15,7 +15,7 @@ for env in ${ENVS:-ant_heavenhell}; do
       for lib in $libs; do
         tag=$(basename $lib .so)
         if [ -d $lib ]; then pk="POB_PKG_ROOT=$PWD/$lib POB_LIB=$PWD/$lib/po_brax_amd/libpob.so"; else pk="POB_LIB=$PWD/$lib"; fi
-        env $pk timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-200} --env $env --batch $B ${EXTRA:-} \
+        env $pk timeout -k 10 120 python bench.py --no-cpu-baseline --flop-envs 0 --steps ${STEPS:-200} --env $env --batch $B ${EXTRA:-} \
           > gpurun_out/ab/$tag.$env.$B.$r.json 2>/dev/null || exit 1
       done
     done

@@ -21,6 +21,6 @@ i=0
 IFS=';' read -ra CFG <<< "${BENCH:---env ant_heavenhell --global-batch 4096;--env ant_tag --global-batch 8192;--env ant_gather --global-batch 16384;--env ant_tag;--env mixed --qp-dtype f16 --global-batch 32768}"
 for c in "${CFG[@]}"; do
   i=$((i + 1))
-  timeout -k 10 120 python bench.py --no-cpu-baseline --steps ${STEPS:-200} $c > $OUT/bench_$i.json 2> $OUT/bench_$i.err || { tail -10 $OUT/bench_$i.err; exit 1; }
+  timeout -k 10 180 python bench.py --no-cpu-baseline --steps ${STEPS:-200} $c > $OUT/bench_$i.json 2> $OUT/bench_$i.err || { tail -10 $OUT/bench_$i.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/bench_$i.json')); print('$c', '%.4e' % d['value'], d['roofline']['kernel_ms'])"
 done

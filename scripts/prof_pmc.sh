@@ -9,7 +9,7 @@ TAG=${TAG:?}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 $PWD/bench.py --no-cpu-baseline --steps 30 --warmup 3 $ARGS"
+B="python3 $PWD/bench.py --no-cpu-baseline --flop-envs 0 --steps 30 --warmup 3 $ARGS"
 cd /tmp
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- $B > $OUT/trace.bench.json 2> $OUT/trace.err || { tail -5 $OUT/trace.err; exit 1; }
 i=0

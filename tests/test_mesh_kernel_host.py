@@ -53,11 +53,10 @@ extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b
   const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
   const float T = (r * r) * 1.00000095367431640625f;
   HostGuard g;
-  const BSeg capw = mcap_seg(g, La, Lb);
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    mesh_face(g, f, capw, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float dist) {
+    mesh_face(g, f, La, Lb, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float dist) {
       put(out, n, tau, mwall_world_n(W, nl), r, dist);
       ++n;
     });
@@ -88,9 +87,9 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
       }
       int neq = 0;
       for (int kk = 0; kk < 4; ++kk) neq += c[kk].d2 == best.d2;
-      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties(g, F, t); ++g_ties; }
+      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties_ool(f, La, Lb, W.hx, W.hy, hz, t); ++g_ties; }
       float tau, dist; v3 nl;
-      if (mface_contact(g, F, best, r, T, tau, nl, dist)) { put(out, n, tau, mwall_world_n(W, nl), r, dist); ++n; }
+      if (mface_contact(g, F.k, best, r, T, tau, nl, dist)) { put(out, n, tau, mwall_world_n(W, nl), r, dist); ++n; }
     }
   }
   return n;
