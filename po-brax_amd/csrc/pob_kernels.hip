@@ -827,6 +827,12 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 
   POB_TS(1);
   // ---- physics (10 substeps in registers + the lane's LDS slots)
+#ifndef POB_QUAD_TWO_PASS
+#define POB_QUAD_TWO_PASS 1
+#endif
+#ifndef POB_QUAD_NEAR_MARGIN
+#define POB_QUAD_NEAR_MARGIN 0.5f
+#endif
   float jang[QNJ], jvel[QNJ];
   v3 cvl[QNB], cal[QNB];
   TaskOut t;
@@ -845,12 +851,54 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #pragma nounroll
       for (int it = 0; it < Sp->substeps; ++it) qlegacy_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls);
     } else {
-#pragma nounroll
 #if defined(POB_EXP_NO_COLLIDE)
+#pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false, S.friction);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
+#pragma nounroll
     for (int it = 0; it < 0 * iters; ++it) qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, false, S.friction);  // timing experiment only
 #else
+    // Two passes (wave-uniform): a wave whose lanes are all clear of the walls' broadphase boxes
+    // (grown by POB_QUAD_NEAR_MARGIN) at the start of the step runs the substeps without the
+    // wall code and checks the broadphase of every collide substep; if a lane met one, the wave
+    // reloads the step's state and runs the wall pass (the no-wall pass is exact when it
+    // completes: every wall pass item list would have been empty).  The wall pass's registers
+    // and code then cost only the waves near a wall.
+    // (AntGather only: its ants start at the arena's centre, so whole waves run the no-wall
+    // pass -- 0.272 -> 0.122 ms at B = 65 536; the HH / TAG waves nearly always hold an ant near
+    // a wall, and the second copy of the substep loop costs them 5-10 %, profiles/r5m)
+    constexpr bool TWO = KIND == POB_GATHER && POB_QUAD_TWO_PASS;
+    int pass = TWO ? (__any(qwall_mask_margin(S, bd, POB_QUAD_NEAR_MARGIN) != 0u) ? 1 : 0) : 1;
+    for (;;) {
+    if (pass == 0) {
+      bool near = false;
+#pragma nounroll
+      for (int it = 0; it < 2 * iters; ++it) {
+#if POB_QUAD_PRIO == 1
+        const int lvl = (it * 4) / (2 * iters);
+        if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
+        qpbd_substep<false, true>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric, &near);
+      }
+      if (!__any(near)) break;
+      // a lane met a wall's broadphase: the step again, from its state, with the walls
+      pass = 1;
+#pragma unroll
+      for (int l = 0; l < QNB; ++l) {
+        const int g = qbody_global(l, k);
+        bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
+        bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
+        bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
+        bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
+        Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f));
+        Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f));
+      }
+      continue;
+    }
+#pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) {
       // Issue priority falls with progress, so a SIMD's four waves (one per block) advance
       // together: with the default oldest-first arbitration the first wave finishes early
@@ -877,6 +925,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       else __builtin_amdgcn_s_setprio(0);
 #endif
       qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);
+    }
+    break;
     }
 #endif
     }

@@ -558,16 +558,20 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
   }
 }
 
-template <int NB, class G, class SegOf, class Apply>
+// (LANE_FALLBACK false: the caller guarantees all 64 lanes active and handles the per-lane
+// walk itself -- the four-lane kernel keeps it out of line)
+template <int NB, bool LANE_FALLBACK = true, class G, class SegOf, class Apply>
 POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
                           Apply &&apply) {
+  if (LANE_FALLBACK) {
 #ifdef POB_MESH_LANE_WALK
-  if (true) {  // A/B build switch: the per-lane walk everywhere
+    if (true) {  // A/B build switch: the per-lane walk everywhere
 #else
-  if (__ballot(1) != ~0ull) {
+    if (__ballot(1) != ~0ull) {
 #endif
-    mesh_lane_walk<NB>(g, WT, cz, hz, M, seg_of, apply);
-    return;
+      mesh_lane_walk<NB>(g, WT, cz, hz, M, seg_of, apply);
+      return;
+    }
   }
   const int lane = (int)__lane_id();
   const int grp = lane >> 3, tri = (lane >> 2) & 1, kk = lane & 3;

@@ -127,7 +127,7 @@ struct QWalls {
   float seg[6 * QNB];     // nct > QK only: the segments a, b of the three bodies
 };
 #ifndef POB_QUAD_WAVE_WALK
-#define POB_QUAD_WAVE_WALK 0  // 1: the wave-cooperative face walk (pob_mesh.h mesh_wave_walk)
+#define POB_QUAD_WAVE_WALK 1  // 1: the wave-cooperative face walk (pob_mesh.h mesh_wave_walk)
 #endif
 #if POB_QUAD_WAVE_WALK
 #define QWALK mesh_wave_walk
@@ -165,6 +165,28 @@ POB_D uint32_t qwall_mask(csys_t &S, const QBody &b) {
   for (int w = 0; w < POB_MAXW; ++w) {
     // all POB_MAXW boxes loaded at once, w < nw as a predicate
     const float lx = S.wall_lo[w][0], ly = S.wall_lo[w][1], hx = S.wall_hi[w][0], hy = S.wall_hi[w][1];
+    const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
+    m |= (near & (w < nw)) ? 1u << w : 0u;
+  }
+  return m;
+}
+
+// the broadphase with every wall box grown by a further margin (the wave's choice of pass at
+// the start of a step: a lane whose grown mask is empty is unlikely to meet a wall's
+// broadphase during the step)
+POB_D uint32_t qwall_mask_margin(csys_t &S, const QBody &b, const float margin) {
+  float mnx = b.x[0].x, mxx = b.x[0].x, mny = b.x[0].y, mxy = b.x[0].y;
+#pragma unroll
+  for (int l = 1; l < QNB; ++l) {
+    mnx = fminf(mnx, b.x[l].x); mxx = fmaxf(mxx, b.x[l].x);
+    mny = fminf(mny, b.x[l].y); mxy = fmaxf(mxy, b.x[l].y);
+  }
+  const int nw = S.n_walls;
+  uint32_t m = 0u;
+#pragma unroll
+  for (int w = 0; w < POB_MAXW; ++w) {
+    const float lx = S.wall_lo[w][0] - margin, ly = S.wall_lo[w][1] - margin;
+    const float hx = S.wall_hi[w][0] + margin, hy = S.wall_hi[w][1] + margin;
     const bool near = (mnx <= hx) & (mxx >= lx) & (mny <= hy) & (mxy >= ly);
     m |= (near & (w < nw)) ? 1u << w : 0u;
   }
@@ -246,12 +268,65 @@ POB_D void qpose_seg(csys_t &S, const float *LT, const QBody &b, const int l, v3
 // the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
 // order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
 // its segments for the out-of-line re-walks (qwalls_rewalk).
+// the face walk of the detection, out of line (POB_QUAD_DETECT_OOL): the kernel's substep keeps
+// its allocation free of the walk's working set; a wave calls it only when one of its lanes
+// has a face item.  The pose comes by value, the store through the private block.
+template <bool LANE>
+POB_D void qwalls_walk(csys_t &S, const float *LT, const float *WT, const QBody &b, uint64_t (&M)[QNB], QWalls &ws) {
+  GuardBranch g;
+#if POB_QUAD_WAVE_WALK
+  if (!LANE) {
+    mesh_wave_walk<QNB, false>(g, WT, S.wall_cz, S.wall_hz, M,
+               [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
+               [&](const int l, const int, const float tau, const v3 n, const float dist) {
+      if (ws.nct < QK) {
+        float *c = ws.c + 6 * ws.nct;
+        c[0] = (float)l; c[1] = tau; c[2] = n.x; c[3] = n.y; c[4] = n.z; c[5] = dist;
+      }
+      ++ws.nct;
+    });
+    return;
+  }
+#endif
+  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
+             [&](const int l, const int, const float tau, const v3 n, const float dist) {
+    if (ws.nct < QK) {
+      float *c = ws.c + 6 * ws.nct;
+      c[0] = (float)l; c[1] = tau; c[2] = n.x; c[3] = n.y; c[4] = n.z; c[5] = dist;
+    }
+    ++ws.nct;
+  });
+}
+#ifndef POB_QUAD_DETECT_OOL
+#define POB_QUAD_DETECT_OOL 0
+#endif
+// (the per-lane walk always out of line: the cooperative walk needs every lane of the wave,
+// so the batch's last wave walks per lane -- rare, and kept out of the substep's code)
+__device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float *LT, const float *WT, v3 x0, v3 x1,
+                                                       v3 x2, q4 q0, q4 q1, q4 q2, uint64_t m0, uint64_t m1,
+                                                       uint64_t m2, QWalls *ws) {
+  csys_t &S = *launder(Sp);
+  QBody b;
+  b.x[0] = x0; b.x[1] = x1; b.x[2] = x2;
+  b.q[0] = q0; b.q[1] = q1; b.q[2] = q2;
+  uint64_t M[QNB] = {m0, m1, m2};
+  ws->nct = 0;
+  qwalls_walk<true>(S, LT, WT, b, M, *ws);
+  return ws->nct;
+}
+
+// Wall contact detection of a collide substep, at the pose the position pass projects from
+// (after the kinetic update, before the joint projection: the face walk's working set then
+// meets only the pose -- the velocities are dead until the velocity projection rewrites them,
+// the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
+// order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
+// its segments for the out-of-line re-walks (qwalls_rewalk).
 template <bool WALLS>
 POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws) {
   ws.nct = 0;
   if (!WALLS) return;
   csys_t &S = *launder(Sp);
-  GuardBranch g;
   const v3 rv_leg = qrot_xy(qcap_end(S, LT, 2, 0), b.q[2]);
   uint64_t M[QNB];
   {
@@ -266,16 +341,29 @@ POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBo
 #ifdef POB_EXP_WALK_DEAD
   if (S.n_walls < 64) return;  // timing experiment only: the walk compiled in, never run
 #endif
+#ifdef POB_EXP_CULL_ONLY
+  {  // timing experiment only: the cull's items kept alive, no walk, the passes compiled in
+    uint32_t k0 = (uint32_t)M[0], k1 = (uint32_t)M[1], k2 = (uint32_t)M[2];
+    asm volatile("" : "+v"(k0), "+v"(k1), "+v"(k2));
+    int z = (int)((k0 ^ k1 ^ k2) & 0u);
+    asm volatile("" : "+v"(z));
+    ws.nct = z;
+    return;
+  }
+#endif
   if (!__any((M[0] | M[1] | M[2]) != 0ull)) return;
-  QWALK<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
-             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
-             [&](const int l, const int, const float tau, const v3 n, const float dist) {
-    if (ws.nct < QK) {
-      float *c = ws.c + 6 * ws.nct;
-      c[0] = (float)l; c[1] = tau; c[2] = n.x; c[3] = n.y; c[4] = n.z; c[5] = dist;
-    }
-    ++ws.nct;
-  });
+#if POB_QUAD_WAVE_WALK
+  if (!POB_QUAD_DETECT_OOL && __ballot(1) == ~0ull) qwalls_walk<false>(S, LT, WT, b, M, ws);
+  else
+#endif
+  ws.nct = qwalls_walk_ool(Sp, LT, WT, b.x[0], b.x[1], b.x[2], b.q[0], b.q[1], b.q[2], M[0], M[1], M[2], &ws);
+#ifdef POB_EXP_NO_APPLY
+  {  // timing experiment only: the walk runs, its contacts are not applied
+    int z = ws.nct & 0;
+    asm volatile("" : "+v"(z));
+    ws.nct = z;
+  }
+#endif
   if (ws.nct > QK) {  // (rare) the detection-time segments for the re-walks
     QMesh ms;
     qmesh_segments(S, LT, b, rv_leg, ms);
@@ -596,10 +684,14 @@ POB_D float quad_friction(const csys_t &S) {
   return f;
 }
 
-// One XPBD substep on a lane quad (see the header comment for the split).
-template <bool WALLS>
+// One XPBD substep on a lane quad (see the header comment for the split).  CHECK (with WALLS
+// false): the substep of the no-wall pass, which still evaluates the wall broadphase of every
+// collide substep at the point the wall pass would (qwalls_detect) and reports a lane whose
+// mask is not empty in *near -- with every mask empty the wall pass finds no face item, so
+// the two passes compute the same bits.
+template <bool WALLS, bool CHECK = false>
 POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const Lds &L,
-                        const bool COLLIDE, const float fric) {
+                        const bool COLLIDE, const float fric, bool *near = nullptr) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
   // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
@@ -646,6 +738,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   QWalls ws;
   ws.nct = 0;
   if (COLLIDE) qwalls_detect<WALLS>(Sp, LT, WT, b, ws);
+  if (CHECK && COLLIDE) *near = *near | (qwall_mask(*launder(Sp), b) != 0u);
   // 3. position projection
   QGround gc;
   {
