@@ -48,6 +48,10 @@ _TASK_READ = {"ant_heavenhell": 6, "ant_gather": 48, "ant_tag": 2, "ant": 0}
 _TASK_WRITE = {"ant_heavenhell": 0, "ant_gather": 48, "ant_tag": 3, "ant": 0}
 _OBS = {"ant_heavenhell": 114, "ant_gather": 211, "ant_tag": 103, "ant": 87}
 MIXED = ("ant_heavenhell", "ant_gather", "ant_tag")  # --env mixed (BASELINE.json config 5)
+# --obs-mask: po_env_mask(env, **kw) (standard_observability_masks.py) of the po-envs; stock
+# Ant: the reference's own POSITION / VELOCITY sets (po_brax/standard_observability_masks.py)
+OBS_MASKS = {"none": None, "no-cfrc": dict(cfrc=False), "position": dict(velocity=False, cfrc=False, task=False),
+             "position+task": dict(velocity=False, cfrc=False)}
 HEADLINE_METRIC = "env-steps/sec AntHeavenHell batch 65536 @1/2/4/8 GPU; % HBM roofline"  # BASELINE.json
 VALU_PEAK_TF = 157.3   # FP32 vector peak, MI355X_MICROARCH.md (chip-level parameters)
 HBM_PEAK_GBS = 8000.0  # HBM3E spec peak
@@ -103,6 +107,13 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
                          "hipGraph (po_brax_amd.rollout); --gather-obs and the sharded gym path are eager")
+    ap.add_argument("--obs-mask", default="none", choices=sorted(OBS_MASKS),
+                    help="observation mask fused into the step kernel (create(..., obs_mask=idx), C ABI v7): "
+                         "the step also stores obs[:, idx] (BASELINE config 2: '--global-batch 4096 "
+                         "--obs-mask no-cfrc')")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch rehearsal without a GPU: parse the arguments, join the process group (gloo), "
+                         "gather the rank table and print the rank-0 line with no measurement")
     ap.add_argument("--legacy-spring", action="store_true",
                     help="brax <= 0.0.12 spring/impulse dynamics (the physics notebooks/ant_tag.ipynb:449 "
                          "pins) instead of PBD")
@@ -118,6 +129,8 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
@@ -128,8 +141,13 @@ def main() -> int:
         ap.error("--gym runs one env kind")
     if args.legacy_spring and args.env == "mixed":
         ap.error("--legacy-spring runs one env kind")
+    if args.obs_mask != "none" and args.env == "mixed":
+        ap.error("--obs-mask runs one env kind")
+    mask = obs_mask_of(args.env, args.obs_mask)
     ranks = rank_devices(dev, world)  # every rank's device, gathered over the process group
     ekw = {"legacy_spring": True} if args.legacy_spring else {}
+    if mask is not None:
+        ekw["obs_mask"] = mask
 
     from po_brax_amd import envs, jumpy
     from po_brax_amd.sharding import ObsGatherer, Shard, shard_keys
@@ -182,7 +200,7 @@ def main() -> int:
 
     do_gather = args.gather_obs and world > 1 and args.env != "mixed"
     gatherer = ObsGatherer(total, obs_of().shape[-1], device=dev) if do_gather else None
-    gather_ms = []
+    gather_ev = []  # (start, end) events of each timed step's all-gather (side stream)
 
     def one_step(t):
         if gym is not None:
@@ -243,12 +261,11 @@ def main() -> int:
             ev_b[k].record()
             if gatherer is not None:
                 p = (gatherer.k - 1) % gatherer.depth
-                gather_ms.append((gatherer._t0[p], gatherer._done[p]))
+                gather_ev.append((gatherer._t0[p], gatherer._done[p]))
         if gatherer is not None:  # the last gather belongs to the timed steps too
             gatherer.result((gatherer.k - 1) % gatherer.depth)
     torch.cuda.synchronize()
-    if gatherer is not None:
-        gather_ms = [a.elapsed_time(b) for a, b in gather_ms]
+    gather_ms = [a.elapsed_time(b) for a, b in gather_ev] if gatherer is not None else []
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -266,11 +283,13 @@ def main() -> int:
     # time whenever the kernel is shorter than it (small batches)
     kern_ms = g0.elapsed_time(g1) / args.steps if roll is not None else eager_ms
     gather_ms = (sum(gather_ms) / len(gather_ms)) if do_gather else None
-    elapsed = torch.tensor([wall, kern_ms, gather_ms or 0.0], dtype=torch.float64,
-                           device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    wall, kern_ms_max = float(elapsed[0]), float(elapsed[1])
+    overlap = gather_overlap(ev_a, ev_b, gather_ev) if do_gather and roll is None else None
+    # every rank's numbers, gathered (the line reports the MAX and the per-rank table)
+    table = gather_rank_stats([wall, kern_ms, gather_ms or 0.0, eager_ms,
+                               _num((overlap or {}).get("overlap_frac")), float(B)],
+                              world, dev if args.dist_backend == "nccl" else torch.device("cpu"))
+    wall, kern_ms_max = max(r[0] for r in table), max(r[1] for r in table)
+    gather_max = max(r[2] for r in table)
     ms_per_step = 1e3 * wall / args.steps
     value = total * args.steps / wall
     finite = bool(torch.isfinite(obs_of()).all())
@@ -286,7 +305,7 @@ def main() -> int:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     qb = 2 if args.qp_dtype == "f16" else 4
     kinds = list(zip(MIXED, mixed_sizes(B))) if args.env == "mixed" else [(args.env, B)]
-    bpe = sum(bytes_per_env_step(n, qb) * b for n, b in kinds) / B
+    bpe = sum(bytes_per_env_step(n, qb) * b for n, b in kinds) / B + 4 * (0 if mask is None else len(mask))
     fw = None
     try:
         import orc  # test-infrastructure oracle: FLOP count of the restated algorithm only
@@ -348,7 +367,13 @@ def main() -> int:
         "hbm": {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
     }
-    prof = committed_profile(args.env, B, args.qp_dtype, args.legacy_spring)
+    build = build_identity()
+    prof, stale = committed_profile(args.env, B, args.qp_dtype, args.legacy_spring, build["lib_sha256"],
+                                    args.obs_mask)
+    if stale is not None and gym is None:  # a profile of this config, but of another build of libpob.so
+        roofline["traffic_stale_profile"] = (f"profiles/{stale['source']} profiled a different libpob.so "
+                                             f"({(stale.get('build') or {}).get('lib_sha256', 'unrecorded')[:12]}); "
+                                             "its counters are not reported for this build")
     if prof is not None and gym is None:
         if prof.get("traffic_bytes"):
             roofline["traffic"] = prof["traffic_bytes"]
@@ -377,7 +402,8 @@ def main() -> int:
                                       and not args.policy_mlp and not args.legacy_spring)
                   else f"env-steps/sec {args.env} " + ("legacy_spring " if args.legacy_spring else "")
                   + (f"global batch {total}" if strong else f"batch {args.batch}/GPU")
-                  + (f" with a {args.policy_mlp}-hidden MLP policy in the loop" if args.policy_mlp else ""),
+                  + (f" with a {args.policy_mlp}-hidden MLP policy in the loop" if args.policy_mlp else "")
+                  + (f" + obs mask ({args.obs_mask})" if mask is not None else ""),
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -390,24 +416,111 @@ def main() -> int:
                                "uniform(-1,1) actions (threefry)"
                                + (f", kinds {dict(kinds)} in one launch" if args.env == "mixed" else "")
                                + (", RCCL obs all-gather per step" if do_gather else "")
+                               + (f", obs mask '{args.obs_mask}' ({len(mask)} of {_OBS[args.env]} columns) "
+                                  "stored by the step kernel" if mask is not None else "")
                                + (f", MLP policy (D x {args.policy_mlp} x 8, tanh) per step in the same graph"
                                   if args.policy_mlp else ""),
                    "env": args.env, "global_batch": total, "batch_per_gpu": B,
                    "episode_length": args.episode_length, "qp_storage": args.qp_dtype, "parallelism": par,
                    "dynamics": "legacy_spring" if args.legacy_spring else "pbd",
+                   "obs_mask": args.obs_mask, "obs_mask_columns": 0 if mask is None else len(mask),
                    "path": "gym" if gym is not None else "brax",
                    "launch": "hipGraph replay of the K steps" if roll is not None else "eager per step"},
-        "gpu_event_ms_per_step": round(kern_ms_max + (float(elapsed[2]) if do_gather else 0.0), 4),
+        "gpu_event_ms_per_step": round(kern_ms_max, 4),
         "roofline": roofline, "cpu_baseline": cpu, "obs_finite": finite,
         # what ran: the process group's size and each rank's device (so a reader can tell N ranks
         # on N devices from N ranks sharing one)
         "world_size": world, "dist_backend": args.dist_backend if world > 1 else None,
         "rank_devices": ranks, "distinct_devices": len({r["device"] for r in ranks}),
+        "per_rank": per_rank_rows(table, ranks, do_gather),
+        "build": build,
     }
     if do_gather:
-        line["obs_allgather_ms"] = round(float(elapsed[2]), 4)
+        # device time of one step's all-gather (side stream, max over ranks) and how much of
+        # it ran under the next step's kernel (rank 0's events; the table has every rank's)
+        line["obs_allgather_ms"] = round(gather_max, 4)
         line["obs_allgather_bytes"] = total * obs_of().shape[-1] * 4
+        line["obs_allgather_overlap"] = overlap
+        line["obs_allgather_exposed_ms_per_step"] = round(max(0.0, ms_per_step - kern_ms_max), 4)
     print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def gather_rank_stats(vals, world: int, device) -> list:
+    """every rank's list of floats (all_gather over the process group), rank order"""
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    if world == 1:
+        return [t.tolist()]
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.tolist() for p in parts]
+
+
+def per_rank_rows(table, ranks, gather: bool) -> list:
+    """the rank-0 line's per-rank table: device, envs, wall and kernel time (and the gather's)"""
+    rows = []
+    for r, (v, d) in enumerate(zip(table, ranks)):
+        row = {"rank": r, "device": d.get("device"), "envs": int(v[5]), "kernel_ms": _r4(v[1]),
+               "eager_event_ms": _r4(v[3]), "wall_s": _r4(v[0])}
+        if gather:
+            row["obs_allgather_ms"] = _r4(v[2])
+            row["obs_allgather_overlap_frac"] = _r4(v[4])
+        rows.append(row)
+    return rows
+
+
+def _num(x) -> float:
+    return float("nan") if x is None else float(x)
+
+
+def _r4(x):
+    return None if x is None or x != x else round(float(x), 4)
+
+
+def gather_overlap(ev_a, ev_b, gather_ev) -> dict:
+    """How much of each step's all-gather (side stream, events gather_ev[k]) ran while step
+    k + 1's kernel did ([ev_a[k + 1], ev_b[k + 1]] on the compute stream): the events' times
+    relative to ev_a[0].  The last step's gather has no next step and is left out."""
+    ref = ev_a[0]
+    tot = ov = 0.0
+    for k in range(len(gather_ev) - 1):
+        g0, g1 = ref.elapsed_time(gather_ev[k][0]), ref.elapsed_time(gather_ev[k][1])
+        s0, s1 = ref.elapsed_time(ev_a[k + 1]), ref.elapsed_time(ev_b[k + 1])
+        tot += g1 - g0
+        ov += max(0.0, min(g1, s1) - max(g0, s0))
+    n = max(1, len(gather_ev) - 1)
+    return {"gathers": len(gather_ev) - 1, "mean_ms": round(tot / n, 4), "overlapped_ms": round(ov / n, 4),
+            "overlap_frac": round(ov / tot, 4) if tot > 0 else None,
+            "basis": "HIP events: side-stream all-gather of step k vs step k + 1's compute-stream span"}
+
+
+def dry_run(args, world: int, rank: int) -> int:
+    """--dry-run: the multi-rank plumbing of a real run (argument parser, process group, rank
+    table gather, shard sizes, the rank-0 line) with no device work -- what the CPU tests
+    run through launch_ranks."""
+    from po_brax_amd.sharding import Shard
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    strong = args.batch <= 0
+    total = args.global_batch if strong else args.batch * world
+    shard = Shard(total, world, rank)
+    me = {"rank": rank, "device": f"cpu:{rank}", "pid": os.getpid()}
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    table = gather_rank_stats([float("nan"), float("nan"), 0.0, float("nan"), float("nan"), float(shard.size)],
+                              world, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "env": args.env, "world_size": world, "global_batch": total,
+                          "scaling": "strong" if strong else "weak", "steps": args.steps, "warmup": args.warmup,
+                          "obs_mask": args.obs_mask, "gather_obs": args.gather_obs,
+                          "rank_devices": ranks, "per_rank": per_rank_rows(table, ranks, args.gather_obs)}))
+        sys.stdout.flush()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -418,39 +531,69 @@ def launch_ranks(n: int, argv=None, script: str = None) -> int:
     """Run this command as ``n`` ranks on this node (what torchrun would do): child processes
     with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, sharing this
     process's stdout (rank 0 prints the JSON line).  Returns non-zero if any rank fails; the
-    other ranks are then terminated (they would wait at a barrier)."""
+    other ranks are then terminated (they would wait at a barrier).  SIGTERM / Ctrl-C of this
+    process terminates every rank too (then killed after 30 s) and returns 143 / 130."""
+    import signal
     import socket
     import subprocess
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__),
-                                       *(sys.argv[1:] if argv is None else argv)], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
-                for q in live:
-                    q.terminate()
-                for q in live:
-                    try:
-                        q.wait(timeout=30)
-                    except subprocess.TimeoutExpired:
-                        q.kill()
-        if live:
-            time.sleep(0.2)
+
+    class _Term(Exception):
+        pass
+
+    def _on_term(signum, frame):
+        raise _Term()
+
+    try:
+        old = signal.signal(signal.SIGTERM, _on_term)
+    except ValueError:  # not the main thread: no handler (the caller owns signals)
+        old = None
+    procs, live, rc = [], [], 0
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__),
+                                           *(sys.argv[1:] if argv is None else argv)], env=env))
+            live.append(procs[-1])
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr)
+                    _stop(live)
+                    live = []
+                    break
+            if live:
+                time.sleep(0.2)
+    except (_Term, KeyboardInterrupt) as ex:
+        rc = 143 if isinstance(ex, _Term) else 130
+        print(f"bench.py: {'SIGTERM' if rc == 143 else 'interrupted'}; stopping {len(live)} rank(s)", file=sys.stderr)
+    finally:
+        _stop(live)
+        if old is not None:
+            signal.signal(signal.SIGTERM, old)
     return rc
+
+
+def _stop(procs) -> None:
+    """terminate, then kill after 30 s, the given child processes (exact PIDs we started)"""
+    import subprocess
+    for q in procs:
+        if q.poll() is None:
+            q.terminate()
+    for q in procs:
+        try:
+            q.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            q.kill()
+            q.wait()
 
 
 def rank_devices(dev, world: int) -> list:
@@ -481,21 +624,59 @@ def step_kernel(B: int) -> str:
     return "k_step_quad"
 
 
-def committed_profile(env: str, B: int, qp: str, legacy: bool = False):
-    """Counters per launch from the newest committed PMC profile of this exact config
-    (profiles/*_traffic.json, written by profiles/summarize.py); None if there is none."""
-    best, key = None, None
+def committed_profile(env: str, B: int, qp: str, legacy: bool = False, lib_sha256: str = None,
+                      obs_mask: str = "none"):
+    """(profile, stale): the counters per launch of the newest committed PMC profile of this
+    exact config (profiles/*_traffic.json, written by profiles/summarize.py) whose profiled
+    run loaded the same libpob.so (the bench line's build.lib_sha256), and the newest profile
+    of the config from any other build (None when there is a current one)."""
+    cur, stale = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
         try:
             t = json.load(open(p))
         except (OSError, ValueError):
             continue
         if t.get("env") == env and t.get("batch") == B and t.get("qp_storage", "f32") == qp and \
-                "k_step" in (t.get("kernel") or "") and bool(t.get("legacy_spring", False)) == bool(legacy):
+                "k_step" in (t.get("kernel") or "") and bool(t.get("legacy_spring", False)) == bool(legacy) and \
+                (t.get("obs_mask") or "none") == obs_mask:
             k = (t.get("generated", 0.0), p)  # newest by the summary's timestamp, then name
-            if key is None or k > key:
-                best, key = t, k
-    return best
+            same = lib_sha256 is not None and (t.get("build") or {}).get("lib_sha256") == lib_sha256
+            if same and (cur is None or k > cur[0]):
+                cur = (k, t)
+            elif not same and (stale is None or k > stale[0]):
+                stale = (k, t)
+    return (cur[1] if cur else None), (stale[1] if stale and not cur else None)
+
+
+def build_identity() -> dict:
+    """The loaded libpob.so (path, sha256) and the sha256 of the sources it is built from."""
+    import hashlib
+    from po_brax_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    src = hashlib.sha256()
+    csrc = os.path.join(ROOT, "po-brax_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)) if os.path.isdir(csrc) else []:
+        if fn.endswith((".hip", ".h", ".cpp")):
+            src.update(fn.encode())
+            with open(os.path.join(csrc, fn), "rb") as f:
+                src.update(f.read())
+    return {"lib": os.path.relpath(_lib.LIB_PATH, ROOT) if _lib.LIB_PATH.startswith(ROOT) else _lib.LIB_PATH,
+            "lib_sha256": h.hexdigest(), "csrc_sha256": src.hexdigest(), "abi": _lib.ABI_VERSION}
+
+
+def obs_mask_of(env: str, name: str):
+    """The --obs-mask column indices (None for 'none')."""
+    kw = OBS_MASKS[name]
+    if kw is None:
+        return None
+    from po_brax_amd import standard_observability_masks as M
+    if env == "ant":
+        parts = [M.POSITION["ant"]] + ([] if kw.get("velocity") is False else [M.VELOCITY["ant"]])
+        import numpy as np
+        return np.concatenate(parts)
+    return M.po_env_mask(env, **kw)
 
 
 def cpu_baseline(name: str, B: int, seconds: float, threads: int = 0, legacy: bool = False) -> dict:

@@ -31,6 +31,7 @@
  *                       RandomizedAutoResetWrapperCached.step wrappers.py:103
  *   pob_obs_gather      obs[:, idx] with the index sets of
  *                       po_brax/standard_observability_masks.py:5-67
+ *   pob_env_set_obs_mask  the same gather fused into pob_step (pob_state.obs_masked)
  *
  * Conventions: every pointer argument of a compute call is DEVICE memory owned by the
  * caller (the library allocates only its static tables at create time and never per
@@ -48,7 +49,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 6
+#define POB_ABI_VERSION 7
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -122,6 +123,11 @@ typedef struct pob_state {
    * double-buffering the any-done word (step k ORs into word k % 2, its masked reset reads
    * that word and clears the other) needs no fill kernel per step. */
   uint32_t *any_done_clear;
+  /* Optional (ABI v7): obs[:, idx] of the env's observation mask (pob_env_set_obs_mask), (B, K)
+   * float32, written by pob_step / pob_step_mixed from the same observation rows in the same
+   * launch (po_brax/standard_observability_masks.py:5-67 applied as obs[:, idx]).  The reset
+   * entry points do not write it (pob_obs_gather does). */
+  float *obs_masked;
 } pob_state;
 
 typedef struct pob_env pob_env;
@@ -138,6 +144,11 @@ void pob_env_destroy(pob_env *env);
 /* Free the device tables of every destroyed env now (ABI v6); returns how many buffers were
  * released.  Calls hipFree: never call it while a stream is being captured. */
 int pob_release_deferred(void);
+/* The env's observation mask (ABI v7): K column indices into its observation (0 <= idx < D,
+ * K <= 256, host memory); K = 0 clears it.  A step whose pob_state.obs_masked is set stores
+ * obs[:, idx] there.  Copies the env's device table (hipMemcpy): call it before stepping,
+ * never while a stream is being captured or a launch of this env is queued. */
+int pob_env_set_obs_mask(pob_env *env, const int32_t *idx, int K);
 int pob_env_dims(const pob_env *env, int *n_bodies, int *obs_dim, int *act_dim);
 /* host copy of default_angle() (8 floats, radians): System.default_angle [ext] */
 int pob_env_default_angle(const pob_env *env, float *out8);

@@ -60,7 +60,7 @@ struct pob_env {
 #define POB_STATE_FIELDS(X)                                                                    \
   X(pos) X(rot) X(vel) X(ang) X(obs) X(reward) X(done) X(steps) X(truncation) X(m0) X(m1) X(m2) \
   X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done) X(done_u8) X(trunc_i32) \
-  X(m0_i32) X(m1_i32) X(any_done_clear)
+  X(m0_i32) X(m1_i32) X(any_done_clear) X(obs_masked)
 
 struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
@@ -70,7 +70,15 @@ struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   uint8_t *done_u8;  // typed copies of step outputs (optional, pob.h)
   int32_t *trunc_i32, *m0_i32, *m1_i32;
   uint32_t *any_done_clear;  // pob_reset_where_done zeroes it (optional)
+  float *obs_masked;         // obs[:, mask] (optional, ABI v7)
 };
+// obs[:, mask] of a pass's staged observation rows (rows x D floats in LDS at stg), stored
+// next to the obs rows: each row's K columns by the wave's lanes (pob_env_set_obs_mask)
+POB_D void store_obs_masked(csys_t &S, float *dst, const float *stg, const int rows, const int D, const int lane) {
+  const int K = S.obs_mask_n;
+  for (int r = 0; r < rows; ++r)
+    for (int c = lane; c < K; c += 64) dst[(size_t)r * K + c] = stg[r * D + S.obs_mask[c]];
+}
 static StatePtrs to_ptrs(const pob_state &s) {
   StatePtrs p;
 #define POB_CP(f) p.f = s.f;
@@ -1064,6 +1072,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     } else {
       for (int i = lane; i < n; i += 64) dst[i] = stg[i];
     }
+    if (out.obs_masked)  // the observation mask's columns of the same rows (ABI v7)
+      store_obs_masked(S, out.obs_masked + (size_t)(b_first + p0) * S.obs_mask_n, stg, pn, D, lane);
     wave_lds_sync();
 #ifdef POB_EXP_TIMING_OBS
     if (p0 == 0) POB_TS(6);
@@ -1483,6 +1493,8 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     } else {
       for (int i = lane; i < n; i += 64) dst[i] = stg[i];
     }
+    if (out.obs_masked)  // the observation mask's columns of the same rows (ABI v7)
+      store_obs_masked(S, out.obs_masked + (size_t)(b_first + p0) * S.obs_mask_n, stg, pn, D, lane);
     wave_lds_sync();
   }
 
@@ -1794,6 +1806,8 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     } else {
       for (int i = lane; i < n; i += 64) dst[i] = stg[i];
     }
+    if (out.obs_masked)  // the observation mask's columns of the same rows (ABI v7)
+      store_obs_masked(S, out.obs_masked + (size_t)(b_first + p0) * S.obs_mask_n, stg, pn, D, lane);
     wave_lds_sync();
   }
 
@@ -2855,6 +2869,7 @@ static int check_step(const pob_env *e, int B, const pob_state *in, const float 
        !out->first_pos || !out->first_rot || !out->first_vel || !out->first_ang || !out->first_obs))
     return fail(POB_EINVAL, "AUTORESET needs first_qp/first_obs in both states");
   if ((flags & POB_F_EPISODE) && (!out->steps || !out->truncation)) return fail(POB_EINVAL, "EPISODE needs steps/truncation");
+  if (out->obs_masked && e->sys.obs_mask_n == 0) return fail(POB_EINVAL, "obs_masked given but the env has no observation mask");
   return POB_OK;
 }
 
@@ -2996,6 +3011,17 @@ int pob_random_actions(uint32_t *key_io, int total, int first, int B, int A, flo
   hipLaunchKernelGGL(k_actions, grid_for(B * A, 256), dim3(256), 0, st, key_io, total, first, B, A, act);
   hipLaunchKernelGGL(k_advance_key, dim3(1), dim3(1), 0, st, key_io);
   return hip_check(hipGetLastError(), "k_actions launch");
+}
+
+int pob_env_set_obs_mask(pob_env *e, const int32_t *idx, int K) {
+  if (!e) return fail(POB_EINVAL, "env is NULL");
+  if (K < 0 || K > POB_MAX_OBS_MASK) return fail(POB_EINVAL, "obs mask: K out of range");
+  if (K > 0 && !idx) return fail(POB_EINVAL, "obs mask: idx is NULL");
+  for (int i = 0; i < K; ++i)
+    if (idx[i] < 0 || idx[i] >= e->sys.D) return fail(POB_EINVAL, "obs mask: index out of range for the observation");
+  e->sys.obs_mask_n = K;
+  for (int i = 0; i < POB_MAX_OBS_MASK; ++i) e->sys.obs_mask[i] = (int16_t)(i < K ? idx[i] : 0);
+  return hip_check(hipMemcpy(e->d_sys, &e->sys, sizeof(pob_sys), hipMemcpyHostToDevice), "hipMemcpy(sys)");
 }
 
 int pob_obs_gather(const float *obs, int B, int D, const int32_t *idx, int K, float *out, void *stream) {

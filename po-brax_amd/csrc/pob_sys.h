@@ -34,6 +34,7 @@
 // per-role rows of the sixteen-lanes-per-env kernel (pob_hexa.h: HT_* offsets)
 #define POB_HEX_FLOATS 36
 
+#define POB_MAX_OBS_MASK 256  // >= the largest observation (AntGather: 211)
 struct pob_sys {
   int kind, N, D, n_obj;
   int substeps, n_walls, n_grid;
@@ -79,6 +80,10 @@ struct pob_sys {
   int torso_point;    // body 0's capsule end and ground end are the body origin (the Ant torso
                       // sphere): its contact points are x itself, no rotation needed
   const float *grid;  // GA object grid (n_grid, 3), device memory owned by the env
+  // observation mask (pob_env_set_obs_mask, ABI v7): the step kernels also store
+  // obs[:, obs_mask[0 .. obs_mask_n)] into pob_state.obs_masked
+  int obs_mask_n;
+  int16_t obs_mask[POB_MAX_OBS_MASK];
 };
 static_assert(offsetof(pob_sys, wall_row) == offsetof(pob_sys, leg) + sizeof(float) * 4 * POB_LEG_FLOATS,
               "the block table (leg rows, wall rows) is staged as one contiguous copy");

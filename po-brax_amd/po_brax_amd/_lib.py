@@ -22,7 +22,7 @@ RESET_GYM, RESET_OWN = 0, 1
 KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 QP_F32, QP_F16 = 0, 1
 MIX_MAX = 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class pob_params(C.Structure):
@@ -48,7 +48,7 @@ class pob_state(C.Structure):
     _fields_ = [(n, _VP) for n in (
         "pos", "rot", "vel", "ang", "obs", "reward", "done", "steps", "truncation",
         "m0", "m1", "m2", "rng", "first_pos", "first_rot", "first_vel", "first_ang",
-        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32", "any_done_clear")]
+        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32", "any_done_clear", "obs_masked")]
 
 
 # Every symbol include/pob.h declares (checked by tests/test_lib_symbols.py).
@@ -57,6 +57,7 @@ EXPORTS = (
     "pob_env_destroy", "pob_release_deferred", "pob_env_dims", "pob_env_default_angle", "pob_reset", "pob_step",
     "pob_step_mixed", "pob_reset_where_done", "pob_reset_where_done_shard", "pob_default_qp",
     "pob_random_split", "pob_random_split_batch", "pob_random_uniform", "pob_random_actions", "pob_obs_gather",
+    "pob_env_set_obs_mask",
 )
 
 
@@ -93,6 +94,7 @@ def _load():
     lib.pob_random_uniform.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _VP, _VP]
     lib.pob_random_actions.argtypes = [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP]
     lib.pob_obs_gather.argtypes = [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP, _VP]
+    lib.pob_env_set_obs_mask.argtypes = [_VP, C.POINTER(C.c_int32), C.c_int]
     if lib.pob_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH}: ABI version {lib.pob_abi_version()} != {ABI_VERSION}; rebuild it")
     for name in EXPORTS:

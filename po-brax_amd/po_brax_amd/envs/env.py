@@ -217,9 +217,13 @@ class PoBraxEnv(Env):
     info_rng = True              # info['rng'] is part of the State (False: stock brax ant)
     int_metrics: tuple = ()      # engine slots (m0, m1) whose public metric is int32 after step
 
-    def __init__(self, device=None, qp_dtype=torch.float32, **params):
+    def __init__(self, device=None, qp_dtype=torch.float32, obs_mask=None, **params):
         """``qp_dtype`` (engine extension): storage type of qp / first_qp, float32 (the
-        reference's) or float16 (binary16 storage, float32 arithmetic in the kernels)."""
+        reference's) or float16 (binary16 storage, float32 arithmetic in the kernels).
+        ``obs_mask`` (engine extension): column indices into this env's observation (e.g.
+        ``standard_observability_masks.po_env_mask(...)``); the step kernel then also stores
+        ``obs[:, obs_mask]`` as ``state.info['obs_masked']`` (B, K) in the same launch
+        (po_brax/standard_observability_masks.py:5-67 applied as obs[:, idx])."""
         self.device = torch.device(device if device is not None else "cuda")
         self._params = _lib.pob_params()
         check(lib.pob_default_params(C.byref(self._params)))
@@ -232,6 +236,14 @@ class PoBraxEnv(Env):
         self._set_params(params)
         self._action_repeat = 1
         self._owner = None
+        self._obs_mask = None
+        if obs_mask is not None:
+            import numpy as np
+            m = obs_mask.detach().cpu().numpy() if isinstance(obs_mask, torch.Tensor) else obs_mask
+            m = np.asarray(m).ravel()
+            if m.dtype.kind not in "iu":
+                raise TypeError("obs_mask must hold integer column indices")
+            self._obs_mask = np.ascontiguousarray(m.astype(np.int32))
         self._create()
         self.sys = System(self._owner, self._body_names())
 
@@ -246,6 +258,29 @@ class PoBraxEnv(Env):
         self._params.action_repeat = self._action_repeat
         self._owner = _Handle(_lib.KINDS[self.kind], self._params, self.device)
         self._N, self._D, self._A = self._owner.N, self._owner.D, self._owner.A
+        if self._obs_mask is not None:
+            m = self._obs_mask
+            if m.size and (m.min() < 0 or m.max() >= self._D):
+                raise ValueError(f"obs_mask index out of range for observation size {self._D}")
+            check(lib.pob_env_set_obs_mask(self._handle, m.ctypes.data_as(C.POINTER(C.c_int32)), int(m.size)))
+            self._obs_mask_dev = torch.from_numpy(m).to(self.device)
+
+    @property
+    def obs_mask(self):
+        """The observation mask's column indices (None without one)."""
+        return None if self._obs_mask is None else self._obs_mask.copy()
+
+    @property
+    def masked_observation_size(self) -> int:
+        return 0 if self._obs_mask is None else int(self._obs_mask.size)
+
+    def _gather_masked(self, b: dict) -> None:
+        """obs_masked from obs by the column gather kernel (the reset entry points do not fuse it)."""
+        B = b["obs"].shape[0]
+        K = int(self._obs_mask.size)
+        if B and K:
+            check(lib.pob_obs_gather(b["obs"].data_ptr(), B, self._D, self._obs_mask_dev.data_ptr(), K,
+                                     b["obs_masked"].data_ptr(), _lib.stream_handle(self.device)))
 
     @property
     def _handle(self) -> C.c_void_p:
@@ -277,6 +312,8 @@ class PoBraxEnv(Env):
             b.update(first_pos=torch.empty((B, N, 3), **q), first_rot=torch.empty((B, N, 4), **q),
                      first_vel=torch.empty((B, N, 3), **q), first_ang=torch.empty((B, N, 3), **q),
                      first_obs=torch.empty((B, D), **f))
+        if self._obs_mask is not None and self._obs_mask.size:
+            b["obs_masked"] = torch.empty((B, int(self._obs_mask.size)), **f)
         return b
 
     @staticmethod
@@ -322,6 +359,8 @@ class PoBraxEnv(Env):
         for k in ("any_done", "any_done_clear"):
             if k in a:
                 b[k] = a[k]
+        if "obs_masked" in state.info:
+            b["obs_masked"] = state.info["obs_masked"]
         for k in _TYPED:  # the typed step outputs of a previous in-place step (reused)
             if k in a:
                 b[k] = a[k]
@@ -374,6 +413,8 @@ class PoBraxEnv(Env):
         if "first_pos" in b:
             info["first_qp"] = QP(b["first_pos"], b["first_rot"], b["first_vel"], b["first_ang"])
             info["first_obs"] = b["first_obs"]
+        if "obs_masked" in b:
+            info["obs_masked"] = b["obs_masked"]
         # the public tensors handed out, so _bufs_of can tell them from caller replacements
         aux["pub"] = {"done": done, **{f"m{self.slot_names.index(n)}": t for n, t in metrics.items()
                                        if n in self.slot_names}}
@@ -407,6 +448,8 @@ class PoBraxEnv(Env):
         b = self._empty(B, episode, first)
         cs = self._cstate(b)
         pob.reset(self._handle.value, B, keys.data_ptr(), C.addressof(cs), _lib.stream_handle(self.device))
+        if "obs_masked" in b:
+            self._gather_masked(b)
         return self._state_of(b, False, squeeze)
 
     @staticmethod
@@ -505,6 +548,8 @@ class PoBraxEnv(Env):
         pob.reset_where_done_shard(self._handle.value, B, int(total) if total else B, int(first), mode,
                                    _lib.ptr(gym_in) or 0, _lib.ptr(gym_out) or 0, C.addressof(cs),
                                    _lib.stream_handle(self.device))
+        if "obs_masked" in b:  # the reset rows' masked columns (the step fuses them; this path does not)
+            self._gather_masked(b)
 
 
 # set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here

@@ -58,6 +58,10 @@ def main(src, dst_prefix):
                    "env": cfg.get("env"), "batch": cfg.get("batch_per_gpu", cfg.get("global_batch")),
                    "qp_storage": cfg.get("qp_storage"),
                    "legacy_spring": cfg.get("dynamics") == "legacy_spring",
+                   "obs_mask": cfg.get("obs_mask", "none"),
+                   # the profiled run's libpob.so: bench.committed_profile reports these
+                   # counters only for the same build
+                   "build": bench.get("build"),
                    "fetch_bytes_raw": f, "write_bytes": w, "traffic_bytes": 2 * f + w,
                    "valu_insts": mean("SQ_INSTS_VALU"), "grbm_gui_active": mean("GRBM_GUI_ACTIVE"),
                    "waves": mean("SQ_WAVES"),

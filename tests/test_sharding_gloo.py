@@ -255,3 +255,21 @@ def test_obs_gatherer_double_buffer_world2():
             p.join(timeout=120)
             assert p.exitcode == 0
         assert res == [True, True], total
+
+
+def test_obs_gatherer_ragged_world4():
+    """world 4 (gloo): ragged shards, including an empty one (total 3: 1 + 1 + 1 + 0), an
+    uneven split (50 = 13 + 13 + 12 + 12) and an even one (48), through the same slot
+    rotation: every step's gathered batch equals the global obs in env order."""
+    ctx = mp.get_context("spawn")
+    for total in (3, 50, 48):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_gather_rank, args=(r, 4, port, total, q)) for r in range(4)]
+        for p in procs:
+            p.start()
+        res = q.get(timeout=180)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        assert res == [True] * 4, total
