@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   const float *WT = otab + 8 * OT_FLOATS;
   constexpr int OMW = hex_max_walls(KIND);
   HWalls<OMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
-  hwalls_load(otab + OT_TAB_FLOATS, HW);
+  hwalls_load(otab + OT_TAB_FLOATS, HW, pob_face_table(S));
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
@@ -1648,7 +1648,7 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
   const float *WT = htab + 16 * HT_FLOATS;
   HWalls<HMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
-  hwalls_load(htab + HT_TAB_FLOATS, HW);
+  hwalls_load(htab + HT_TAB_FLOATS, HW, pob_face_table(S));
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)

@@ -21,6 +21,12 @@
 #include "pob_math.h"
 
 #define POB_MESH_MARGIN 1e-3f
+// the face constants table (pob_sys::face_c) is read through the constant address space
+#ifdef POB_MESH_HOST
+typedef const float *fcptr_t;
+#else
+typedef __attribute__((address_space(4))) const float *fcptr_t;
+#endif
 
 // one wall: centre x, y (z common), z-rotation cos / sin, half extents x, y (z common)
 struct MWall {
@@ -187,24 +193,25 @@ POB_D F3 btri_point(const BTri &T, const F3 pt) {
 }
 
 // A face (axis k, outward sign sg, plane w = w0, half extents ha, hb) with the capsule's
-// segment in face coordinates: its edges as segments (exact constants of ha, hb: every
-// derived quantity equals bseg_make's), its two triangles, and the segment-plane point.
-// Edges V0 V1 (a), V1 V2 (b), V0 V2 (diagonal), V2 V3 (a), V0 V3 (b); triangle t0 = (V0, V1,
-// V2), t1 = (V0, V2, V3) (oracle bface).
+// segment in face coordinates and the face's constants fc (pob_sys::face_c[wall][k],
+// pob_face_consts: its edges' segment terms and triangles' 1 / det -- exactly bseg_make's /
+// btri_make's values, formed once per env).  Edges V0 V1 (a), V1 V2 (b), V0 V2 (diagonal),
+// V2 V3 (a), V0 V3 (b); triangle t0 = (V0, V1, V2), t1 = (V0, V2, V3) (oracle bface).
 struct MFace {
   int k;
   float sg, ha, hb, w0, ha2, hb2;
-  BSeg A;                        // the capsule's segment
-  float ilA, hlA, iddA, ilB, hlB, iddB, ilD, hlD, iddD, e_d;  // a / b / diagonal edge terms
-  float tt;                      // the segment-plane point's parameter
+  BSeg A;          // the capsule's segment
+  fcptr_t fc;      // the face's constants (POB_FC_*)
 };
 // the capsule's segment in the wall frame (once per wall; oracle capsule_wall_mesh capw)
 template <class G>
 POB_D BSeg mcap_seg(G &g, const v3 La, const v3 Lb) {
   return bseg_make(g, f3(La.x, La.y, La.z), f3(Lb.x - La.x, Lb.y - La.y, Lb.z - La.z));
 }
+// fcw: the wall's three axes' constants (pob_sys::face_c[wall])
 template <class G>
-POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const float hy, const float hz) {
+POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const float hy, const float hz,
+                  fcptr_t fcw) {
   MFace F;
   const int k = f >> 1;
   F.k = k;
@@ -215,31 +222,30 @@ POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const flo
   F.A = bseg_perm(capw, k);
   F.ha2 = F.ha + F.ha;  // V1 - V0 = (ha - (-ha), ..): exact
   F.hb2 = F.hb + F.hb;
-  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2;
-  F.e_d = FMA(F.hb2, F.hb2, F.ha2 * F.ha2);
-  const float lA = g.sqrt(dA), lB = g.sqrt(dB), lD = g.sqrt(F.e_d);  // (half extents > 1e-8: pob_system.cpp)
-  F.ilA = g.rcp(lA + 1e-6f); F.hlA = lA * 0.5f; F.iddA = g.rcp(dA + 1e-6f);
-  F.ilB = g.rcp(lB + 1e-6f); F.hlB = lB * 0.5f; F.iddB = g.rcp(dB + 1e-6f);
-  F.ilD = g.rcp(lD + 1e-6f); F.hlD = lD * 0.5f; F.iddD = g.rcp(F.e_d + 1e-6f);
-  F.tt = bclamp01((F.sg * F.w0 - F.sg * F.A.p0.w) * g.rcp(F.sg * F.A.d.w + 1e-6f));
+  F.fc = fcw + POB_FACE_FLOATS * k;
+  (void)g;
   return F;
+}
+// the segment-plane point's parameter (oracle bface: both triangles, n = (0, 0, sg))
+template <class G>
+POB_D float mface_tt(G &g, const MFace &F) {
+  return bclamp01((F.sg * F.w0 - F.sg * F.A.p0.w) * g.rcp(F.sg * F.A.d.w + 1e-6f));
 }
 // edge e of the face as a segment: 0 V0 V1, 1 V1 V2, 2 V0 V2, 3 V2 V3, 4 V0 V3, 5 V2 V0, 6 V3 V0
 POB_D BSeg medge(const MFace &F, const int e) {
   const float ha = F.ha, hb = F.hb, w0 = F.w0;
   BSeg s;
   const bool ea = e == 0 || e == 3, eb = e == 1 || e == 4 || e == 6, ed = e == 2 || e == 5;
-  const bool neg = e >= 3;  // direction -a (3), -b (6), -diagonal (5); 4 is +b
   const float da = ea ? (e == 3 ? -F.ha2 : F.ha2) : (ed ? (e == 5 ? -F.ha2 : F.ha2) : 0.0f);
   const float db = eb ? (e == 6 ? -F.hb2 : F.hb2) : (ed ? (e == 5 ? -F.hb2 : F.hb2) : 0.0f);
-  (void)neg;
   const float pa = (e == 1) ? ha : ((e == 3 || e == 5) ? ha : -ha);
   const float pb = (e == 3 || e == 5 || e == 6) ? hb : -hb;
+  const int cls = ea ? 0 : (eb ? 1 : 2);
   s.p0 = f3(pa, pb, w0);
   s.d = f3(da, db, 0.0f);
-  s.il = ea ? F.ilA : (eb ? F.ilB : F.ilD);
-  s.hl = ea ? F.hlA : (eb ? F.hlB : F.hlD);
-  s.idd = ea ? F.iddA : (eb ? F.iddB : F.iddD);
+  s.il = F.fc[POB_FC_IL(cls)];
+  s.hl = F.fc[POB_FC_HL(cls)];
+  s.idd = F.fc[POB_FC_IDD(cls)];
   s.dir = f3(da * s.il, db * s.il, 0.0f);
   s.mid = f3(FMA(s.dir.a, s.hl, pa), FMA(s.dir.b, s.hl, pb), w0);
   return s;
@@ -250,12 +256,12 @@ POB_D BTri mtri(const MFace &F, const int t) {
   T.p0 = f3(-F.ha, -F.hb, F.w0);
   T.e0 = t == 0 ? f3(F.ha2, 0.0f, 0.0f) : f3(F.ha2, F.hb2, 0.0f);
   T.e1 = t == 0 ? f3(F.ha2, F.hb2, 0.0f) : f3(0.0f, F.hb2, 0.0f);
-  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2;
+  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = F.fc[POB_FC_ED];
   // a = e0.e0, b = e0.e1, c = e1.e1 with the zero products dropped (exact: +0 terms)
-  T.a = t == 0 ? dA : F.e_d;
+  T.a = t == 0 ? dA : e_d;
   T.b = t == 0 ? dA : dB;
-  T.c = t == 0 ? F.e_d : dB;
-  T.idet = 1.0f;  // set by the caller (one reciprocal per triangle, in the guard's policy)
+  T.c = t == 0 ? e_d : dB;
+  T.idet = F.fc[POB_FC_IDET(t)];
   T.s01 = medge(F, t == 0 ? 0 : 2);
   T.s12 = medge(F, t == 0 ? 1 : 3);
   T.s20 = medge(F, t == 0 ? 5 : 6);
@@ -275,10 +281,10 @@ POB_D MCand mface_cand(G &g, const MFace &F, const int t, const int kk) {
     bseg_seg(g, F.A, medge(F, e), S, P, u);
     c = bcand(S, P, u);
   } else if (kk == 3) {
-    BTri T = mtri(F, t);
-    T.idet = g.rcp(FMA(T.a, T.c, -(T.b * T.b)));
-    const F3 sp = f3fma(F.A.d, F.tt, F.A.p0);
-    c = bcand(sp, btri_point(T, sp), F.tt);
+    const BTri T = mtri(F, t);
+    const float tt = mface_tt(g, F);
+    const F3 sp = f3fma(F.A.d, tt, F.A.p0);
+    c = bcand(sp, btri_point(T, sp), tt);
   }
   return c;
 }
@@ -296,11 +302,11 @@ POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
     d2[kk] = f3d2(sp[kk], tp[kk]);
   }
   {
-    BTri T = mtri(F, t);
-    T.idet = g.rcp(FMA(T.a, T.c, -(T.b * T.b)));
-    sp[3] = f3fma(F.A.d, F.tt, F.A.p0);
+    const BTri T = mtri(F, t);
+    const float tt = mface_tt(g, F);
+    sp[3] = f3fma(F.A.d, tt, F.A.p0);
     tp[3] = btri_point(T, sp[3]);
-    u[3] = F.tt;
+    u[3] = tt;
     d2[3] = f3d2(sp[3], tp[3]);
   }
   const float mn = fminf(fminf(d2[0], d2[1]), fminf(d2[2], d2[3]));
@@ -337,15 +343,16 @@ POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
 // the guard policies give the same bits
 #ifdef POB_MESH_HOST
 POB_D MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
-                               const int t) {
+                               fcptr_t fcw, const int t) {
   HostGuard g;
-  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz), t);
+  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz, fcw), t);
 }
 #else
 __device__ __attribute__((noinline)) MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx,
-                                                           const float hy, const float hz, const int t) {
+                                                           const float hy, const float hz, fcptr_t fcw,
+                                                           const int t) {
   GuardBranch g;
-  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz), t);
+  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz, fcw), t);
 }
 #endif
 
@@ -395,8 +402,8 @@ struct MFaceOut {
 };
 template <class G>
 POB_D MFaceOut mesh_face_contacts(G &g, const int f, const v3 La, const v3 Lb, const float hx, const float hy,
-                                  const float hz, const float r, const float T) {
-  const MFace F = mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz);
+                                  const float hz, fcptr_t fcw, const float r, const float T) {
+  const MFace F = mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz, fcw);
   const float R = r + POB_MESH_MARGIN;
   const F3 A = F.A.p0;
   const float ha = F.ha, hb = F.hb, w0 = F.w0;
@@ -428,13 +435,12 @@ POB_D MFaceOut mesh_face_contacts(G &g, const int f, const v3 La, const v3 Lb, c
   MFENCE();
   if (left) { bseg_seg(g, F.A, medge(F, 4), S, P, u); mpick(c[1], tie[1], bcand(S, P, u)); }
   MFENCE();
-  const F3 sp = f3fma(F.A.d, F.tt, F.A.p0);
+  const float tt = mface_tt(g, F);
+  const F3 sp = f3fma(F.A.d, tt, F.A.p0);
   if (!(fabsf(sp.w - w0) >= R)) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      BTri Tr = mtri(F, t);
-      Tr.idet = g.rcp(FMA(Tr.a, Tr.c, -(Tr.b * Tr.b)));
-      mpick(c[t], tie[t], bcand(sp, btri_point(Tr, sp), F.tt));
+      mpick(c[t], tie[t], bcand(sp, btri_point(mtri(F, t), sp), tt));
       MFENCE();
     }
   }
@@ -444,7 +450,7 @@ POB_D MFaceOut mesh_face_contacts(G &g, const int f, const v3 La, const v3 Lb, c
     MCand ct = c[t];
     // (rare: two candidates at one distance; the face is formed again from the end points so
     // that its terms need not stay live through the candidates)
-    if (tie[t] && ct.d2 < T) ct = mtri_pick_ties_ool(f, La, Lb, hx, hy, hz, t);
+    if (tie[t] && ct.d2 < T) ct = mtri_pick_ties_ool(f, La, Lb, hx, hy, hz, fcw, t);
     o.tau[t] = 0.0f; o.dist[t] = 0.0f; o.nl[t] = V(0.0f, 0.0f, 0.0f);
     o.hit[t] = mface_contact(g, f >> 1, ct, r, T, o.tau[t], o.nl[t], o.dist[t]);
   }
@@ -455,9 +461,10 @@ POB_D MFaceOut mesh_face_contacts(G &g, const int f, const v3 La, const v3 Lb, c
 // register allocation -- the caller saves its live registers around the call, i.e. only when
 // a lane of the wave has a face item (POB_MESH_NOINLINE)
 __device__ __attribute__((noinline)) MFaceOut mesh_face_ool(const int f, const v3 La, const v3 Lb, const float hx,
-                                                         const float hy, const float hz, const float r, const float T) {
+                                                         const float hy, const float hz, fcptr_t fcw,
+                                                         const float r, const float T) {
   GuardBranch g;
-  return mesh_face_contacts(g, f, La, Lb, hx, hy, hz, r, T);
+  return mesh_face_contacts(g, f, La, Lb, hx, hy, hz, fcw, r, T);
 }
 #endif
 #ifndef POB_MESH_NOINLINE
@@ -466,16 +473,16 @@ __device__ __attribute__((noinline)) MFaceOut mesh_face_ool(const int f, const v
 // emit(tau, n_local, dist) for triangle 0 then 1 when it penetrates
 template <class G, class Fn>
 POB_D void mesh_face(G &g, const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
-                     const float r, const float T, Fn &&emit) {
+                     fcptr_t fcw, const float r, const float T, Fn &&emit) {
 #if POB_MESH_NOINLINE && !defined(POB_MESH_HOST)
   if constexpr (std::is_same<G, GuardBranch>::value) {
-    const MFaceOut o = mesh_face_ool(f, La, Lb, hx, hy, hz, r, T);
+    const MFaceOut o = mesh_face_ool(f, La, Lb, hx, hy, hz, fcw, r, T);
     if (o.hit[0]) emit(o.tau[0], o.nl[0], o.dist[0]);
     if (o.hit[1]) emit(o.tau[1], o.nl[1], o.dist[1]);
     return;
   }
 #endif
-  const MFaceOut o = mesh_face_contacts(g, f, La, Lb, hx, hy, hz, r, T);
+  const MFaceOut o = mesh_face_contacts(g, f, La, Lb, hx, hy, hz, fcw, r, T);
   if (o.hit[0]) emit(o.tau[0], o.nl[0], o.dist[0]);
   if (o.hit[1]) emit(o.tau[1], o.nl[1], o.dist[1]);
 }
@@ -524,8 +531,8 @@ POB_D int msum_dpp(const int v) { return v + __builtin_amdgcn_mov_dpp(v, CTRL, 0
 
 // each lane walks its own items, one face per iteration (mesh_face)
 template <int NB, class G, class SegOf, class Apply>
-POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
-                          Apply &&apply) {
+POB_D void mesh_lane_walk(G &g, const float *WT, fcptr_t FC, const float cz, const float hz, uint64_t (&M)[NB],
+                          SegOf &&seg_of, Apply &&apply) {
   while (true) {
     bool has = false;
     int s = 0;
@@ -550,7 +557,7 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
       const v3 La = mwall_local(W, cz, A);
       const v3 Lb = seg ? mwall_local(W, cz, B) : La;
       const float T = (r * r) * 1.00000095367431640625f;  // r^2 (1 + 2^-20)
-      mesh_face(g, bit & 7, La, Lb, W.hx, W.hy, hz, r, T,
+      mesh_face(g, bit & 7, La, Lb, W.hx, W.hy, hz, FC + 3 * POB_FACE_FLOATS * (bit >> 3), r, T,
                 [&](const float tau, const v3 nl, const float dist) {
         apply(s, bit, tau, mwall_world_n(W, nl), dist);
       });
@@ -561,15 +568,15 @@ POB_D void mesh_lane_walk(G &g, const float *WT, const float cz, const float hz,
 // (LANE_FALLBACK false: the caller guarantees all 64 lanes active and handles the per-lane
 // walk itself -- the four-lane kernel keeps it out of line)
 template <int NB, bool LANE_FALLBACK = true, class G, class SegOf, class Apply>
-POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz, uint64_t (&M)[NB], SegOf &&seg_of,
-                          Apply &&apply) {
+POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, const float hz, uint64_t (&M)[NB],
+                          SegOf &&seg_of, Apply &&apply) {
   if (LANE_FALLBACK) {
 #ifdef POB_MESH_LANE_WALK
     if (true) {  // A/B build switch: the per-lane walk everywhere
 #else
     if (__ballot(1) != ~0ull) {
 #endif
-      mesh_lane_walk<NB>(g, WT, cz, hz, M, seg_of, apply);
+      mesh_lane_walk<NB>(g, WT, FC, cz, hz, M, seg_of, apply);
       return;
     }
   }
@@ -631,9 +638,10 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     const int mo = second ? mb : ma;
     const bool sego = (mo & 64) != 0;
     const MWall W = mwall_row(WT + POB_WALL_FLOATS * ((mo >> 3) & 7));
+    fcptr_t fcw = FC + 3 * POB_FACE_FLOATS * ((mo >> 3) & 7);
     const v3 La = mwall_local(W, cz, Ao);
     const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
-    const MFace F = mface(g, mo & 7, mcap_seg(g, La, Lb), W.hx, W.hy, hz);
+    const MFace F = mface(g, mo & 7, mcap_seg(g, La, Lb), W.hx, W.hy, hz, fcw);
     MCand c = mface_cand(g, F, tri, gv ? kk : 7);
     c.d2 = mcand_key(c.d2);
     // each triangle's first strict minimum over its quad, and the number of candidates at it
@@ -648,7 +656,7 @@ POB_D void mesh_wave_walk(G &g, const float *WT, const float cz, const float hz,
     if (gv && kk == kmin) {
       const float T = (ro * ro) * 1.00000095367431640625f;
       MCand ct = c;
-      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties_ool(mo & 7, La, Lb, W.hx, W.hy, hz, tri);  // (rare: brax's tie average)
+      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties_ool(mo & 7, La, Lb, W.hx, W.hy, hz, fcw, tri);  // (rare: brax's tie average)
       v3 nl;
       hit = mface_contact(g, F.k, ct, ro, T, tau, nl, dst);
       if (hit) nw = mwall_world_n(W, nl);

@@ -276,7 +276,7 @@ POB_D void qwalls_walk(csys_t &S, const float *LT, const float *WT, const QBody 
   GuardBranch g;
 #if POB_QUAD_WAVE_WALK
   if (!LANE) {
-    mesh_wave_walk<QNB, false>(g, WT, S.wall_cz, S.wall_hz, M,
+    mesh_wave_walk<QNB, false>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
                [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
                [&](const int l, const int, const float tau, const v3 n, const float dist) {
       if (ws.nct < QK) {
@@ -288,7 +288,7 @@ POB_D void qwalls_walk(csys_t &S, const float *LT, const float *WT, const QBody 
     return;
   }
 #endif
-  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  mesh_lane_walk<QNB>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
              [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
              [&](const int l, const int, const float tau, const v3 n, const float dist) {
     if (ws.nct < QK) {
@@ -429,7 +429,7 @@ __device__ __attribute__((noinline)) void qwalls_rewalk(csys_t *Sp, const float 
   const uint32_t wa = st->on ? (1u << S.n_walls) - 1u : 0u;
   uint64_t M[QNB];
   qmesh_items(S, LT, WT, wa | (wa << 8) | (wa << 16), ms, M);
-  QWALK<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  QWALK<QNB>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
              [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
              [&](const int l, const int, const float tau, const v3 n, const float dist) {
     if (VEL) qwall_vel_one(g, S, SC, LT, x, q, v, w, l, tau, n, dist, d0, d1);
@@ -578,7 +578,7 @@ POB_D void qcontacts_static(csys_t *Sp, const float *LT, const float *WT, const 
     const uint32_t lw = qwall_mask(S, b);
     qmesh_items(S, LT, WT, lw | (lw << 8) | (lw << 16), ms, M);
   }
-  mesh_lane_walk<QNB>(g, WT, S.wall_cz, S.wall_hz, M,
+  mesh_lane_walk<QNB>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
                       [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
                       [&](const int l, const int, const float tau, const v3 n, const float dist) {
     const v3 x = qpick3(l, b.x);

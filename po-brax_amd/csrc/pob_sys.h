@@ -35,6 +35,38 @@
 #define POB_HEX_FLOATS 36
 
 #define POB_MAX_OBS_MASK 256  // >= the largest observation (AntGather: 211)
+
+// Per (wall, face axis k) constants of the capsule x TriangulatedBox forms (pob_mesh.h): a
+// face of axis k has half extents (ha, hb) = (hy, hz) / (hx, hz) / (hx, hy) and edges of
+// three classes -- along a (length 2 ha), along b (2 hb), the diagonal -- each with brax's
+// segment terms il = 1 / (len + 1e-6), hl = len / 2, idd = 1 / (d.d + 1e-6) (oracle bseg_make
+// of the edge: d.d is exactly the one nonzero square, or the FMA of the two for the diagonal),
+// then e_d = d.d of the diagonal and the two triangles' 1 / det (oracle btri_make).  The
+// same IEEE operations as the oracle's per-face evaluation (sqrt, division and fma are
+// correctly rounded here and there), formed once per env instead of per face evaluation.
+#define POB_FACE_FLOATS 12
+#define POB_FC_IL(c) (3 * (c))
+#define POB_FC_HL(c) (3 * (c) + 1)
+#define POB_FC_IDD(c) (3 * (c) + 2)
+#define POB_FC_ED 9
+#define POB_FC_IDET(t) (10 + (t))
+static inline void pob_face_consts(const float ha, const float hb, float *o) {
+  const float ha2 = ha + ha, hb2 = hb + hb;
+  const float dA = ha2 * ha2, dB = hb2 * hb2;
+  const float e_d = __builtin_fmaf(hb2, hb2, ha2 * ha2);
+  const float dd[3] = {dA, dB, e_d};
+  for (int c = 0; c < 3; ++c) {
+    const float len = __builtin_sqrtf(dd[c]);
+    o[POB_FC_IL(c)] = 1.0f / (len + 1e-6f);
+    o[POB_FC_HL(c)] = len * 0.5f;
+    o[POB_FC_IDD(c)] = 1.0f / (dd[c] + 1e-6f);
+  }
+  o[POB_FC_ED] = e_d;
+  // t0 = (V0, V1, V2): a = dA, b = dA, c = e_d; t1 = (V0, V2, V3): a = e_d, b = dB, c = dB
+  o[POB_FC_IDET(0)] = 1.0f / __builtin_fmaf(dA, e_d, -(dA * dA));
+  o[POB_FC_IDET(1)] = 1.0f / __builtin_fmaf(e_d, dB, -(dB * dB));
+}
+
 struct pob_sys {
   int kind, N, D, n_obj;
   int substeps, n_walls, n_grid;
@@ -58,6 +90,7 @@ struct pob_sys {
   // a culled wall is farther than r from the capsule, no contact)
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
   float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
+  float face_c[POB_MAXW][3][POB_FACE_FLOATS];  // pob_face_consts of every wall's three axes
   float friction, s_pos, half_s_ang;
   // legacy spring dynamics (pob_params.legacy_spring; brax <= 0.0.12): joint stiffness, spring
   // damping, limit strength, Baumgarte rate (baumgarte_erp * substeps / dt)

@@ -254,6 +254,8 @@ const char *build_system(int kind, const pob_params &p, pob_sys &s) {
     if (s.wall_c[w][2] != s.wall_cz || s.wall_h[w][2] != s.wall_hz) return "walls: centre z / half height differ";
     // pob_mesh.h mface forms the face edges' lengths without brax's safe_norm zero test
     if (!(s.wall_h[w][0] > 1e-6f && s.wall_h[w][1] > 1e-6f && s.wall_h[w][2] > 1e-6f)) return "walls: degenerate box";
+    for (int k = 0; k < 3; ++k)  // face axis k: (ha, hb) = (hy, hz) / (hx, hz) / (hx, hy)
+      pob_face_consts(s.wall_h[w][k == 0 ? 1 : 0], s.wall_h[w][k == 2 ? 1 : 2], s.face_c[w][k]);
     float *R = s.wall_row[w];
     R[0] = s.wall_c[w][0]; R[1] = s.wall_c[w][1]; R[2] = s.wall_cos[w];
     R[3] = s.wall_sin[w]; R[4] = s.wall_h[w][0]; R[5] = s.wall_h[w][1];

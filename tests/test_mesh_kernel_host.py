@@ -19,6 +19,7 @@ ROOT = os.path.dirname(HERE)
 MESH_H = os.path.join(ROOT, "po-brax_amd", "csrc", "pob_mesh.h")
 
 SHIM = r"""
+#include "pob_sys.h"
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -38,6 +39,10 @@ struct HostGuard {
 
 DRIVER = r"""
 static int g_ties = 0;
+// the wall's face constants (pob_sys::face_c[w], as pob_system.cpp builds them)
+static void face_table(float hx, float hy, float hz, float *fcw) {
+  for (int k = 0; k < 3; ++k) pob_face_consts(k == 0 ? hy : hx, k == 2 ? hy : hz, fcw + POB_FACE_FLOATS * k);
+}
 extern "C" int host_tie_count(void) { const int n = g_ties; g_ties = 0; return n; }
 // the oracle's row: (tau, n, pen = r - dist, cd = 1e-6 + dist), as the kernels' callers form them
 static void put(float *out, int n, float tau, v3 nw, float r, float dist) {
@@ -52,11 +57,13 @@ extern "C" int host_mesh_contacts(const float *w, const float *a, const float *b
   const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
   const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
   const float T = (r * r) * 1.00000095367431640625f;
+  float fcw[3 * POB_FACE_FLOATS];
+  face_table(W.hx, W.hy, hz, fcw);
   HostGuard g;
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    mesh_face(g, f, La, Lb, W.hx, W.hy, hz, r, T, [&](float tau, v3 nl, float dist) {
+    mesh_face(g, f, La, Lb, W.hx, W.hy, hz, fcw, r, T, [&](float tau, v3 nl, float dist) {
       put(out, n, tau, mwall_world_n(W, nl), r, dist);
       ++n;
     });
@@ -72,11 +79,13 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
   const v3 Lb = seg ? mwall_local(W, cz, V(b[0], b[1], b[2])) : La;
   const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, hz, r + POB_MESH_MARGIN);
   const float T = (r * r) * 1.00000095367431640625f;
+  float fcw[3 * POB_FACE_FLOATS];
+  face_table(W.hx, W.hy, hz, fcw);
   HostGuard g;
   int n = 0;
   for (int f = 0; f < 6; ++f) {
     if (!((fm >> f) & 1u)) continue;
-    const MFace F = mface(g, f, mcap_seg(g, La, Lb), W.hx, W.hy, hz);
+    const MFace F = mface(g, f, mcap_seg(g, La, Lb), W.hx, W.hy, hz, fcw);
     for (int t = 0; t < 2; ++t) {
       // (the wave walk's reduction: NaN distances enter as +inf, lexicographic (d2, kk) minimum)
       MCand c[4]; MCand best; int kb = 0;
@@ -87,7 +96,7 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
       }
       int neq = 0;
       for (int kk = 0; kk < 4; ++kk) neq += c[kk].d2 == best.d2;
-      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties_ool(f, La, Lb, W.hx, W.hy, hz, t); ++g_ties; }
+      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties_ool(f, La, Lb, W.hx, W.hy, hz, fcw, t); ++g_ties; }
       float tau, dist; v3 nl;
       if (mface_contact(g, F.k, best, r, T, tau, nl, dist)) { put(out, n, tau, mwall_world_n(W, nl), r, dist); ++n; }
     }
@@ -105,7 +114,7 @@ def host_mesh(tmp_path_factory):
     src.write_text(SHIM + body + DRIVER)
     so = d / "mesh_host.so"
     subprocess.check_call(["g++", "-O2", "-mfma", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
-                           "-shared", "-o", str(so), str(src)])
+                           "-I", os.path.dirname(MESH_H), "-shared", "-o", str(so), str(src)])
     lib = C.CDLL(str(so))
     FP = C.POINTER(C.c_float)
     lib.host_mesh_contacts.argtypes = [FP, FP, FP, C.c_int, C.c_float, FP]
