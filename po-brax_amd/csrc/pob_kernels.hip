@@ -762,9 +762,13 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   const bool act_lane = b < B;
   // the wave's 16 envs are consecutive rows of every state array
   const int b_first = (gt - lane) >> 2;
-  const int nenv = B - b_first < 16 ? (B - b_first > 0 ? B - b_first : 0) : 16;
+  if (b_first >= B) return;  // (wave-uniform: a block's waves past the batch; no barrier follows)
+  const int nenv = B - b_first < 16 ? B - b_first : 16;
   const int le = b - b_first;
-  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  // The physics runs on all 64 lanes (the wave walk's DPP / bpermute rounds need every lane):
+  // the lanes past the batch in its last wave replay env B - 1 and store nothing.
+  const int bl = act_lane ? b : B - 1, lel = bl - b_first;
+  const size_t r3 = (size_t)bl * N * 3, r4 = (size_t)bl * N * 4;
 
   // ---- state load: coalesced vector loads into the wave's region, then every lane
   // picks its bodies (the host sets POB_F_STAGED when the qp pointers are 16-B aligned
@@ -787,11 +791,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       if (pr == 0) A1.template put<NMAX * 4, POB_NDYN * 4>(stg + n0, n1, lane);
       else A1.template put<NMAX * 3, POB_NDYN * 3>(stg + n0, n1, lane);
       wave_lds_sync();
-      if (act_lane) {
+      {
 #pragma unroll
         for (int l = 0; l < QNB; ++l) {
           const int g = qbody_global(l, k);
-          const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
+          const float *s0 = stg + (lel * N + g) * c0, *s1 = stg + n0 + (lel * N + g) * c1;
           if (pr == 0) {
             bd.x[l] = V(s0[0], s0[1], s0[2]);
             bd.q[l].w = s1[0]; bd.q[l].x = s1[1]; bd.q[l].y = s1[2]; bd.q[l].z = s1[3];
@@ -810,10 +814,10 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       const float *X = arr == 0 ? in.pos : (arr == 1 ? in.rot : (arr == 2 ? in.vel : in.ang));
       stage_load<QT>(X, (size_t)b_first * N * c, nenv * N * c, stg, lane);
       wave_lds_sync();
-      if (act_lane) {
+      {
 #pragma unroll
         for (int l = 0; l < QNB; ++l) {
-          const int o = (le * N + qbody_global(l, k)) * c;
+          const int o = (lel * N + qbody_global(l, k)) * c;
           if (arr == 0) bd.x[l] = V(stg[o], stg[o + 1], stg[o + 2]);
           else if (arr == 1) { bd.q[l].w = stg[o]; bd.q[l].x = stg[o + 1]; bd.q[l].y = stg[o + 2]; bd.q[l].z = stg[o + 3]; }
           else if (arr == 2) bd.v[l] = V(stg[o], stg[o + 1], stg[o + 2]);
@@ -822,7 +826,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       }
       wave_lds_sync();
     }
-  } else if (act_lane) {
+  } else {
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       const int g = qbody_global(l, k);
@@ -845,11 +849,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   v3 cvl[QNB], cal[QNB];
   TaskOut t;
   t.tp_ok = false;
-  if (act_lane) {
+  {
     const float xb = bd.x[0].x;
     float a[QNJ];
 #pragma unroll
-    for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)b * POB_NJ + 2 * k + jl];
+    for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)bl * POB_NJ + 2 * k + jl];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
@@ -876,7 +880,24 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     // pass -- 0.272 -> 0.122 ms at B = 65 536; the HH / TAG waves nearly always hold an ant near
     // a wall, and the second copy of the substep loop costs them 5-10 %, profiles/r5m)
     constexpr bool TWO = KIND == POB_GATHER && POB_QUAD_TWO_PASS;
+    constexpr bool WALLS = KIND != POB_ANT;
+    // Wall passes: the fast one keeps at most QK wall contacts per lane and collide substep in
+    // its store; a wave one of whose lanes had more (rare) runs the step again from its state in
+    // the slow pass, which re-walks the overflowing lanes' faces (qwalls_rewalk_inl).  The
+    // overflow handling then costs the fast pass nothing: its code and registers are elsewhere.
     int pass = TWO ? (__any(qwall_mask_margin(S, bd, POB_QUAD_NEAR_MARGIN) != 0u) ? 1 : 0) : 1;
+    auto reload = [&]() {
+#pragma unroll
+      for (int l = 0; l < QNB; ++l) {
+        const int g = qbody_global(l, k);
+        bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
+        bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
+        bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
+        bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
+        Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f));
+        Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f));
+      }
+    };
     for (;;) {
     if (pass == 0) {
       bool near = false;
@@ -894,45 +915,44 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       if (!__any(near)) break;
       // a lane met a wall's broadphase: the step again, from its state, with the walls
       pass = 1;
-#pragma unroll
-      for (int l = 0; l < QNB; ++l) {
-        const int g = qbody_global(l, k);
-        bd.x[l] = ld3<QT>(in.pos, r3 + 3 * g);
-        bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
-        bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
-        bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
-        Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f));
-        Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f));
-      }
+      reload();
       continue;
     }
+    if (pass == 1 && WALLS) {
+      bool ovf = false;
+#pragma nounroll
+      for (int it = 0; it < 2 * iters; ++it) {
+        // Issue priority falls with progress, so a SIMD's four waves (one per block) advance
+        // together: with the default oldest-first arbitration the first wave finishes early
+        // and the last one runs its final substeps alone, at one-wave latency (measured per
+        // wave with POB_EXP_TIMING: p0..max of the physics phase 94 K..211 K ticks before,
+        // 133 K..182 K with this; kernel 0.120 -> 0.112 ms at B = 65 536).
+#if POB_QUAD_PRIO == 1
+        const int lvl = (it * 4) / (2 * iters);
+        if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
+        qpbd_substep<WALLS, false, false>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric, nullptr, &ovf);
+        if (__any(ovf)) break;
+      }
+      if (!__any(ovf)) break;
+      pass = 2;
+      reload();
+      continue;
+    }
+    // the slow wall pass (after an overflow) / the stock ant (no walls)
 #pragma nounroll
     for (int it = 0; it < 2 * iters; ++it) {
-      // Issue priority falls with progress, so a SIMD's four waves (one per block) advance
-      // together: with the default oldest-first arbitration the first wave finishes early
-      // and the last one runs its final substeps alone, at one-wave latency (measured per
-      // wave with POB_EXP_TIMING: p0..max of the physics phase 94 K..211 K ticks before,
-      // 133 K..182 K with this; kernel 0.120 -> 0.112 ms at B = 65 536).
 #if POB_QUAD_PRIO == 1
       const int lvl = (it * 4) / (2 * iters);
       if (lvl == 0) __builtin_amdgcn_s_setprio(3);
       else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
       else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
-#elif POB_QUAD_PRIO == 2  // experiment: the levels spent on the last three substeps
-      const int left = 2 * iters - it;
-      if (left > 3) __builtin_amdgcn_s_setprio(3);
-      else if (left == 3) __builtin_amdgcn_s_setprio(2);
-      else if (left == 2) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-#elif POB_QUAD_PRIO == 3  // experiment: the levels spent on the last six substeps, two each
-      const int left = 2 * iters - it;
-      if (left > 6) __builtin_amdgcn_s_setprio(3);
-      else if (left > 4) __builtin_amdgcn_s_setprio(2);
-      else if (left > 2) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
 #endif
-      qpbd_substep<KIND != POB_ANT>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);
+      qpbd_substep<WALLS>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);
     }
     break;
     }
@@ -950,7 +970,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     }
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { cvl[l] = Ls.get3(QL_CV(l)); cal[l] = Ls.get3(QL_CA(l)); }
-    if (k == 0) {
+    if (act_lane && k == 0) {
       float steps = in.steps ? in.steps[b] : 0.0f;
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
       t.steps = steps;

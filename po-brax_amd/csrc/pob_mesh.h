@@ -269,24 +269,32 @@ POB_D BTri mtri(const MFace &F, const int t) {
 }
 // candidate kk of triangle t (oracle bface order): 0..2 the triangle's edges (t0: V0 V1, V1 V2,
 // V0 V2; t1: V0 V2, V2 V3, V0 V3) against the segment, 3 the segment-plane point and its
-// closest triangle point; any other kk: none (d2 = +inf)
+// closest triangle point; any other kk: none (d2 = +inf).  S, P: the candidate's points (the
+// cooperative walk's tie average needs them; zero for none)
 template <class G>
-POB_D MCand mface_cand(G &g, const MFace &F, const int t, const int kk) {
+POB_D MCand mface_cand(G &g, const MFace &F, const int t, const int kk, F3 &S, F3 &P) {
   MCand c;
   c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
+  S = f3(0.0f, 0.0f, 0.0f);
+  P = S;
   if (kk < 3) {
     const int e = t == 0 ? kk : (kk == 0 ? 2 : kk + 2);
-    F3 S, P;
     float u;
     bseg_seg(g, F.A, medge(F, e), S, P, u);
     c = bcand(S, P, u);
   } else if (kk == 3) {
     const BTri T = mtri(F, t);
     const float tt = mface_tt(g, F);
-    const F3 sp = f3fma(F.A.d, tt, F.A.p0);
-    c = bcand(sp, btri_point(T, sp), tt);
+    S = f3fma(F.A.d, tt, F.A.p0);
+    P = btri_point(T, S);
+    c = bcand(S, P, tt);
   }
   return c;
+}
+template <class G>
+POB_D MCand mface_cand(G &g, const MFace &F, const int t, const int kk) {
+  F3 S, P;
+  return mface_cand(g, F, t, kk, S, P);
 }
 // the triangle's pick with brax's tie rule (oracle bpick): all four candidates, the minimum,
 // ties averaged in candidate order (the slow path of a tie: the fast forms take the first
@@ -345,6 +353,12 @@ POB_D MCand mtri_pick_ties(G &g, const MFace &F, const int t) {
 POB_D MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
                                fcptr_t fcw, const int t) {
   HostGuard g;
+  return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz, fcw), t);
+}
+#elif defined(POB_MESH_TIES_INLINE)  // A/B build switch: the tie path inline
+POB_D MCand mtri_pick_ties_ool(const int f, const v3 La, const v3 Lb, const float hx, const float hy, const float hz,
+                               fcptr_t fcw, const int t) {
+  GuardBranch g;
   return mtri_pick_ties(g, mface(g, f, mcap_seg(g, La, Lb), hx, hy, hz, fcw), t);
 }
 #else
@@ -528,6 +542,28 @@ POB_D void mlexmin_dpp(float &d, int &kk) {
 }
 template <int CTRL>
 POB_D int msum_dpp(const int v) { return v + __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true); }
+// lane j's value within the quad (quad_perm [j, j, j, j])
+template <int J>
+POB_D float mquad_read(const float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), J * 0x55, 0xf, 0xf, true));
+}
+// brax's tie rule over the quad's four candidates (oracle bpick with cnt > 1): the points,
+// parameters of the candidates at the minimum key summed in candidate order from zero, then
+// divided by their count -- every lane of the quad active (DPP reads)
+template <int J>
+POB_D void mtie_add(const float key, const float dmin, const F3 S, const F3 P, const float u, F3 &Ss, F3 &Ps,
+                    float &us, float &cnt) {
+  const float kj = mquad_read<J>(key);
+  const F3 Sj = f3(mquad_read<J>(S.a), mquad_read<J>(S.b), mquad_read<J>(S.w));
+  const F3 Pj = f3(mquad_read<J>(P.a), mquad_read<J>(P.b), mquad_read<J>(P.w));
+  const float uj = mquad_read<J>(u);
+  if (kj == dmin) {
+    Ss = f3(Ss.a + Sj.a, Ss.b + Sj.b, Ss.w + Sj.w);
+    Ps = f3(Ps.a + Pj.a, Ps.b + Pj.b, Ps.w + Pj.w);
+    us += uj;
+    cnt += 1.0f;
+  }
+}
 
 // each lane walks its own items, one face per iteration (mesh_face)
 template <int NB, class G, class SegOf, class Apply>
@@ -642,7 +678,8 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
     const v3 La = mwall_local(W, cz, Ao);
     const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
     const MFace F = mface(g, mo & 7, mcap_seg(g, La, Lb), W.hx, W.hy, hz, fcw);
-    MCand c = mface_cand(g, F, tri, gv ? kk : 7);
+    F3 Sc, Pc;
+    MCand c = mface_cand(g, F, tri, gv ? kk : 7, Sc, Pc);
     c.d2 = mcand_key(c.d2);
     // each triangle's first strict minimum over its quad, and the number of candidates at it
     float dmin = c.d2;
@@ -650,15 +687,25 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
     mlexmin_dpp<0xB1>(dmin, kmin);  // quad_perm [1, 0, 3, 2]
     mlexmin_dpp<0x4E>(dmin, kmin);  // quad_perm [2, 3, 0, 1]
     const int neq = msum_dpp<0x4E>(msum_dpp<0xB1>(c.d2 == dmin ? 1 : 0));
+    const float T = (ro * ro) * 1.00000095367431640625f;
+    // (rare) two or more candidates at a minimum below the radius: brax's average of them,
+    // gathered over the quad (the same sums as the oracle's bpick, in candidate order)
+    const bool tie = gv && neq > 1 && dmin < T;
+    if (__any(tie)) {
+      F3 Ss = f3(0.0f, 0.0f, 0.0f), Ps = Ss;
+      float us = 0.0f, cnt = 0.0f;
+      mtie_add<0>(c.d2, dmin, Sc, Pc, c.u, Ss, Ps, us, cnt);
+      mtie_add<1>(c.d2, dmin, Sc, Pc, c.u, Ss, Ps, us, cnt);
+      mtie_add<2>(c.d2, dmin, Sc, Pc, c.u, Ss, Ps, us, cnt);
+      mtie_add<3>(c.d2, dmin, Sc, Pc, c.u, Ss, Ps, us, cnt);
+      if (tie && kk == kmin) c = bcand(f3(Ss.a / cnt, Ss.b / cnt, Ss.w / cnt), f3(Ps.a / cnt, Ps.b / cnt, Ps.w / cnt), us / cnt);
+    }
     float tau = 0.0f, dst = 0.0f;
     v3 nw = V(0.0f, 0.0f, 0.0f);
     bool hit = false;
     if (gv && kk == kmin) {
-      const float T = (ro * ro) * 1.00000095367431640625f;
-      MCand ct = c;
-      if (neq > 1 && c.d2 < T) ct = mtri_pick_ties_ool(mo & 7, La, Lb, W.hx, W.hy, hz, fcw, tri);  // (rare: brax's tie average)
       v3 nl;
-      hit = mface_contact(g, F.k, ct, ro, T, tau, nl, dst);
+      hit = mface_contact(g, F.k, c, ro, T, tau, nl, dst);
       if (hit) nw = mwall_world_n(W, nl);
     }
     // the owners take their items' triangles in order: the winners' lanes first (all four

@@ -322,8 +322,11 @@ __device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float
 // the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
 // order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
 // its segments for the out-of-line re-walks (qwalls_rewalk).
-template <bool WALLS>
-POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws) {
+// OVF false (the fast wall pass): a lane with more contacts than the store holds only reports
+// it in *ovf (the wave then runs the step again in the slow pass, OVF true: the detection-time
+// segments kept for the re-walks)
+template <bool WALLS, bool OVF = true>
+POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws, bool *ovf = nullptr) {
   ws.nct = 0;
   if (!WALLS) return;
   csys_t &S = *launder(Sp);
@@ -353,10 +356,11 @@ POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBo
 #endif
   if (!__any((M[0] | M[1] | M[2]) != 0ull)) return;
 #if POB_QUAD_WAVE_WALK
-  if (!POB_QUAD_DETECT_OOL && __ballot(1) == ~0ull) qwalls_walk<false>(S, LT, WT, b, M, ws);
-  else
-#endif
+  // (the step kernel runs its substeps on all 64 lanes of every wave: step_quad_body)
+  qwalls_walk<false>(S, LT, WT, b, M, ws);
+#else
   ws.nct = qwalls_walk_ool(Sp, LT, WT, b.x[0], b.x[1], b.x[2], b.q[0], b.q[1], b.q[2], M[0], M[1], M[2], &ws);
+#endif
 #ifdef POB_EXP_NO_APPLY
   {  // timing experiment only: the walk runs, its contacts are not applied
     int z = ws.nct & 0;
@@ -364,6 +368,10 @@ POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBo
     ws.nct = z;
   }
 #endif
+  if (!OVF) {
+    *ovf = *ovf | (ws.nct > QK);
+    return;
+  }
   if (ws.nct > QK) {  // (rare) the detection-time segments for the re-walks
     QMesh ms;
     qmesh_segments(S, LT, b, rv_leg, ms);
@@ -439,10 +447,47 @@ __device__ __attribute__((noinline)) void qwalls_rewalk(csys_t *Sp, const float 
   for (int l = 0; l < QNB; ++l) { st->d0[l] = d0[l]; st->d1[l] = d1[l]; }
 }
 
+// The same re-walk inline (POB_QUAD_REWALK_INLINE, the default): the wave-cooperative walk
+// with no lane fallback (the step kernel's substeps run on all 64 lanes) and no call -- a call
+// site in the pass, however rarely taken, confines every value live across it to the
+// callee-saved registers, which spilled the substep's state at every collide substep.  The
+// segments come from the store, the substep-start pose (position pass) from LDS.
+#ifndef POB_QUAD_REWALK_INLINE
+#define POB_QUAD_REWALK_INLINE 1
+#endif
+template <bool VEL>
+POB_D void qwalls_rewalk_inl(csys_t &S, const float *LT, const float *WT, const QBody &b, const Lds &L,
+                             const QWalls &ws, const bool ovf, const float fric, v3 (&d0)[QNB], v3 (&d1)[QNB]) {
+  GuardBranch g;
+  const HCon SC{fric, S.inv_h};
+  QMesh ms;
+#pragma unroll
+  for (int l = 0; l < QNB; ++l) {
+    ms.a[l] = V(ws.seg[6 * l], ws.seg[6 * l + 1], ws.seg[6 * l + 2]);
+    ms.b[l] = V(ws.seg[6 * l + 3], ws.seg[6 * l + 4], ws.seg[6 * l + 5]);
+  }
+  const uint32_t wa = ovf ? (1u << S.n_walls) - 1u : 0u;
+  uint64_t M[QNB];
+  qmesh_items(S, LT, WT, wa | (wa << 8) | (wa << 16), ms, M);
+  mesh_wave_walk<QNB, false>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qmesh_seg(S, LT, ms, l, A, B, r, seg); },
+             [&](const int l, const int, const float tau, const v3 n, const float dist) {
+    if constexpr (VEL) {
+      qwall_vel_one(g, S, SC, LT, b.x, b.q, b.v, b.w, l, tau, n, dist, d0, d1);
+    } else {
+      v3 px[QNB];
+      q4 pq[QNB];
+#pragma unroll
+      for (int k = 0; k < QNB; ++k) { px[k] = L.get3(QL_PX(k)); pq[k] = L.get4(QL_PQ(k)); }
+      qwall_pos_one(g, S, SC, LT, b.x, b.q, px, pq, l, tau, n, dist, d0, d1);
+    }
+  });
+}
+
 // Position pass of a collide substep: ground contacts (ground first per body, oracle order),
 // then the wall contacts from the store in detection order
-template <bool WALLS>
-POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const Lds &L, QGround &gc,
+template <bool WALLS, bool OVF = true>
+POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBody &b, const Lds &L, QGround &gc,
                               const QWalls &ws, v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
@@ -476,7 +521,13 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
       qwall_pos_one(g, S, SC, LT, b.x, b.q, px, pq, (int)c[0], c[1], V(c[2], c[3], c[4]), c[5], DX, DA);
     }
   }
+  if (!OVF) return;  // (the fast pass: a wave with an overflow runs the step again)
+#if POB_QUAD_REWALK_INLINE
+  if (__any(ovf)) qwalls_rewalk_inl<false>(S, LT, WT, b, L, ws, ovf, fric, DX, DA);
+  if (false) {
+#else
   if (__any(ovf)) {
+#endif
     QOvf st;
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
@@ -487,15 +538,18 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, cons
     st.fric = fric;
     st.on = ovf ? 1 : 0;
     qwalls_rewalk<false>(Sp, LT, WT, &st);
+    // everything live after the call comes back from the block (the callee leaves the pose as
+    // it is), so nothing of the pass is live across the call: the call's clobbers then cost no
+    // spills of the substep's state (they would fall in every substep, not only on overflow)
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) { DX[l] = st.d0[l]; DA[l] = st.d1[l]; }
+    for (int l = 0; l < QNB; ++l) { DX[l] = st.d0[l]; DA[l] = st.d1[l]; b.x[l] = st.x[l]; b.q[l] = st.q[l]; }
   }
 }
 
 // Velocity pass: ground contacts, then the wall contacts from the store (contact points
 // x + tau rotate(e0, q) at the post-projection pose)
-template <bool WALLS>
-POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, const QBody &b, const QGround &gc,
+template <bool WALLS, bool OVF = true>
+POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, QBody &b, const QGround &gc,
                               const QWalls &ws, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
@@ -526,7 +580,13 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
       qwall_vel_one(g, S, SC, LT, b.x, b.q, b.v, b.w, (int)c[0], c[1], V(c[2], c[3], c[4]), c[5], dV, dW);
     }
   }
+  if (!OVF) return;  // (the fast pass: a wave with an overflow runs the step again)
+#if POB_QUAD_REWALK_INLINE
+  if (__any(ovf)) qwalls_rewalk_inl<true>(S, LT, WT, b, Lds{nullptr, 0, 0}, ws, ovf, fric, dV, dW);
+  if (false) {
+#else
   if (__any(ovf)) {
+#endif
     QOvf st;
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
@@ -538,7 +598,10 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, cons
     st.on = ovf ? 1 : 0;
     qwalls_rewalk<true>(Sp, LT, WT, &st);
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) { dV[l] = st.d0[l]; dW[l] = st.d1[l]; }
+    for (int l = 0; l < QNB; ++l) {
+      dV[l] = st.d0[l]; dW[l] = st.d1[l];
+      b.x[l] = st.x[l]; b.q[l] = st.q[l]; b.v[l] = st.v[l]; b.w[l] = st.w[l];
+    }
   }
 }
 
@@ -689,9 +752,9 @@ POB_D float quad_friction(const csys_t &S) {
 // collide substep at the point the wall pass would (qwalls_detect) and reports a lane whose
 // mask is not empty in *near -- with every mask empty the wall pass finds no face item, so
 // the two passes compute the same bits.
-template <bool WALLS, bool CHECK = false>
+template <bool WALLS, bool CHECK = false, bool OVF = true>
 POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const Lds &L,
-                        const bool COLLIDE, const float fric, bool *near = nullptr) {
+                        const bool COLLIDE, const float fric, bool *near = nullptr, bool *ovf = nullptr) {
 #pragma unroll
   for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
   // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
@@ -737,7 +800,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   // 2b. wall contact detection (collide substeps), at the pose the projection starts from
   QWalls ws;
   ws.nct = 0;
-  if (COLLIDE) qwalls_detect<WALLS>(Sp, LT, WT, b, ws);
+  if (COLLIDE) qwalls_detect<WALLS, OVF>(Sp, LT, WT, b, ws, ovf);
   if (CHECK && COLLIDE) *near = *near | (qwall_mask(*launder(Sp), b) != 0u);
   // 3. position projection
   QGround gc;
@@ -767,7 +830,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
       qtorso_add<2>(DX[0], DA[0], tq, imp0);
       qtorso_add<3>(DX[0], DA[0], tq, imp0);
     }
-    if (COLLIDE) qcontacts_position<WALLS>(Sp, LT, WT, b, L, gc, ws, DX, DA, fric);
+    if (COLLIDE) qcontacts_position<WALLS, OVF>(Sp, LT, WT, b, L, gc, ws, DX, DA, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.x[l] = vadd(b.x[l], DX[l]);
@@ -791,7 +854,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontacts_velocity<WALLS>(Sp, LT, WT, b, gc, ws, dV, dW, fric);
+    qcontacts_velocity<WALLS, OVF>(Sp, LT, WT, b, gc, ws, dV, dW, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);

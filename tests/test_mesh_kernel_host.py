@@ -89,14 +89,27 @@ extern "C" int host_mesh_contacts_split(const float *w, const float *a, const fl
     for (int t = 0; t < 2; ++t) {
       // (the wave walk's reduction: NaN distances enter as +inf, lexicographic (d2, kk) minimum)
       MCand c[4]; MCand best; int kb = 0;
+      F3 S[4], P[4];
       for (int kk = 0; kk < 4; ++kk) {
-        c[kk] = mface_cand(g, F, t, kk);
+        c[kk] = mface_cand(g, F, t, kk, S[kk], P[kk]);
         c[kk].d2 = mcand_key(c[kk].d2);
         if (kk == 0 || c[kk].d2 < best.d2 || (c[kk].d2 == best.d2 && kk < kb)) { best = c[kk]; kb = kk; }
       }
       int neq = 0;
       for (int kk = 0; kk < 4; ++kk) neq += c[kk].d2 == best.d2;
-      if (neq > 1 && best.d2 < T) { best = mtri_pick_ties_ool(f, La, Lb, W.hx, W.hy, hz, fcw, t); ++g_ties; }
+      if (neq > 1 && best.d2 < T) {  // (the walk's quad gather: mtie_add over kk = 0..3)
+        F3 Ss = f3(0.0f, 0.0f, 0.0f), Ps = Ss;
+        float us = 0.0f, cnt = 0.0f;
+        const float dmin = best.d2;
+        for (int kk = 0; kk < 4; ++kk)
+          if (c[kk].d2 == dmin) {
+            Ss = f3(Ss.a + S[kk].a, Ss.b + S[kk].b, Ss.w + S[kk].w);
+            Ps = f3(Ps.a + P[kk].a, Ps.b + P[kk].b, Ps.w + P[kk].w);
+            us += c[kk].u; cnt += 1.0f;
+          }
+        best = bcand(f3(Ss.a / cnt, Ss.b / cnt, Ss.w / cnt), f3(Ps.a / cnt, Ps.b / cnt, Ps.w / cnt), us / cnt);
+        ++g_ties;
+      }
       float tau, dist; v3 nl;
       if (mface_contact(g, F.k, best, r, T, tau, nl, dist)) { put(out, n, tau, mwall_world_n(W, nl), r, dist); ++n; }
     }
