@@ -138,7 +138,7 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
   uint64_t Ms[1] = {M};
-  mesh_wave_walk<1>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
+  mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     [&](const int, const int bit, const float tau, const v3 n, const float dist) {
     // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
@@ -174,7 +174,7 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
   }
   if (!__any(ovf)) return;
   uint64_t Ms[1] = {ovf ? ms.mc : 0ull};
-  mesh_wave_walk<1>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
+  mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     [&](const int, const int, const float tau, const v3 n, const float dist) {
     ocontact_vel_pe(g, SC, false, HT[HT_R] - dist, vfma(rv, tau, b.x), n, 1e-6f + dist, im, b.x, b.v, b.w, dV, dW);

@@ -1268,7 +1268,10 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   const bool act_lane = b < B;
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   constexpr int sh = obs_shift(KIND);
-  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  // the physics runs on all 64 lanes (the wave walk's DPP / bpermute rounds need every lane):
+  // the lanes past the batch in its last wave replay env B - 1 and store nothing
+  const int bl = act_lane ? b : B - 1, lel = bl - b_first;
+  const size_t r3 = (size_t)bl * N * 3, r4 = (size_t)bl * N * 4;
   const bool lane0 = m == 0;  // A_0: the env's POMDP tail
 
   // ---- state load: coalesced loads of the 8 envs' rows into LDS (pairs of arrays), then
@@ -1288,11 +1291,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       wave_lds_sync();
       if (KIND == POB_GATHER && pr == 0 && act_lane && isA && S.n_obj <= POB_GA_QUAD_MAX)
         ga_quad_prefetch<QT>(S, in, r3, stg + le * N * 3, k, gop);
-      if (act_lane) {
+      {
 #pragma unroll
         for (int sl = 0; sl < ONB; ++sl) {
           const int g = sl == 0 ? g0 : g1;
-          const float *s0 = stg + (le * N + g) * c0, *s1 = stg + n0 + (le * N + g) * c1;
+          const float *s0 = stg + (lel * N + g) * c0, *s1 = stg + n0 + (lel * N + g) * c1;
           if (pr == 0) {
             bd.x[sl] = V(s0[0], s0[1], s0[2]);
             bd.q[sl].w = s1[0]; bd.q[sl].x = s1[1]; bd.q[sl].y = s1[2]; bd.q[sl].z = s1[3];
@@ -1304,7 +1307,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       }
       wave_lds_sync();
     }
-  } else if (act_lane) {
+  } else {
 #pragma unroll
     for (int sl = 0; sl < ONB; ++sl) {
       const int g = sl == 0 ? g0 : g1;
@@ -1315,14 +1318,14 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     }
     // AntGather: the A lanes' object positions ride along with the state loads (one round
     // trip; the registers are free at the octet kernel's occupancy)
-    if (KIND == POB_GATHER && isA && S.n_obj <= POB_GA_QUAD_MAX) {
+    if (KIND == POB_GATHER && act_lane && isA && S.n_obj <= POB_GA_QUAD_MAX) {
       ga_quad_prefetch<QT>(S, in, r3, nullptr, k, gop);
       gop_ok = true;
     }
   }
   (void)NMAX;
   // the action, loaded with the state (its round trip overlaps the table loads)
-  const float a_in = act_lane ? act[(size_t)b * POB_NJ + jown] : 0.0f;
+  const float a_in = act[(size_t)bl * POB_NJ + jown];
   // the role table, staged after the state loads are issued (both in flight together; the
   // block is one wave, so an LDS wait orders the table writes before its reads)
   {
@@ -1356,7 +1359,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
     task_prefetch<KIND, QT>(in, r3, t);
   }
-  if (act_lane) {
+  {
     const float xb = bd.x[0].x;
     const float a = a_in;
 #pragma unroll
@@ -1420,7 +1423,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 #pragma unroll
     for (int sl = 0; sl < ONB; ++sl) Ls.set3(3 * sl, cvl[sl]);
     wave_lds_sync();
-    if (lane0) {
+    if (act_lane && lane0) {
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && t.pdone != 0.0f) t.steps = 0.0f;
       t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
       if (KIND == POB_ANT) {
@@ -1612,7 +1615,10 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   const bool act_lane = b < B;
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   constexpr int sh = obs_shift(KIND);
-  const size_t r3 = (size_t)b * N * 3, r4 = (size_t)b * N * 4;
+  // the physics runs on all 64 lanes (as in the eight-lane kernel): the lanes past the batch
+  // in its last wave replay env B - 1 and store nothing
+  const int bl = act_lane ? b : B - 1, lel = bl - b_first;
+  const size_t r3 = (size_t)bl * N * 3, r4 = (size_t)bl * N * 4;
   const bool lane0 = r == 0;  // P_hip_0: the env's POMDP tail
 
   // ---- state load: coalesced loads of the 4 envs' rows into LDS (pairs of arrays), then
@@ -1631,28 +1637,28 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     wave_lds_sync();
     if (KIND == POB_GATHER && act_lane && r < 4 && S.n_obj <= POB_GA_QUAD_MAX)
       ga_quad_prefetch<QT>(S, in, r3, stg + le * N * 3, r, gop);
-    if (act_lane) {
-      const float *sx = stg + (le * N + g) * 3, *sq = stg + n3 + (le * N + g) * 4;
-      const float *sv = stg + n3 + n4 + (le * N + g) * 3, *sw = stg + 2 * n3 + n4 + (le * N + g) * 3;
+    {
+      const float *sx = stg + (lel * N + g) * 3, *sq = stg + n3 + (lel * N + g) * 4;
+      const float *sv = stg + n3 + n4 + (lel * N + g) * 3, *sw = stg + 2 * n3 + n4 + (lel * N + g) * 3;
       bd.x = V(sx[0], sx[1], sx[2]);
       bd.q.w = sq[0]; bd.q.x = sq[1]; bd.q.y = sq[2]; bd.q.z = sq[3];
       bd.v = V(sv[0], sv[1], sv[2]);
       bd.w = V(sw[0], sw[1], sw[2]);
     }
     wave_lds_sync();
-  } else if (act_lane) {
+  } else {
     bd.x = ld3<QT>(in.pos, r3 + 3 * g);
     bd.q = ld4<QT>(in.rot, r4 + 4 * g);
     bd.v = ld3<QT>(in.vel, r3 + 3 * g);
     bd.w = ld3<QT>(in.ang, r3 + 3 * g);
     // AntGather: lanes 0..3's object positions ride along with the state loads
-    if (KIND == POB_GATHER && r < 4 && S.n_obj <= POB_GA_QUAD_MAX) {
+    if (KIND == POB_GATHER && act_lane && r < 4 && S.n_obj <= POB_GA_QUAD_MAX) {
       ga_quad_prefetch<QT>(S, in, r3, nullptr, r, gop);
       gop_ok = true;
     }
   }
   // the action, loaded with the state (its round trip overlaps the table loads)
-  const float a_in = act_lane ? act[(size_t)b * POB_NJ + jown] : 0.0f;
+  const float a_in = act[(size_t)bl * POB_NJ + jown];
   constexpr int HMW = hex_max_walls(KIND);
   // the role table, staged after the state loads are issued (as in the eight-lane kernel)
   {
@@ -1685,7 +1691,7 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     t.rng0 = in.rng[2 * b]; t.rng1 = in.rng[2 * b + 1];
     task_prefetch<KIND, QT>(in, r3, t);
   }
-  if (act_lane) {
+  {
     const float xb = bd.x.x;
     const float a = a_in;
     const int iters = Sp->substeps / 2;
@@ -1743,7 +1749,7 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     // the bodies' contact velocity sums for the stock ant's contact cost
     Ls.set3(0, cvl);
     wave_lds_sync();
-    if (lane0) {
+    if (act_lane && lane0) {
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && t.pdone != 0.0f) t.steps = 0.0f;
       t.xb = xb; t.ctrl = 0.0f; t.contact = 0.0f;
       if (KIND == POB_ANT) {

@@ -216,7 +216,7 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
-  mesh_wave_walk<ONB>(g, WT, HW.fc, HW.cz, HW.hz, M,
+  mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
                       [&](const int s, const int bit, const float tau, const v3 n, const float dist) {
     const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
@@ -280,7 +280,7 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
   }
   if (!__any(ovf)) return;
   uint64_t M[ONB] = {ovf ? ms.mc[0] : 0ull, ovf ? ms.mc[1] : 0ull};
-  mesh_wave_walk<ONB>(g, WT, HW.fc, HW.cz, HW.hz, M,
+  mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) {
                         const float *c = CS + 64 * (OCS_SEG + 6 * s);
                         A = V(c[0], c[64], c[128]);
