@@ -881,10 +881,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     // a wall, and the second copy of the substep loop costs them 5-10 %, profiles/r5m)
     constexpr bool TWO = KIND == POB_GATHER && POB_QUAD_TWO_PASS;
     constexpr bool WALLS = KIND != POB_ANT;
-    // Wall passes: the fast one keeps at most QK wall contacts per lane and collide substep in
-    // its store; a wave one of whose lanes had more (rare) runs the step again from its state in
-    // the slow pass, which re-walks the overflowing lanes' faces (qwalls_rewalk_inl).  The
-    // overflow handling then costs the fast pass nothing: its code and registers are elsewhere.
+    // Wall passes (POB_QUAD_FAST_PASS, off): a fast pass keeping at most QK wall contacts per
+    // lane and collide substep, a wave with more (rare) running the step again in the slow pass
+    // with the re-walks.  Measured slower than the one wall pass with the inline re-walk (HH
+    // B = 65 536 0.2163 vs 0.1877 ms, TAG 0.1330 vs 0.1221; profiles/r5s_ab.txt): the two loops'
+    // live ranges spilled the step's values around them.
     int pass = TWO ? (__any(qwall_mask_margin(S, bd, POB_QUAD_NEAR_MARGIN) != 0u) ? 1 : 0) : 1;
     auto reload = [&]() {
 #pragma unroll
@@ -918,7 +919,10 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       reload();
       continue;
     }
-    if (pass == 1 && WALLS) {
+#ifndef POB_QUAD_FAST_PASS
+#define POB_QUAD_FAST_PASS 0
+#endif
+    if (pass == 1 && WALLS && POB_QUAD_FAST_PASS) {
       bool ovf = false;
 #pragma nounroll
       for (int it = 0; it < 2 * iters; ++it) {

@@ -202,7 +202,36 @@ struct MFace {
   float sg, ha, hb, w0, ha2, hb2;
   BSeg A;          // the capsule's segment
   fcptr_t fc;      // the face's constants (POB_FC_*)
+#ifdef POB_MESH_FC_INLINE  // A/B build switch: the constants formed per face evaluation
+  float cv[POB_FACE_FLOATS];
+#endif
 };
+// the face's constants: edge class c's (il, hl, idd), the diagonal's d.d, triangle t's 1 / det
+POB_D void mfc_edge(const MFace &F, const int c, float &il, float &hl, float &idd) {
+#ifdef POB_MESH_FC_INLINE
+  il = c == 0 ? F.cv[POB_FC_IL(0)] : (c == 1 ? F.cv[POB_FC_IL(1)] : F.cv[POB_FC_IL(2)]);
+  hl = c == 0 ? F.cv[POB_FC_HL(0)] : (c == 1 ? F.cv[POB_FC_HL(1)] : F.cv[POB_FC_HL(2)]);
+  idd = c == 0 ? F.cv[POB_FC_IDD(0)] : (c == 1 ? F.cv[POB_FC_IDD(1)] : F.cv[POB_FC_IDD(2)]);
+#else
+  il = F.fc[POB_FC_IL(c)];
+  hl = F.fc[POB_FC_HL(c)];
+  idd = F.fc[POB_FC_IDD(c)];
+#endif
+}
+POB_D float mfc_ed(const MFace &F) {
+#ifdef POB_MESH_FC_INLINE
+  return F.cv[POB_FC_ED];
+#else
+  return F.fc[POB_FC_ED];
+#endif
+}
+POB_D float mfc_idet(const MFace &F, const int t) {
+#ifdef POB_MESH_FC_INLINE
+  return t == 0 ? F.cv[POB_FC_IDET(0)] : F.cv[POB_FC_IDET(1)];
+#else
+  return F.fc[POB_FC_IDET(t)];
+#endif
+}
 // the capsule's segment in the wall frame (once per wall; oracle capsule_wall_mesh capw)
 template <class G>
 POB_D BSeg mcap_seg(G &g, const v3 La, const v3 Lb) {
@@ -223,6 +252,22 @@ POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const flo
   F.ha2 = F.ha + F.ha;  // V1 - V0 = (ha - (-ha), ..): exact
   F.hb2 = F.hb + F.hb;
   F.fc = fcw + POB_FACE_FLOATS * k;
+#ifdef POB_MESH_FC_INLINE  // (pob_face_consts' operations in the guard's policy)
+  {
+    const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = FMA(F.hb2, F.hb2, F.ha2 * F.ha2);
+    const float dd[3] = {dA, dB, e_d};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float len = g.sqrt(dd[c]);
+      F.cv[POB_FC_IL(c)] = g.rcp(len + 1e-6f);
+      F.cv[POB_FC_HL(c)] = len * 0.5f;
+      F.cv[POB_FC_IDD(c)] = g.rcp(dd[c] + 1e-6f);
+    }
+    F.cv[POB_FC_ED] = e_d;
+    F.cv[POB_FC_IDET(0)] = g.rcp(FMA(dA, e_d, -(dA * dA)));
+    F.cv[POB_FC_IDET(1)] = g.rcp(FMA(e_d, dB, -(dB * dB)));
+  }
+#endif
   (void)g;
   return F;
 }
@@ -243,9 +288,7 @@ POB_D BSeg medge(const MFace &F, const int e) {
   const int cls = ea ? 0 : (eb ? 1 : 2);
   s.p0 = f3(pa, pb, w0);
   s.d = f3(da, db, 0.0f);
-  s.il = F.fc[POB_FC_IL(cls)];
-  s.hl = F.fc[POB_FC_HL(cls)];
-  s.idd = F.fc[POB_FC_IDD(cls)];
+  mfc_edge(F, cls, s.il, s.hl, s.idd);
   s.dir = f3(da * s.il, db * s.il, 0.0f);
   s.mid = f3(FMA(s.dir.a, s.hl, pa), FMA(s.dir.b, s.hl, pb), w0);
   return s;
@@ -256,12 +299,12 @@ POB_D BTri mtri(const MFace &F, const int t) {
   T.p0 = f3(-F.ha, -F.hb, F.w0);
   T.e0 = t == 0 ? f3(F.ha2, 0.0f, 0.0f) : f3(F.ha2, F.hb2, 0.0f);
   T.e1 = t == 0 ? f3(F.ha2, F.hb2, 0.0f) : f3(0.0f, F.hb2, 0.0f);
-  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = F.fc[POB_FC_ED];
+  const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = mfc_ed(F);
   // a = e0.e0, b = e0.e1, c = e1.e1 with the zero products dropped (exact: +0 terms)
   T.a = t == 0 ? dA : e_d;
   T.b = t == 0 ? dA : dB;
   T.c = t == 0 ? e_d : dB;
-  T.idet = F.fc[POB_FC_IDET(t)];
+  T.idet = mfc_idet(F, t);
   T.s01 = medge(F, t == 0 ? 0 : 2);
   T.s12 = medge(F, t == 0 ? 1 : 3);
   T.s20 = medge(F, t == 0 ? 5 : 6);
