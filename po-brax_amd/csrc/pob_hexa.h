@@ -96,7 +96,12 @@ struct HMesh {
 template <int MW, class G>
 POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float *WT, const HWalls<MW> &HW,
                               const bool torso, const HBody &b, const v3 px, const q4 pq, HGround &gc, HMesh &ms,
-                              v3 &DX, v3 &DA, float *CS) {
+                              v3 &DX, v3 &DA, float *CS, unsigned long long *tacc = nullptr) {
+#ifdef POB_EXP_TIMING_SUB
+  const unsigned long long _tc0 = __builtin_amdgcn_s_memtime();  // (slot 5: the broadphase + face cull)
+#else
+  (void)tacc;
+#endif
   gc.pe = vadd(b.x, qrot_xy(HTV(HT, HT_GE), b.q));
   gc.pen = HT[HT_HASG] != 0.0f ? HT[HT_GR] - gc.pe.z : -1.0f;
   const float im = HT[HT_IM];
@@ -134,21 +139,46 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
     const uint32_t fm = mesh_face_mask(La, Lb, W.hx, W.hy, HW.hz, R);
     M |= on ? (uint64_t)fm << (8 * w) : 0ull;
   }
+#ifdef POB_EXP_TIMING_SUB
+  if (tacc) tacc[5] += __builtin_amdgcn_s_memtime() - _tc0;
+#endif
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
+  // the walk only collects the contacts (its rounds hand each one to its owner lane: a store of
+  // five floats); the position responses follow from the store in walk order, one loop over
+  // the lanes' contacts instead of the response code in every round's hand-over
   uint64_t Ms[1] = {M};
   mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     [&](const int, const int bit, const float tau, const v3 n, const float dist) {
-    // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
-    owall_position(g, SC, HT[HT_R] - dist, vfma(rv, tau, b.x), n, 1e-6f + dist, im, b.x, b.q, pq, px, DX, DA);
     ms.mc |= 1ull << bit;
     if (ms.nct < HMAXC) {
       float *c = CS + 64 * 5 * ms.nct;
       c[0] = tau; c[64] = n.x; c[128] = n.y; c[192] = n.z; c[256] = dist;
     }
     ++ms.nct;
+  });
+  const bool ovf = ms.nct > HMAXC;
+  const int nc = ovf ? 0 : ms.nct;
+#pragma unroll 1
+  for (int i = 0; i < HMAXC; ++i) {
+    if (!__any(i < nc)) break;
+    if (i < nc) {
+      // penetration r - dist; the contact at the triangle point pe - (1e-6 + dist) n
+      const float *c = CS + 64 * 5 * i;
+      owall_position(g, SC, HT[HT_R] - c[256], vfma(rv, c[0], b.x), V(c[64], c[128], c[192]), 1e-6f + c[256], im, b.x,
+                     b.q, pq, px, DX, DA);
+    }
+  }
+  if (!__any(ovf)) return;
+  // (rare) more contacts than the store holds: the contact faces walked again, each contact
+  // applied as it comes (the same contacts in the same order)
+  uint64_t Mo[1] = {ovf ? ms.mc : 0ull};
+  mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Mo,
+                    [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
+                    [&](const int, const int, const float tau, const v3 n, const float dist) {
+    owall_position(g, SC, HT[HT_R] - dist, vfma(rv, tau, b.x), n, 1e-6f + dist, im, b.x, b.q, pq, px, DX, DA);
   });
 }
 
@@ -286,7 +316,11 @@ POB_D void hpbd_substep(G &g, csys_t &S, const float *HT, const float *WT, const
     }
     HSUB_T(1)
     if (COLLIDE) {
-      hcontacts_position<MW>(g, SC, HT, WT, HW, torso, b, px, pq, gc, ms, DX, DA, CS);
+      hcontacts_position<MW>(g, SC, HT, WT, HW, torso, b, px, pq, gc, ms, DX, DA, CS
+#ifdef POB_EXP_TIMING_SUB
+                             , tacc
+#endif
+      );
       HSUB_T(4)
     }
     b.x = vadd(b.x, DX);

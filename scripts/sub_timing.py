@@ -38,7 +38,7 @@ print(f"{NAME} B={B} waves={W}: wave ticks p50 {np.median(tot):.0f} max {tot.max
 phys = t[:, 2] - t[:, 1]
 print(f"physics (stamp 1->2) p50 {np.median(phys):.0f}")
 names = (("accel+kinetic", "joint", "wall position+update", "wall contact vel", "contact detect",
-          "ground position", "velocity projection", "ground contact vel") if LPE == 16 else
+          "(of which broadphase + face cull)", "velocity projection", "ground contact vel") if LPE == 16 else
          ("accel+kinetic", "joint", "position update", "contact vel (ground+wall)", "contact detect",
           "contact position (ground+wall)", "velocity projection", "-"))
 for i, n in zip(range(5, 13), names):
