@@ -232,11 +232,10 @@ POB_D void qmesh_items(csys_t &S, const float *LT, const float *WT, const uint32
 }
 
 // the walk's view of the lane's bodies: body l's segment, radius and kind (the torso is the
-// sphere at its centre).  The four-lane kernel walks per lane (pob_mesh.h mesh_lane_walk): at
-// four waves per SIMD the wave-cooperative walk measured slower (HH B = 65 536 0.1369 ->
-// 0.1598 ms, TAG 0.1238 -> 0.1415; profiles/r4h/ab1.txt) -- the SIMD is issue-bound, so the
-// cooperative round's idle-lane work and cross-lane traffic are not free, and its registers
-// pushed the 128-VGPR budget's spills from 160 to 224 B.
+// sphere at its centre).  (Round 4 walked per lane here -- the cooperative walk measured slower
+// at four waves per SIMD when its registers pushed the substep's spills up, profiles/r4h; round 5
+// made it call-free and spill-free, and the cooperative walk is the four-lane kernel's walk:
+// DESIGN.md §4 "Round-5 findings".)
 POB_D void qmesh_seg(csys_t &S, const float *LT, const QMesh &ms, const int l, v3 &A, v3 &B, float &r, bool &seg) {
   A = vsel3(l == 0, ms.a[0], vsel3(l == 1, ms.a[1], ms.a[2]));
   B = vsel3(l == 0, ms.b[0], vsel3(l == 1, ms.b[1], ms.b[2]));
@@ -262,15 +261,9 @@ POB_D void qpose_seg(csys_t &S, const float *LT, const QBody &b, const int l, v3
   seg = l != 0;
 }
 
-// Wall contact detection of a collide substep, at the pose the position pass projects from
-// (after the kinetic update, before the joint projection: the face walk's working set then
-// meets only the pose -- the velocities are dead until the velocity projection rewrites them,
-// the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
-// order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
-// its segments for the out-of-line re-walks (qwalls_rewalk).
-// the face walk of the detection, out of line (POB_QUAD_DETECT_OOL): the kernel's substep keeps
-// its allocation free of the walk's working set; a wave calls it only when one of its lanes
-// has a face item.  The pose comes by value, the store through the private block.
+// The face walk of the detection: the cooperative walk (every lane of the wave is active in
+// the substeps, step_quad_body) or, in the per-lane build (POB_QUAD_WAVE_WALK 0), each lane's
+// own walk out of line (qwalls_walk_ool).  The contacts go to the lane's store.
 template <bool LANE>
 POB_D void qwalls_walk(csys_t &S, const float *LT, const float *WT, const QBody &b, uint64_t (&M)[QNB], QWalls &ws) {
   GuardBranch g;
@@ -298,11 +291,7 @@ POB_D void qwalls_walk(csys_t &S, const float *LT, const float *WT, const QBody 
     ++ws.nct;
   });
 }
-#ifndef POB_QUAD_DETECT_OOL
-#define POB_QUAD_DETECT_OOL 0
-#endif
-// (the per-lane walk always out of line: the cooperative walk needs every lane of the wave,
-// so the batch's last wave walks per lane -- rare, and kept out of the substep's code)
+// (the per-lane build's walk, out of line: POB_QUAD_WAVE_WALK 0)
 __device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float *LT, const float *WT, v3 x0, v3 x1,
                                                        v3 x2, q4 q0, q4 q1, q4 q2, uint64_t m0, uint64_t m1,
                                                        uint64_t m2, QWalls *ws) {
@@ -321,7 +310,7 @@ __device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float
 // meets only the pose -- the velocities are dead until the velocity projection rewrites them,
 // the corrections not yet live).  The contacts (body, tau, n, dist) go to the store in walk
 // order (per body the oracle's (wall, face, triangle) order); a lane with more than QK keeps
-// its segments for the out-of-line re-walks (qwalls_rewalk).
+// its segments for the re-walks of the position and velocity passes (qwalls_rewalk_inl).
 // OVF false (the fast wall pass): a lane with more contacts than the store holds only reports
 // it in *ovf (the wave then runs the step again in the slow pass, OVF true: the detection-time
 // segments kept for the re-walks)
