@@ -752,23 +752,39 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   POB_TS(0);
   float *stg = lds + ((int)threadIdx.x >> 6) * POB_STAGE_FLOATS;  // this wave's region
   const Lds Ls{stg, 64, lane};
-  const int b = gt >> 2;
-  const int k = gt & 3;
+  int b = gt >> 2;
+  int k = gt & 3;
   const float *LT = legtab + k * POB_LEG_FLOATS;
   const float *WT = legtab + 4 * POB_LEG_FLOATS;
   const int kind = KIND != POB_MIXED ? KIND : S.kind;
   const int N = n_bodies<KIND>(S), D = obs_dim<KIND>(S);
   const int sh = obs_shift(kind);
-  const bool act_lane = b < B;
+  bool act_lane = b < B;
   // the wave's 16 envs are consecutive rows of every state array
-  const int b_first = (gt - lane) >> 2;
+  int b_first = (gt - lane) >> 2;
   if (b_first >= B) return;  // (wave-uniform: a block's waves past the batch; no barrier follows)
-  const int nenv = B - b_first < 16 ? B - b_first : 16;
-  const int le = b - b_first;
+  int nenv = B - b_first < 16 ? B - b_first : 16;
+  int le = b - b_first;
   // The physics runs on all 64 lanes (the wave walk's DPP / bpermute rounds need every lane):
   // the lanes past the batch in its last wave replay env B - 1 and store nothing.
-  const int bl = act_lane ? b : B - 1, lel = bl - b_first;
-  const size_t r3 = (size_t)bl * N * 3, r4 = (size_t)bl * N * 4;
+  int bl = act_lane ? b : B - 1, lel = bl - b_first;
+  size_t r3 = (size_t)bl * N * 3, r4 = (size_t)bl * N * 4;
+  // the same indices from an opaque copy of the thread index (after the substep loop: the copies
+  // above are then dead across it, instead of held -- in practice spilled -- through it)
+  auto rederive = [&]() {
+    int g2 = gt;
+    asm volatile("" : "+v"(g2));
+    b = g2 >> 2;
+    k = g2 & 3;
+    act_lane = b < B;
+    b_first = (g2 - (g2 & 63)) >> 2;
+    nenv = B - b_first < 16 ? B - b_first : 16;
+    le = b - b_first;
+    bl = act_lane ? b : B - 1;
+    lel = bl - b_first;
+    r3 = (size_t)bl * N * 3;
+    r4 = (size_t)bl * N * 4;
+  };
 
   // ---- state load: coalesced vector loads into the wave's region, then every lane
   // picks its bodies (the host sets POB_F_STAGED when the qp pointers are 16-B aligned
@@ -850,7 +866,6 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   TaskOut t;
   t.tp_ok = false;
   {
-    const float xb = bd.x[0].x;
     float a[QNJ];
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)bl * POB_NJ + 2 * k + jl];
@@ -858,6 +873,18 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
     for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
     const float fric = quad_friction(S);
+    // (per kind, bit 1 << KIND: HH 1, GA 2, TAG 4, ant 8, mixed 16 -- the register allocation of
+    // each instantiation reacts differently; profiles/r5x_ab.txt: HH B = 65 536 0.1873 ms with
+    // neither, TAG 0.1176 with both, GA 0.1147 and mixed fp16 B = 32 768 0.1281 with the
+    // re-derivation only; profiles/r5y_ab.txt)
+#ifndef POB_QUAD_FAST_PASS
+#define POB_QUAD_FAST_PASS 4
+#endif
+#ifndef POB_QUAD_REDERIVE
+#define POB_QUAD_REDERIVE 22
+#endif
+    constexpr int KBIT = KIND < 0 ? 16 : 1 << KIND;
+    constexpr bool FASTP = (POB_QUAD_FAST_PASS & KBIT) != 0, REDER = (POB_QUAD_REDERIVE & KBIT) != 0;
     if (LEG) {
       // legacy spring dynamics: every substep kinetic + springs + contact impulses
 #pragma nounroll
@@ -919,10 +946,10 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       reload();
       continue;
     }
-#ifndef POB_QUAD_FAST_PASS
-#define POB_QUAD_FAST_PASS 0
+#ifndef POB_QUAD_SLOW_OOL
+#define POB_QUAD_SLOW_OOL 1  // (with POB_QUAD_FAST_PASS: the slow pass's substep out of line)
 #endif
-    if (pass == 1 && WALLS && POB_QUAD_FAST_PASS) {
+    if (pass == 1 && WALLS && FASTP) {
       bool ovf = false;
 #pragma nounroll
       for (int it = 0; it < 2 * iters; ++it) {
@@ -956,12 +983,26 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
 #endif
+#if POB_QUAD_SLOW_OOL
+      if (WALLS && FASTP) {
+        QSlow st;
+        st.b = bd;
+#pragma unroll
+        for (int j = 0; j < QNJ; ++j) st.act[j] = a[j];
+        qpbd_substep_slow<WALLS>(Sp, LT, WT, &st, Ls.base, Ls.stride, Ls.t, (it & 1) != 0 ? 1 : 0, fric);
+        bd = st.b;
+      } else
+#endif
       qpbd_substep<WALLS>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric);
     }
     break;
     }
 #endif
     }
+    if constexpr (REDER) rederive();
+    // the torso's x at the step's start (the reward's displacement): loaded again (the state
+    // arrays are not written before the task tail)
+    const float xb = ld3<QT>(in.pos, r3).x;
     // joint angle / velocity obs of this lane's joints (a3)
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) {

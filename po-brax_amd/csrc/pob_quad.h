@@ -853,6 +853,26 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   }
 }
 
+// The slow wall pass's substep out of line (POB_QUAD_SLOW_OOL): the step's state through a
+// private block, so the substep loop of the fast pass carries neither the re-walks' code nor
+// a call's register constraints (a wave runs the slow pass only after a contact-store overflow)
+struct QSlow {
+  QBody b;
+  float act[QNJ];
+};
+template <bool WALLS>
+__device__ __attribute__((noinline)) void qpbd_substep_slow(csys_t *Sp, const float *LT, const float *WT, QSlow *st,
+                                                           float *lbase, const int lstride, const int lt, const int collide,
+                                                           const float fric) {
+  QBody b = st->b;
+  float act[QNJ];
+#pragma unroll
+  for (int j = 0; j < QNJ; ++j) act[j] = st->act[j];
+  const Lds L{lbase, lstride, lt};
+  qpbd_substep<WALLS>(Sp, LT, WT, b, act, L, collide != 0, fric);
+  st->b = b;
+}
+
 // ------------------------------------------------------------- legacy spring dynamics
 // brax <= 0.0.12 spring/impulse step (oracle legacy_substep; pinned by the 20 frames of
 // notebooks/ant_tag.ipynb:449) on the same lane quads: kinetic, then spring joints + torque
