@@ -95,3 +95,22 @@ def test_obs_mask_errors():
         envs.create("ant_heavenhell", batch_size=8, obs_mask=[0.5])
     env = envs.create("ant_heavenhell", batch_size=8)
     assert env.masked_observation_size == 0 and env.obs_mask is None
+
+
+def test_obs_mask_mixed_launch():
+    """The mixed launch (config 5's one kernel for HH + GA + TAG): every segment stores its own
+    kind's masked columns (each env's table holds its mask; indices valid for all three)."""
+    from po_brax_amd import jumpy
+    envs = _envs()
+    idx = np.array([0, 1, 2, 14, 15, 28, 29, 60, 102], np.int64)
+    names = ["ant_heavenhell", "ant_gather", "ant_tag"]
+    mix = envs.create_mixed(names, episode_length=3, qp_dtype=torch.float16, obs_mask=idx)
+    sizes = [700, 500, 301]
+    key = jumpy.random_prngkey(4)
+    ms = mix.reset(key, sizes)
+    act = torch.empty((sum(sizes), 8), device="cuda")
+    for t in range(4):
+        jumpy.random_actions_(key, sum(sizes), 0, act)
+        ms = mix.step_(ms, [a.contiguous() for a in mix.split_actions(act)])
+        for n, s in zip(names, ms):
+            _check(s, idx, f"mixed {n} step {t}")
