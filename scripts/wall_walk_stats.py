@@ -55,10 +55,32 @@ for lay, lanes in LAYOUTS.items():
     epw = 64 // len(lanes)
     W = per_lane.reshape(steps, B // epw, epw, NSUB, len(lanes)).transpose(0, 1, 3, 2, 4).reshape(steps, B // epw, NSUB, 64)
     wmax, wtot = W.max(-1), W.sum(-1)
-    rounds = np.maximum(np.ceil(wtot / 4), wmax * 0)  # cooperative: four items a round
+    rounds = np.maximum(np.ceil(wtot / 4), wmax * 0)  # round 4's cooperative walk: four items a round
+    # round 5's walk (pob_mesh.h mesh_wave_walk): eight groups a round, a lane's first and
+    # second items; "rank-major": eight groups from any lane's next items
+    def _rounds(w, cap):
+        w = w.copy()
+        n = np.zeros(w.shape[:-1])
+        while (w > 0).any():
+            live = (w > 0).any(-1)
+            take = np.zeros_like(w)
+            left = np.full(w.shape[:-1], 8)
+            for r in range(cap):
+                has = (w - take) > 0
+                cum = np.cumsum(has, -1)
+                sel = has & (cum <= left[..., None])
+                take += sel
+                left = left - sel.sum(-1)
+            w -= take
+            n += live
+        return n
+    r8 = _rounds(W, 2)
+    rrm = _rounds(W, 8)
     per_step_lane = wmax.sum(-1)  # per-lane walk iterations per step per wave
     per_step_coop = rounds.sum(-1)
     print(f"  {lay:13s} items/lane {per_lane.mean():.3f}; per wave-substep busiest lane {wmax.mean():.2f} "
           f"(max {wmax.max()}), total {wtot.mean():.2f} (p99 {np.percentile(wtot, 99):.0f}, max {wtot.max()}), "
           f"coop rounds {rounds.mean():.2f}; per step and wave: lane-walk iterations mean {per_step_lane.mean():.1f} "
           f"max {per_step_lane.max()}, coop rounds mean {per_step_coop.mean():.1f} max {per_step_coop.max()}")
+    print(f"  {'':13s} 8 groups, 2 items per lane and round: rounds per step and wave mean {r8.sum(-1).mean():.2f} "
+          f"max {r8.sum(-1).max():.0f}; rank-major: mean {rrm.sum(-1).mean():.2f} max {rrm.sum(-1).max():.0f}")
