@@ -111,15 +111,14 @@ struct QMesh {
   v3 a[QNB], b[QNB];
 };
 // The lane's wall contacts of a collide substep (pob_mesh.h, brax capsule x TriangulatedBox):
-// the position pass walks the lane's face items with each segment formed from the detection
-// pose when the walk needs it (x, q: the pose the position pass projects from, unchanged until
-// its end), applies every contact as it is found and keeps the first QK (body, tau, n, dist)
-// in a private array for the velocity pass.  A lane with more keeps its detection-time
-// segments instead (a second private array, written only then) and its velocity pass re-walks
-// every face the cull keeps from them -- the same operations on the same operands: the same
-// contacts in the same order.  Nothing of this is live in registers between the passes but
-// the count, so the walk's working set does not push the substep's state out of the 128-VGPR
-// budget.
+// the detection (before the joint projection, at the pose the position pass projects from)
+// walks the lane's face items -- M[l] bit 8 w + f per body l -- with each segment formed from
+// that pose when the walk needs it, and keeps the first QK contacts (body, tau, n, dist) in a
+// private array in walk order; the position and velocity passes apply them from there.  A lane
+// with more keeps its detection-time segments instead (a second private array, written only
+// then) and both passes re-walk every face the cull keeps from them (qwalls_rewalk_inl) -- the
+// same operations on the same operands: the same contacts in the same order.  Nothing of this
+// is live in registers between the passes but the count.
 #define QK 8
 struct QWalls {
   int nct;                // wall contacts of the position pass
