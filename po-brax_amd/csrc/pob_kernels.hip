@@ -742,7 +742,19 @@ __device__ __forceinline__ void quad_store_dyn(const StatePtrs &in, const StateP
   }
 }
 
-template <int KIND, typename QT, bool LEG = false>
+// Wall-contact overflow handling of the four-lane kernel (MODE): 0 = in the kernel (the position
+// and velocity passes re-walk an overflowing lane's faces); 1 = the fast launch: a wave with an
+// overflowing lane stores nothing but POB_OVF_MARK in its first env's first obs element and
+// exits; 2 = the fix-up launch right after it: only the marked waves run, the whole step with
+// the re-walks.  The re-walk code's mere presence in the substep loop cost 15 % (HH) through
+// register pressure (profiles/r6a_ab.txt); split, the common launch carries none of it.  The
+// mark lives in the state's own obs buffer (obs is an output only: no kernel reads it), so
+// concurrent launches on disjoint state slices (GraphRollout groups) do not interfere.
+#define POB_OVF_MARK 0x7FA5A5A5u  // a signalling NaN with a payload: no arithmetic produces it
+// (test hook: POB_QUAD_FORCE_FIXUP=1 makes the fast launch hand every wave to the fix-up launch,
+// so the parity tests run the fix-up path on every env; an internal flags bit)
+#define POB_F_INT_FORCE_FIXUP (1u << 30)
+template <int KIND, typename QT, bool LEG = false, int MODE = 0>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
                           const float *legtab) {
@@ -763,6 +775,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   // the wave's 16 envs are consecutive rows of every state array
   int b_first = (gt - lane) >> 2;
   if (b_first >= B) return;  // (wave-uniform: a block's waves past the batch; no barrier follows)
+  if (MODE == 2 && __float_as_uint(out.obs[(size_t)b_first * D]) != POB_OVF_MARK) return;  // (not marked)
   int nenv = B - b_first < 16 ? B - b_first : 16;
   int le = b - b_first;
   // The physics runs on all 64 lanes (the wave walk's DPP / bpermute rounds need every lane):
@@ -949,7 +962,29 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #ifndef POB_QUAD_SLOW_OOL
 #define POB_QUAD_SLOW_OOL 1  // (with POB_QUAD_FAST_PASS: the slow pass's substep out of line)
 #endif
-    if (pass == 1 && WALLS && FASTP) {
+    if (MODE == 1 && WALLS) {
+      // the fast launch: the store only; a wave with an overflowing lane leaves the step to the
+      // fix-up launch (nothing of its state is written: every output store follows the physics)
+      bool ovf = false;
+#pragma nounroll
+      for (int it = 0; it < 2 * iters; ++it) {
+#if POB_QUAD_PRIO == 1
+        const int lvl = (it * 4) / (2 * iters);
+        if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
+        qpbd_substep<WALLS, false, false>(Sp, LT, WT, bd, a, Ls, (it & 1) != 0, fric, nullptr, &ovf);
+        if (__any(ovf)) break;
+      }
+      if (__any(ovf) || (flags & POB_F_INT_FORCE_FIXUP)) {
+        if (lane == 0) out.obs[(size_t)b_first * D] = __uint_as_float(POB_OVF_MARK);
+        return;
+      }
+      break;
+    }
+    if (pass == 1 && WALLS && FASTP && MODE == 0) {
       bool ovf = false;
 #pragma nounroll
       for (int it = 0; it < 2 * iters; ++it) {
@@ -984,7 +1019,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       else __builtin_amdgcn_s_setprio(0);
 #endif
 #if POB_QUAD_SLOW_OOL
-      if (WALLS && FASTP) {
+      if (WALLS && FASTP && MODE == 0) {
         QSlow st;
         st.b = bd;
 #pragma unroll
@@ -1180,7 +1215,17 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   POB_TS_WRITE();
 }
 
-template <int KIND, typename QT>
+// MODE 2 (the fix-up launch): does any wave of the block carry the overflow mark?  (before
+// the block's table staging: a block without one exits at once)
+POB_D bool quad_block_marked(const int B, const int D, const float *obs, const int bt0) {
+  bool any = false;
+  for (int w = 0; w < (int)blockDim.x / 64; ++w) {
+    const int bf = (bt0 + 64 * w) >> 2;
+    if (bf < B) any = any | (__float_as_uint(obs[(size_t)bf * D]) == POB_OVF_MARK);
+  }
+  return any;
+}
+template <int KIND, typename QT, int MODE = 0>
 __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const void *sysp, const int B,
                                                                        const StatePtrs in,
                                                                        const float *__restrict__ act,
@@ -1188,9 +1233,11 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
                                                                        const int L) {
   __shared__ float lds[QL_FLOATS * 256];
   __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
+  if (MODE == 2 && !quad_block_marked(B, obs_dim<KIND>(*(csys_t *)(size_t)sysp), out.obs, (int)(blockIdx.x * blockDim.x)))
+    return;
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
-  step_quad_body<KIND, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
-                           (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
+  step_quad_body<KIND, QT, false, MODE>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+                                        (int)(blockIdx.x * blockDim.x + threadIdx.x), lds, legtab);
 }
 
 // AntGather at most three waves per SIMD (B <= 3 x 16 x SIMDs): the same kernel with the
@@ -1246,7 +1293,7 @@ POB_D const void *uniform_ptr(const void *p) {
 #ifndef POB_MIXED_MIN_WAVES
 #define POB_MIXED_MIN_WAVES 3  // config 5 runs 2 waves per SIMD: 170 VGPRs, no spills (128: 144 B of scratch, +6 %)
 #endif
-template <typename QT>
+template <typename QT, int MODE = 0>
 __global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const MixArgs A, const uint32_t flags,
                                                                         const int L) {
   __shared__ float lds[QL_FLOATS * 256];
@@ -1274,8 +1321,10 @@ __global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const M
   const float *act = POB_PICK(act);
   const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
 #undef POB_PICK
+  if (MODE == 2 && !quad_block_marked(B, obs_dim<POB_MIXED>(*(csys_t *)(size_t)sysp), out.obs, (bx - blk0) * 256))
+    return;
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
-  step_quad_body<POB_MIXED, QT>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
+  step_quad_body<POB_MIXED, QT, false, MODE>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
                                 (bx - blk0) * 256 + (int)threadIdx.x, lds, legtab);
 }
 
@@ -2769,6 +2818,21 @@ static void launch_step_oct(int kind, int n_cu, hipStream_t st, const void *sp, 
   if (acc) launch_step_oct_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
   else launch_step_oct_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
 }
+// The fast + fix-up launches per kind (bit 1 << kind, mixed 16): HH B = 65 536 0.1877 ->
+// 0.1634 ms, TAG 0.1192 -> 0.1055, GA 0.1148 -> 0.1145, mixed fp16 B = 32 768 0.1281 -> 0.1316
+// (profiles/r6b_ab.txt, r6c_ab.txt); POB_QUAD_SPLIT=0 / 1 forces the one-launch form / the split.
+#ifndef POB_QUAD_SPLIT_KINDS
+#define POB_QUAD_SPLIT_KINDS 7
+#endif
+static bool quad_split_launch(int kind) {
+  const char *f = getenv("POB_QUAD_SPLIT");
+  if (f) return atoi(f) != 0;
+  return ((POB_QUAD_SPLIT_KINDS >> (kind < 0 ? 4 : kind)) & 1) != 0;
+}
+static uint32_t quad_force_fixup() {
+  const char *f = getenv("POB_QUAD_FORCE_FIXUP");
+  return f && atoi(f) != 0 ? POB_F_INT_FORCE_FIXUP : 0u;
+}
 template <typename QT>
 static void launch_step_quad(int kind, bool legacy, int n_cu, hipStream_t st, const void *sp, int B,
                              const StatePtrs &pi, const float *act, const StatePtrs &po, uint32_t flags, int L) {
@@ -2790,10 +2854,34 @@ static void launch_step_quad(int kind, bool legacy, int n_cu, hipStream_t st, co
     hipLaunchKernelGGL((k_step_quad_ga3<QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
     return;
   }
+  // walls: the fast launch, then the fix-up launch of its overflowing waves (MODE 1 / 2 above)
+  const bool split = quad_split_launch(kind);
+  flags |= split ? quad_force_fixup() : 0u;
   switch (kind) {
-    case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_GATHER: hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
-    case POB_TAG: hipLaunchKernelGGL((k_step_quad<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
+    case POB_HEAVENHELL:
+      if (split) {
+        hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT, 1>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+        hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT, 2>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      } else {
+        hipLaunchKernelGGL((k_step_quad<POB_HEAVENHELL, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      }
+      break;
+    case POB_GATHER:
+      if (split) {
+        hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT, 1>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+        hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT, 2>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      } else {
+        hipLaunchKernelGGL((k_step_quad<POB_GATHER, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      }
+      break;
+    case POB_TAG:
+      if (split) {
+        hipLaunchKernelGGL((k_step_quad<POB_TAG, QT, 1>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+        hipLaunchKernelGGL((k_step_quad<POB_TAG, QT, 2>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      } else {
+        hipLaunchKernelGGL((k_step_quad<POB_TAG, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      }
+      break;
     default: hipLaunchKernelGGL((k_step_quad<POB_ANT, QT>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
 }
@@ -2992,8 +3080,20 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   if (stage) flags |= POB_F_STAGED;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blk);
-  if (envs[0]->sys.qp_f16) hipLaunchKernelGGL((k_step_mixed<__half>), g, dim3(256), 0, st, A, flags, episode_length);
-  else hipLaunchKernelGGL((k_step_mixed<float>), g, dim3(256), 0, st, A, flags, episode_length);
+  if (quad_split_launch(POB_MIXED)) {  // the fast launch, then the fix-up launch of its overflowing waves
+    flags |= quad_force_fixup();
+    if (envs[0]->sys.qp_f16) {
+      hipLaunchKernelGGL((k_step_mixed<__half, 1>), g, dim3(256), 0, st, A, flags, episode_length);
+      hipLaunchKernelGGL((k_step_mixed<__half, 2>), g, dim3(256), 0, st, A, flags, episode_length);
+    } else {
+      hipLaunchKernelGGL((k_step_mixed<float, 1>), g, dim3(256), 0, st, A, flags, episode_length);
+      hipLaunchKernelGGL((k_step_mixed<float, 2>), g, dim3(256), 0, st, A, flags, episode_length);
+    }
+  } else if (envs[0]->sys.qp_f16) {
+    hipLaunchKernelGGL((k_step_mixed<__half>), g, dim3(256), 0, st, A, flags, episode_length);
+  } else {
+    hipLaunchKernelGGL((k_step_mixed<float>), g, dim3(256), 0, st, A, flags, episode_length);
+  }
   return hip_check(hipGetLastError(), "k_step_mixed launch");
 }
 

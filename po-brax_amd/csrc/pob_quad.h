@@ -119,7 +119,9 @@ struct QMesh {
 // then) and both passes re-walk every face the cull keeps from them (qwalls_rewalk_inl) -- the
 // same operations on the same operands: the same contacts in the same order.  Nothing of this
 // is live in registers between the passes but the count.
-#define QK 8
+#ifndef QK
+#define QK 12  // (8: HH B = 65 536 0.2038 ms with the split launch, 12: 0.1634 -- fewer fix-up waves; 16, 24: the same; profiles/r6c_ab.txt)
+#endif
 struct QWalls {
   int nct;                // wall contacts of the position pass
   float c[6 * QK];        // the first QK: body, tau, n, dist
@@ -511,7 +513,9 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBod
   }
   if (!OVF) return;  // (the fast pass: a wave with an overflow runs the step again)
 #if POB_QUAD_REWALK_INLINE
-  if (__any(ovf)) qwalls_rewalk_inl<false>(S, LT, WT, b, L, ws, ovf, fric, DX, DA);
+#ifndef POB_EXP_NO_REWALK
+  if (__any(ovf)) qwalls_rewalk_inl<false>(S, LT, WT, b, L, ws, ovf, fric, DX, DA);  // (timing experiment: off)
+#endif
   if (false) {
 #else
   if (__any(ovf)) {
@@ -570,7 +574,9 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, QBod
   }
   if (!OVF) return;  // (the fast pass: a wave with an overflow runs the step again)
 #if POB_QUAD_REWALK_INLINE
+#ifndef POB_EXP_NO_REWALK
   if (__any(ovf)) qwalls_rewalk_inl<true>(S, LT, WT, b, Lds{nullptr, 0, 0}, ws, ovf, fric, dV, dW);
+#endif
   if (false) {
 #else
   if (__any(ovf)) {

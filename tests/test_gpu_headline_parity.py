@@ -352,3 +352,41 @@ def test_config5_mixed_fp16_full_global_batch_properties():
         assert bool((st.info["steps"] <= 5).all()), name
     assert s[2].done.dtype == torch.bool and s[1].metrics["apples"].dtype == torch.int32
     assert all(bool((st.aux["done"] != 0).all()) for st in s)  # step 5 of 5: the time limit
+
+
+@pytest.mark.parametrize("name,B", [("ant_heavenhell", 16400), ("ant_tag", 16400), ("ant_gather", 65536)])
+def test_fixup_launch_parity(monkeypatch, name, B):
+    """The four-lane kernel's split launch (pob_kernels.hip MODE 1 / 2): every wave forced
+    through the fix-up launch (POB_QUAD_FORCE_FIXUP=1: the fast launch marks every wave and
+    stores nothing, the fix-up launch steps the marked waves with the in-kernel re-walks) is
+    bit-exact against the oracle; the one-launch form (POB_QUAD_SPLIT=0) too."""
+    monkeypatch.setenv("POB_QUAD_FORCE_FIXUP", "1")
+    _per_step(name, B, T=4, seed=21)
+    monkeypatch.delenv("POB_QUAD_FORCE_FIXUP")
+    monkeypatch.setenv("POB_QUAD_SPLIT", "0")
+    _per_step(name, B, T=4, seed=22)
+
+
+def test_fixup_launch_mixed_forced(monkeypatch):
+    """The mixed launch as one launch, split, and split with every wave forced through the
+    fix-up launch: bit for bit the same states."""
+    from po_brax_amd import jumpy
+    envs = _envs()
+    names = ["ant_heavenhell", "ant_gather", "ant_tag"]
+    sizes = [6000, 5000, 4001]
+    outs = []
+    for split, force in (("0", "0"), ("1", "0"), ("1", "1")):  # one launch; split; split, all fixed up
+        monkeypatch.setenv("POB_QUAD_SPLIT", split)
+        monkeypatch.setenv("POB_QUAD_FORCE_FIXUP", force)
+        mix = envs.create_mixed(names, episode_length=3, qp_dtype=torch.float16)
+        key = jumpy.random_prngkey(9)
+        ms = mix.reset(key, sizes)
+        act = torch.empty((sum(sizes), 8), device="cuda")
+        for t in range(4):
+            jumpy.random_actions_(key, sum(sizes), 0, act)
+            ms = mix.step_(ms, [a.contiguous() for a in mix.split_actions(act)])
+        outs.append([(s.qp.pos.clone(), s.obs.clone(), s.reward.clone()) for s in ms])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
