@@ -340,6 +340,8 @@ def main() -> int:
     tflops = f_exe * B / ks / 1e12
     kname = "k_step_mixed" if args.env == "mixed" else (
         f"k_step_legacy<{args.env}>" if args.legacy_spring else f"{step_kernel(B)}<{args.env}>")
+    if split_launch(args.env, B, args.legacy_spring):
+        kname += " fast launch + fix-up launch (kernel_ms: both; traffic / valu: the fast launch)"
     roofline = {
         "bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TF, "unit": "TFLOP/s",
         "frac": round(tflops / VALU_PEAK_TF, 5), "traffic": None,
@@ -622,6 +624,19 @@ def step_kernel(B: int) -> str:
     if B <= int(os.environ.get("POB_OCTET_MAX_B", "16384")):
         return "k_step_oct"
     return "k_step_quad"
+
+
+def split_launch(env: str, B: int, legacy: bool) -> bool:
+    """Does pob_step launch the four-lane kernel as a fast launch + a fix-up launch here
+    (pob_kernels.hip quad_split_launch: HH, GA, TAG on the four-lane kernel; GA at <= 3 waves
+    per SIMD and the mixed launch stay one launch; POB_QUAD_SPLIT overrides)?"""
+    if legacy or env in ("ant", "mixed") or step_kernel(B) != "k_step_quad":
+        return False
+    n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    if env == "ant_gather" and 4 * B <= 3 * 64 * 4 * n_cu:
+        return False
+    f = os.environ.get("POB_QUAD_SPLIT")
+    return int(f) != 0 if f else True
 
 
 def committed_profile(env: str, B: int, qp: str, legacy: bool = False, lib_sha256: str = None,
