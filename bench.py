@@ -4,7 +4,8 @@
 Workload (BASELINE.json configs / SURVEY.md §8(d)): AntHeavenHell, batch 65 536 (the
 metric's "batch 65536 @1/2/4/8 GPU": the global batch split over the N ranks), brax chain ``create('ant_heavenhell', batch_size=B)`` = AutoReset(Vmap(Episode(ActionRepeat
 (env)))) with episode_length 1000, i.e. ONE fused HIP kernel per env-step (PBD physics,
-POMDP logic, obs, episode counter, autoreset).  Synthetic inputs as the survey prescribes:
+POMDP logic, obs, episode counter, autoreset; the four-lane kernel as a fast launch plus a
+fix-up launch that steps only the rare waves whose wall-contact store overflowed).  Synthetic inputs as the survey prescribes:
 ``key = PRNGKey(0)``, reset keys ``split(key, B_total + 1)[1:]`` (sharded by index), per step
 ``key, k = split(key)``, ``action = uniform(k, (B_total, 8), -1, 1)`` -- all generated on the
 device by the threefry kernels BEFORE the timed region (inputs resident in HBM).
