@@ -340,7 +340,7 @@ def main() -> int:
     hbm_gbs = bpe * B / ks / 1e9
     tflops = f_exe * B / ks / 1e12
     kname = "k_step_mixed" if args.env == "mixed" else (
-        f"k_step_legacy<{args.env}>" if args.legacy_spring else f"{step_kernel(B)}<{args.env}>")
+        f"k_step_legacy<{args.env}>" if args.legacy_spring else f"{step_kernel(B, args.env)}<{args.env}>")
     if split_launch(args.env, B, args.legacy_spring):
         kname += " fast launch + fix-up launch (kernel_ms: both; traffic / valu: the fast launch)"
     roofline = {
@@ -615,12 +615,13 @@ def rank_devices(dev, world: int) -> list:
     return out
 
 
-def step_kernel(B: int) -> str:
+def step_kernel(B: int, env: str = "ant_heavenhell") -> str:
     """The step kernel pob_step launches for a batch of B envs (pob_kernels.hip pob_step:
-    sixteen lanes per env up to POB_HEXA_MAX_B (16 x the CU count: 4 096 on MI355X), eight up
-    to POB_OCTET_MAX_B (16 384), four above)."""
+    sixteen lanes per env up to POB_HEXA_MAX_B (per kind: HH 48, TAG 32, else 16 x the CU
+    count), eight up to POB_OCTET_MAX_B (16 384), four above)."""
     n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    if B <= int(os.environ.get("POB_HEXA_MAX_B", str(16 * n_cu))):
+    hex_default = {"ant_heavenhell": 48, "ant_tag": 32}.get(env, 16) * n_cu
+    if B <= int(os.environ.get("POB_HEXA_MAX_B", str(hex_default))):
         return "k_step_hex"
     if B <= int(os.environ.get("POB_OCTET_MAX_B", "16384")):
         return "k_step_oct"
@@ -631,7 +632,7 @@ def split_launch(env: str, B: int, legacy: bool) -> bool:
     """Does pob_step launch the four-lane kernel as a fast launch + a fix-up launch here
     (pob_kernels.hip quad_split_launch: HH, GA, TAG on the four-lane kernel; GA at <= 3 waves
     per SIMD and the mixed launch stay one launch; POB_QUAD_SPLIT overrides)?"""
-    if legacy or env in ("ant", "mixed") or step_kernel(B) != "k_step_quad":
+    if legacy or env in ("ant", "mixed") or step_kernel(B, env) != "k_step_quad":
         return False
     n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     if env == "ant_gather" and 4 * B <= 3 * 64 * 4 * n_cu:

@@ -2761,17 +2761,26 @@ static int octet_max_batch() {
   const char *e = getenv("POB_OCTET_MAX_B");
   return e ? atoi(e) : 16384;
 }
-// sixteen lanes per env while its waves fit one per SIMD: B <= 4 envs x 4 SIMDs x n_cu (4 096
-// on 256 CUs; POB_HEXA_MAX_B overrides; 0 disables).  At two waves per SIMD the eight-lane
+// sixteen lanes per env (POB_HEXA_MAX_B overrides the per-kind limit below; 0 disables).
+// Round 3 (the spring contact model): one wave per SIMD, B <= 4 envs x 4 SIMDs x n_cu (4 096
+// on 256 CUs).  At two waves per SIMD the eight-lane
 // kernel (one wave per SIMD up to B = 8 192) is faster: interleaved A/B, kernel ms
 // (profiles/r3k/kernel_select.txt)
 //                B:  5 120           6 144           7 168           8 192
 //   HH  hex / oct:   0.0371/0.0366   0.0379/0.0365   0.0384/0.0372   0.0388/0.0373
 //   TAG hex / oct:   0.0358/0.0346   0.0376/0.0348   0.0369/0.0350   0.0372/0.0354
 // while at B = 4 096 the sixteen-lane kernel is 19 % faster (HH 0.0295 / 0.0363).
-static int hexa_max_batch(int n_cu) {
+// Round 5 (brax's spelling: the wall walk dominates small batches): per kind, interleaved A/B
+// (profiles/r6h_ab.txt, r6i_ab.txt), hex / oct kernel ms --
+//   HH   B = 6 144 0.0715 / 0.0998, 8 192 0.0750 / 0.1009, 12 288 0.1036 / 0.1098, 16 384 0.1178 / 0.1149
+//   TAG  B = 6 144 0.0502 / 0.0488, 8 192 0.0514 / 0.0541, 12 288 0.0751 / 0.0645
+//   GA   B = 6 144 0.0374 / 0.0356, 8 192 0.0381 / 0.0369
+// so the sixteen-lane kernel runs HH up to 3 waves per SIMD (48 x CUs: 12 288), TAG up to 2
+// (8 192), GA and the stock ant up to 1.
+static int hexa_max_batch(int n_cu, int kind) {
   const char *e = getenv("POB_HEXA_MAX_B");
-  return e ? atoi(e) : 16 * n_cu;
+  if (e) return atoi(e);
+  return (kind == POB_HEAVENHELL ? 48 : (kind == POB_TAG ? 32 : 16)) * n_cu;
 }
 template <typename QT, bool GACC>
 static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
@@ -2786,8 +2795,8 @@ static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, c
 }
 // Up to one wave per SIMD (B <= the SIMD count x 4 envs: the default batch range of this
 // kernel) the wave's dependency chain is the step time and the guard branches split it
-// (GuardAcc, measured HH B=4 096 -3.5 %); with two or more waves per SIMD (a POB_HEXA_MAX_B
-// override) the other wave hides them and the accumulator's VALU operations cost (B = 8 192:
+// (GuardAcc, measured HH B=4 096 -3.5 %); with two or more waves per SIMD (HH and TAG above
+// 16 x CUs, or a POB_HEXA_MAX_B override) the other wave hides them and the accumulator's VALU operations cost (B = 8 192:
 // TAG / GA +1 %), so the branch guards stay.  POB_HEX_GACC=0/1 forces either.
 template <typename QT>
 static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
@@ -3040,7 +3049,7 @@ int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
   const void *sp = (const void *)e->d_sys;
-  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch(e->n_cu) &&  // legacy: lane quads only
+  const bool hex = e->sys.oct_ok && !e->sys.legacy && B <= hexa_max_batch(e->n_cu, e->sys.kind) &&  // legacy: lane quads only
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);
   const bool oct = e->sys.oct_ok && !e->sys.legacy && B <= octet_max_batch() &&
                    e->sys.n_walls <= hex_max_walls(e->sys.kind);

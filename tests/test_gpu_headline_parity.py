@@ -1,7 +1,8 @@
 """GPU parity at the BASELINE.json batch sizes, on the launch paths the bench takes.
 
 ``pob_step`` runs the sixteen-lanes-per-env kernel (``k_step_hex``) while its waves fit one
-per SIMD (B <= 16 x the CU count: 4 096 on MI355X; ``POB_HEXA_MAX_B`` overrides), the
+up to a per-kind batch (HH 48, TAG 32, GA and the stock ant 16 x the CU count: 12 288 / 8 192 /
+4 096 on MI355X; ``POB_HEXA_MAX_B`` overrides), the
 eight-lane kernel (``k_step_oct``) for B <= 16 384 and the four-lane kernel (``k_step_quad``)
 above -- with one-wave (64-thread) blocks when the smaller-batch kernels are disabled
 (``POB_HEXA_MAX_B=0``, ``POB_OCTET_MAX_B=0``) and B <= 4 096, 256-thread blocks otherwise; the
@@ -179,12 +180,33 @@ def test_octet_quad_switch_prefix_identical():
     _prefix_identical(16384, 16385)
 
 
-def test_hexa_octet_switch_prefix_identical():
-    """At the default switch (16 x the CU count): the first n envs of a B = n + 1 run
+def test_hexa_octet_switch_prefix_identical(monkeypatch):
+    """At a switch of 16 x the CU count (the default for AntGather and the stock ant; HH and TAG
+    switch later, pob_kernels.hip hexa_max_batch): the first n envs of a B = n + 1 run
     (eight-lane kernel) equal a B = n run (sixteen-lane kernel) bit for bit, fp32 and fp16
     storage, for every kind."""
     n = 16 * torch.cuda.get_device_properties(0).multi_processor_count
+    monkeypatch.setenv("POB_HEXA_MAX_B", str(n))
     _prefix_identical(n, n + 1)
+
+
+def test_hexa_default_switch_prefix_identical():
+    """At the per-kind default switches (HH 48 x CUs, TAG 32 x CUs): B = n + 1 (eight- or
+    four-lane kernel) against B = n (sixteen-lane kernel at three / two waves per SIMD)."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    envs = _envs()
+    for name, n in (("ant_heavenhell", 48 * n_cu), ("ant_tag", 32 * n_cu)):
+        keys = torch.from_numpy(_keys(n + 1, 3)).cuda()
+        ea = envs.create(name, batch_size=n, episode_length=5)
+        eb = envs.create(name, batch_size=n + 1, episode_length=5)
+        sa, sb = ea.reset(keys[:n].contiguous()), eb.reset(keys)
+        for act in _actions(7, n + 1, 6):
+            a = torch.from_numpy(act).cuda()
+            sa = ea.step_(sa, a[:n].contiguous())
+            sb = eb.step_(sb, a)
+        for f in ("pos", "rot", "vel", "ang"):
+            assert torch.equal(getattr(sa.qp, f), getattr(sb.qp, f)[:n]), (name, f)
+        assert torch.equal(sa.obs, sb.obs[:n]), name
 
 
 def test_hexa_octet_switch_prefix_identical_8192(monkeypatch):
