@@ -92,20 +92,22 @@ def test_per_step_parity_eight_lane_small(monkeypatch, B):
 
 @pytest.mark.parametrize("name,B", [("ant_heavenhell", 8192), ("ant_tag", 8192), ("ant_gather", 8191), ("ant", 8190)])
 def test_per_step_parity_sixteen_lane(monkeypatch, name, B):
-    """The sixteen-lane kernel at two waves per SIMD (config 4's per-GPU TAG batch; selected
-    by POB_HEXA_MAX_B, the default launches the eight-lane kernel there)."""
+    """The sixteen-lane kernel at two waves per SIMD (config 4's per-GPU TAG batch: the default
+    launch for HH and TAG there; POB_HEXA_MAX_B selects it for GA and the stock ant)."""
     monkeypatch.setenv("POB_HEXA_MAX_B", "8192")
     _per_step(name, B, seed=5)
 
 
 @pytest.mark.parametrize("name,B", [("ant_heavenhell", 8192), ("ant_tag", 8192), ("ant_gather", 8191)])
-def test_per_step_parity_eight_lane_default(name, B):
-    """The eight-lane kernel at config 4's per-GPU batch (the default launch there)."""
+def test_per_step_parity_eight_lane_8192(monkeypatch, name, B):
+    """The eight-lane kernel at config 4's per-GPU batch (the default launch there for GA;
+    HH and TAG with the sixteen-lane kernel disabled)."""
+    monkeypatch.setenv("POB_HEXA_MAX_B", "0")
     _per_step(name, B, seed=6)
 
 
 @pytest.mark.parametrize("name", ["ant_heavenhell", "ant_gather", "ant_tag", "ant"])
-@pytest.mark.parametrize("B", [4096, 8192, 16400])  # the sixteen-, eight- and four-lane kernels
+@pytest.mark.parametrize("B", [4096, 8192, 16400])  # sixteen-lane; sixteen (HH, TAG) or eight; four
 def test_free_running_300_steps(name, B):
     """GPU and oracle each run 300 steps from the same reset with no restart (episode length
     100: three autoresets per env on the way), every kernel's default batch range: any float
