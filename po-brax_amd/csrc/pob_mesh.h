@@ -608,6 +608,61 @@ POB_D void mtie_add(const float key, const float dmin, const F3 S, const F3 P, c
   }
 }
 
+// mface_cand on a triangle's quad (lane kk of the quad holds candidate kk; every lane of the
+// quad active): the segment-plane candidate's three triangle-edge projections (btri_point's
+// c1..c3) are computed by the edge lanes beside their own candidates and read by lane 3 over
+// DPP -- the same operations on the same operands as btri_point, one divergent path shorter
+template <class G>
+POB_D MCand mface_cand_quad(G &g, const MFace &F, const int t, const int kk, F3 &S, F3 &P) {
+  MCand c;
+  c.d2 = __builtin_inff(); c.u = 0.0f; c.da = 0.0f; c.db = 0.0f; c.dw = 0.0f;
+  S = f3(0.0f, 0.0f, 0.0f);
+  P = S;
+  const float tt = mface_tt(g, F);
+  const F3 S3 = f3fma(F.A.d, tt, F.A.p0);  // the segment-plane point (lane 3's S)
+  F3 cq = S;
+  float dq = 0.0f;
+  if (kk < 3) {
+    const int e = t == 0 ? kk : (kk == 0 ? 2 : kk + 2);
+    float u;
+    bseg_seg(g, F.A, medge(F, e), S, P, u);
+    c = bcand(S, P, u);
+    // btri_point's edge kk + 1: s01, s12, s20 = V0 V1, V1 V2, V2 V0 (t0) / V0 V2, V2 V3, V3 V0 (t1)
+    const int te = kk < 2 ? e : (t == 0 ? 5 : 6);
+    float tq;
+    cq = bseg_point(medge(F, te), S3, tq);
+    dq = f3d2(S3, cq);
+  }
+  const F3 c1 = f3(mquad_read<0>(cq.a), mquad_read<0>(cq.b), mquad_read<0>(cq.w));
+  const F3 c2 = f3(mquad_read<1>(cq.a), mquad_read<1>(cq.b), mquad_read<1>(cq.w));
+  const F3 c3 = f3(mquad_read<2>(cq.a), mquad_read<2>(cq.b), mquad_read<2>(cq.w));
+  const float d1 = mquad_read<0>(dq), d2 = mquad_read<1>(dq), d3 = mquad_read<2>(dq);
+  if (kk == 3) {
+    // btri_point(mtri(F, t), S3) with the edge terms from the quad
+    const F3 p0 = f3(-F.ha, -F.hb, F.w0);
+    const F3 e0 = t == 0 ? f3(F.ha2, 0.0f, 0.0f) : f3(F.ha2, F.hb2, 0.0f);
+    const F3 e1 = t == 0 ? f3(F.ha2, F.hb2, 0.0f) : f3(0.0f, F.hb2, 0.0f);
+    const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = mfc_ed(F);
+    const float ta = t == 0 ? dA : e_d, tb = t == 0 ? dA : dB, tc = t == 0 ? e_d : dB;
+    const float idet = mfc_idet(F, t);
+    const F3 d = f3sub(S3, p0);
+    const float e0d = f3dot(e0, d), e1d = f3dot(e1, d);
+    const float u = FMA(tc, e0d, -(tb * e1d)) * idet, v = FMA(ta, e1d, -(tb * e0d)) * idet;
+    const bool inside = (0.0f <= u) & (u <= 1.0f) & (0.0f <= v) & (v <= 1.0f) & (u + v <= 1.0f);
+    F3 cp = f3fma(e1, v, f3fma(e0, u, p0));
+    const float d0 = f3d2(cp, S3);
+    const bool k0 = (d0 < d1) & inside;
+    cp = f3sel(k0, cp, c1);
+    float md = k0 ? d0 : d1;
+    cp = f3sel(d2 < md, c2, cp);
+    md = fminf(md, d2);
+    S = S3;
+    P = f3sel(d3 < md, c3, cp);
+    c = bcand(S, P, tt);
+  }
+  return c;
+}
+
 // each lane walks its own items, one face per iteration (mesh_face)
 template <int NB, class G, class SegOf, class Apply>
 POB_D void mesh_lane_walk(G &g, const float *WT, fcptr_t FC, const float cz, const float hz, uint64_t (&M)[NB],
@@ -687,24 +742,20 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(req2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req2, 0u));
     const bool own1 = has && r1 < 8u, own2 = has2 && r2 < 8u;  // (own2 implies own1: n1 < 8)
     const uint64_t pop = (own1 ? 1ull << b1 : 0ull) | (own2 ? 1ull << b2 : 0ull);
+    const int g1 = 8 * (int)r1, g2 = 8 * (int)r2;  // the first lanes of the owner's groups
 #pragma unroll
     for (int q = 0; q < NB; ++q) M[q] = s == q ? (M[q] & ~pop) : M[q];
-    // group owners (wave-uniform): the lane of each of the eight groups
-    int ol = 0;
-    {
-      uint64_t m1 = req1, m2 = req2;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const bool first = q < n1;
-        const uint64_t m = first ? m1 : m2;
-        const int o = m != 0ull ? __builtin_ctzll(m) : 0;
-        ol = grp == q ? o : ol;
-        m1 = first ? (m1 & (m1 - 1ull)) : m1;
-        m2 = first ? m2 : (m2 & (m2 - 1ull));
-      }
-    }
+    // group owners: each owner sends its lane number to its groups' first lanes (forward
+    // permutes; the other lanes write odd lanes, never read), each group reads its first lane
     const bool gv = grp < n1 + n2;
     const bool second = grp >= n1;
+    int ol;
+    {
+      const int p1 = __builtin_amdgcn_ds_permute((own1 ? g1 : (lane | 1)) << 2, lane);
+      const int p2 = __builtin_amdgcn_ds_permute((own2 ? g2 : (lane | 1)) << 2, lane);
+      const int o = __builtin_amdgcn_ds_bpermute((lane & ~7) << 2, second ? p2 : p1);
+      ol = gv ? (o & 63) : 0;
+    }
     v3 A, B;
     float r;
     bool seg;
@@ -722,7 +773,7 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
     const v3 Lb = sego ? mwall_local(W, cz, Bo) : La;
     const MFace F = mface(g, mo & 7, mcap_seg(g, La, Lb), W.hx, W.hy, hz, fcw);
     F3 Sc, Pc;
-    MCand c = mface_cand(g, F, tri, gv ? kk : 7, Sc, Pc);
+    MCand c = mface_cand_quad(g, F, tri, gv ? kk : 7, Sc, Pc);
     c.d2 = mcand_key(c.d2);
     // each triangle's first strict minimum over its quad, and the number of candidates at it
     float dmin = c.d2;
@@ -753,7 +804,6 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
     }
     // the owners take their items' triangles in order: the winners' lanes first (all four
     // fetches in flight), then each contact
-    const int g1 = 8 * (int)r1, g2 = 8 * (int)r2;
     const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 4 + mlane_read_i(kmin, g1 + 4);
     const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 4 + mlane_read_i(kmin, g2 + 4);
     const int nt = __any(own2) ? 4 : 2;
