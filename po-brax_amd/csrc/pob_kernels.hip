@@ -2793,16 +2793,18 @@ static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, c
     default: hipLaunchKernelGGL((k_step_hex<POB_ANT, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
   }
 }
-// Up to one wave per SIMD (B <= the SIMD count x 4 envs: the default batch range of this
-// kernel) the wave's dependency chain is the step time and the guard branches split it
-// (GuardAcc, measured HH B=4 096 -3.5 %); with two or more waves per SIMD (HH and TAG above
-// 16 x CUs, or a POB_HEXA_MAX_B override) the other wave hides them and the accumulator's VALU operations cost (B = 8 192:
-// TAG / GA +1 %), so the branch guards stay.  POB_HEX_GACC=0/1 forces either.
+// Up to one wave per SIMD (B <= the SIMD count x 4 envs) the wave's dependency chain is the
+// step time and the guard branches split it (GuardAcc, measured HH B=4 096 -3.5 %).  With two
+// or more waves per SIMD the spring-model build measured the accumulator's VALU operations as
+// the larger cost (B = 8 192: TAG / GA +1 %); with brax's spelling the accumulator wins there
+// too for HH and TAG (HH B = 8 192 -1.7 %, 12 288 -2.4 %, TAG 8 192 -1 %; profiles/r6p), so
+// HH and TAG take it at every batch, GA and the stock ant up to one wave per SIMD.
+// POB_HEX_GACC=0/1 forces either.
 template <typename QT>
 static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, int B, const StatePtrs &pi,
                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
   const char *f = getenv("POB_HEX_GACC");
-  const bool acc = f ? atoi(f) != 0 : (B + 3) / 4 <= 4 * n_cu;
+  const bool acc = f ? atoi(f) != 0 : (kind == POB_HEAVENHELL || kind == POB_TAG || (B + 3) / 4 <= 4 * n_cu);
   if (acc) launch_step_hex_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
   else launch_step_hex_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
 }
