@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define POB_ABI_VERSION 7
+#define POB_ABI_VERSION 8
 
 enum pob_kind { POB_HEAVENHELL = 0, POB_GATHER = 1, POB_TAG = 2, POB_ANT = 3 };
 
@@ -125,9 +125,18 @@ typedef struct pob_state {
   uint32_t *any_done_clear;
   /* Optional (ABI v7): obs[:, idx] of the env's observation mask (pob_env_set_obs_mask), (B, K)
    * float32, written by pob_step / pob_step_mixed from the same observation rows in the same
-   * launch (po_brax/standard_observability_masks.py:5-67 applied as obs[:, idx]).  The reset
-   * entry points do not write it (pob_obs_gather does). */
+   * launch (po_brax/standard_observability_masks.py:5-67 applied as obs[:, idx]).  Since ABI v8
+   * pob_reset and pob_reset_where_done[_shard] write it too, for the rows they reset. */
   float *obs_masked;
+  /* Optional (ABI v8): per-env scratch bytes (B of them, any contents on entry) for the
+   * four-lane kernel's split launch: its fast launch records in ovf_mark[b] (b = the first env
+   * of each 16-env wave) whether that wave's wall contacts overflowed its store, and the fix-up
+   * launch right after it re-steps exactly the marked waves.  The marks live outside every
+   * output, so no state the caller wrote (first_obs rows copied by AUTORESET, edited info
+   * entries) can be taken for one.  NULL: the one-launch form runs instead (the same results,
+   * slower at large batches).  pob_step / pob_step_mixed read it from `out`; two launches
+   * that may run concurrently must not share it (slices of one buffer are fine). */
+  uint8_t *ovf_mark;
 } pob_state;
 
 typedef struct pob_env pob_env;

@@ -44,6 +44,12 @@ FLAGS = orc.F_EPISODE | orc.F_AUTORESET
 QP = ("pos", "rot", "vel", "ang")
 VARIANTS = ((1, "eps-normal"), (4, "pos-tri"), (8, "form"), (1 | 4, "eps-normal+pos-tri"),
             (13, "all three (brax spelling)"))
+BASE = 0  # the form each variant is measured against (--unpinned: the adopted spelling, 13)
+# the choices nothing pins (round 6, verdict r5 item 4; oracle/pob_oracle.c MV_DIAG ..): each on
+# top of the adopted spelling, measured against it
+UNPINNED = ((13 | 16, "other diagonal (V1-V3)"), (13 | 32, "winding reversed (n inward)"),
+            (13 | 64, "edges as loop p2->p0"), (13 | 128, "world frame"),
+            (13 | 16 | 32 | 64 | 128, "all four"))
 TOL = 1e-5
 
 
@@ -89,8 +95,8 @@ def _ulp(s):
 
 def _study_states(e, s, a, title):
     print(f"  [{title}]")
-    base = _step(e, s, a, 0)
-    print(_line("noise floor (1-ulp pos)", *_moved(_step(e, _ulp(s), a, 0), base)))
+    base = _step(e, s, a, BASE)
+    print(_line("noise floor (1-ulp pos)", *_moved(_step(e, _ulp(s), a, BASE), base)))
     for v, name in VARIANTS:
         print(_line(f"{v:2d} {name}", *_moved(_step(e, s, a, v), base)))
 
@@ -136,7 +142,7 @@ def contact_table(n=20000, seed=11):
         d = rng.normal(size=3)
         d = (d / np.linalg.norm(d) * 0.2828).astype(np.float32)
         a, b, r = c + d, c - d, 0.08
-        L.orc_set_mesh_variant(0)
+        L.orc_set_mesh_variant(BASE)
         c0 = orc.mesh_contacts(wall, a, b, True, r)[:, :5]
         if len(c0) == 0:
             continue
@@ -165,12 +171,18 @@ def main():
     ap.add_argument("--B", type=int, default=1024)
     ap.add_argument("--rollout-variant", type=int, default=None,
                     help="the spelling the rollouts run in (default: the oracle's)")
+    ap.add_argument("--unpinned", action="store_true",
+                    help="the unpinned choices (triangulation, winding, edge loop, frame) against the adopted spelling")
     a = ap.parse_args()
+    global VARIANTS, BASE
+    if a.unpinned:
+        VARIANTS, BASE = UNPINNED, 13
     if a.rollout_variant is not None:
         orc.lib().orc_set_mesh_variant(a.rollout_variant)
     t0 = time.time()
     print(f"# brax capsule_mesh spelling study (oracle/brax_mesh_study.py, B={a.B}; {orc.cpu_model()})")
-    print(f"# one env-step from the same state, variant vs the exact form; 'beyond 1e-5': any qp component of the "
+    print(f"# one env-step from the same state, variant vs {'the adopted spelling (13)' if BASE else 'the exact form'}; "
+          f"'beyond 1e-5': any qp component of the "
           f"9 ant bodies with |a - b| > 1e-5 max(1, |b|)")
     contact_table()
     for name in ("ant_heavenhell", "ant_tag", "ant_gather"):

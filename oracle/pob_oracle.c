@@ -965,8 +965,67 @@ static void bface(float ha, float hb, float w0, float sg, const bseg_t *A, cand_
   }
 }
 
+/* ---- the choices of the brax spelling that nothing pins (round 6; DESIGN.md §3, "unpinned
+ * choices").  brax v1's TriangulatedBox vertex order and face triangulation are not
+ * recoverable without brax, and the restatement evaluates in the wall's own frame where brax
+ * evaluates in the world frame.  Each choice is a variant bit on top of the adopted spelling
+ * (MV_BRAX), measured by oracle/brax_mesh_study.py --unpinned:
+ *   MV_DIAG    the face's other diagonal (V1 - V3): t0 = (V1, V2, V3), t1 = (V1, V3, V0)
+ *   MV_NFLIP   the winding reversed: each triangle's vertices in the opposite order, so
+ *              brax's face normal (the segment-plane candidate's n, which enters through
+ *              n.(b - a) + 1e-6) points into the box
+ *   MV_EDGE    _closest_segment_triangle_points' segment-segment edges as the loop p0 p1,
+ *              p1 p2, p2 p0 (the restatement: p0 p1, p1 p2, p0 p2 -- the diagonal then shared
+ *              by the face's two triangles)
+ *   MV_WORLD   the world frame: the face's vertices and its normal rotated by the wall's z
+ *              rotation and translated by its centre, the capsule's segment from its world end
+ *              points, the generic 3-D forms throughout, the normal (S - P) / (1e-6 + |S - P|)
+ *              in world coordinates
+ *   MV_GENERIC the variant path with none of the above (bit-identical to bface: a self-check)
+ * The default stays MV_BRAX (the kernels' spelling). */
+#define MV_DIAG 16
+#define MV_NFLIP 32
+#define MV_EDGE 64
+#define MV_WORLD 128
+#define MV_GENERIC 256
+#define MV_VARPATH (MV_DIAG | MV_NFLIP | MV_EDGE | MV_WORLD | MV_GENERIC)
+
+/* both triangles of a face given by its corners V[0..3] (V0 V1 V2 V3 of bface, in the frame of
+ * evaluation) and its outward normal n (same frame) against the capsule segment A */
+static void bface_var(const f3 V[4], f3 nout, int mv, const bseg_t *A, cand_t c[2]) {
+  static const int TRI[2][2][3] = {{{0, 1, 2}, {0, 2, 3}}, {{1, 2, 3}, {1, 3, 0}}};
+  const f3 n = (mv & MV_NFLIP) ? F3(-nout.a, -nout.b, -nout.w) : nout;
+  for (int t = 0; t < 2; ++t) {
+    const int *id = TRI[(mv & MV_DIAG) ? 1 : 0][t];
+    const f3 p0 = V[id[0]], p1 = V[(mv & MV_NFLIP) ? id[2] : id[1]], p2 = V[(mv & MV_NFLIP) ? id[1] : id[2]];
+    /* _closest_segment_point_plane(a, b, p0, n): t = (p0.n - n.a) / (n.(b - a) + 1e-6), clipped */
+    FL(1 + 1 + 1);
+    const float tt = bclamp01((f3dot(p0, n) - f3dot(n, A->p0)) * (1.0f / (f3dot(n, A->d) + 1e-6f)));
+    f3 sp[4], tp[4];
+    float u[4], d2[4];
+    const bseg_t Ea = bseg_make(p0, f3sub(p1, p0)), Eb = bseg_make(p1, f3sub(p2, p1));
+    const bseg_t Ec = (mv & MV_EDGE) ? bseg_make(p2, f3sub(p0, p2)) : bseg_make(p0, f3sub(p2, p0));
+    d2[0] = bseg_seg(A, &Ea, &sp[0], &tp[0], &u[0]);
+    d2[1] = bseg_seg(A, &Eb, &sp[1], &tp[1], &u[1]);
+    d2[2] = bseg_seg(A, &Ec, &sp[2], &tp[2], &u[2]);
+    const btri_t T = btri_make(p0, p1, p2);
+    sp[3] = f3fma(A->d, tt, A->p0);
+    u[3] = tt;
+    tp[3] = btri_point(&T, sp[3]);
+    d2[3] = bdist2(sp[3], tp[3]);
+    c[t] = bpick(sp, tp, u, d2);
+  }
+}
+
 /* component k of the wall-local vector (x, y, z) */
 static inline float comp(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+/* wall-local (x, y, z) -> world: R_z(theta) l + c (the inverse of capsule_wall_mesh's map) */
+static inline v3 wall_to_world(const orc_env *e, int w, v3 l, int point) {
+  const float c = e->wall_cos[w], s = e->wall_sin[w];
+  v3 r = V(fmaf(-l.y, s, l.x * c), fmaf(l.y, c, l.x * s), l.z);
+  if (point) r = vadd(r, e->wall_c[w]);
+  return r;
+}
 
 /* the mesh contacts of capsule i (world end points pa, pb; pb unused for the torso) against
  * wall w, appended to ct */
@@ -985,6 +1044,12 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
   /* brax form: the capsule's segment quantities once per wall, in the wall frame (x, y, z) */
   bseg_t capw;
   if (mv & MV_FORM) capw = bseg_make(F3(La.x, La.y, La.z), f3sub(F3(Lb.x, Lb.y, Lb.z), F3(La.x, La.y, La.z)));
+  /* (MV_WORLD: the segment from the world end points) */
+  bseg_t capworld;
+  if (mv & MV_WORLD) {
+    const v3 wb = seg ? pb : pa;
+    capworld = bseg_make(F3(pa.x, pa.y, pa.z), f3sub(F3(wb.x, wb.y, wb.z), F3(pa.x, pa.y, pa.z)));
+  }
   CST(0, 1);
   int n_hit = 0;
   for (int f = 0; f < 6; ++f) {
@@ -1007,7 +1072,28 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
     }
     CST(1, 1);
     cand_t cds[2];
-    if (mv & MV_FORM) {
+    if ((mv & MV_FORM) && (mv & MV_VARPATH)) {
+      /* the unpinned choices (variant path): the face's corners in face coordinates, or in
+       * the world frame */
+      f3 Vc[4] = {F3(-ha, -hb, w0), F3(ha, -hb, w0), F3(ha, hb, w0), F3(-ha, hb, w0)};
+      f3 nrm = F3(0.0f, 0.0f, sg);
+      if (mv & MV_WORLD) {
+        for (int q = 0; q < 4; ++q) {
+          float l[3];
+          l[ka] = Vc[q].a; l[kb] = Vc[q].b; l[k] = Vc[q].w;
+          const v3 wv = wall_to_world(e, w, V(l[0], l[1], l[2]), 1);
+          Vc[q] = F3(wv.x, wv.y, wv.z);
+        }
+        float l[3] = {0.0f, 0.0f, 0.0f};
+        l[k] = sg;
+        const v3 wn = wall_to_world(e, w, V(l[0], l[1], l[2]), 0);
+        nrm = F3(wn.x, wn.y, wn.z);
+        bface_var(Vc, nrm, mv, &capworld, cds);
+      } else {
+        const bseg_t capf = bseg_perm(&capw, k);
+        bface_var(Vc, nrm, mv, &capf, cds);
+      }
+    } else if (mv & MV_FORM) {
       const bseg_t capf = bseg_perm(&capw, k);
       bface(ha, hb, w0, sg, &capf, cds);
     } else {
@@ -1037,13 +1123,14 @@ static void capsule_wall_mesh(const orc_env *e, int i, int w, v3 pa, v3 pb, cont
         if (!(cd.d2 > 0.0f)) CST(6, 1);
       } else if (cd.d2 > 0.0f) { FL(4); cdist = dist; const float inv = 1.0f / dist; nf.a = cd.d.a * inv; nf.b = cd.d.b * inv; nf.w = cd.d.w * inv; }
       else { cdist = 0.0f; nf.a = 0.0f; nf.b = 0.0f; nf.w = sg; CST(6, 1); }
-      /* back to wall-local (x, y, z), then to the world */
+      /* back to wall-local (x, y, z), then to the world (MV_WORLD: world already) */
       float nl[3]; nl[ka] = nf.a; nl[kb] = nf.b; nl[k] = nf.w;
       FL(6 + 1);
       const int m = ct->count++;
       ct->body[m] = i; ct->ground[m] = 0; ct->pen[m] = pen; ct->r[m] = (mv & MV_POS_TRI) ? cdist : r;
       ct->tau[m] = 1.0f - 2.0f * cd.u;
-      ct->n[m] = V(fmaf(-nl[1], s, nl[0] * c), fmaf(nl[1], c, nl[0] * s), nl[2]);
+      if ((mv & MV_WORLD) && (mv & MV_FORM)) ct->n[m] = V(nf.a, nf.b, nf.w);
+      else ct->n[m] = V(fmaf(-nl[1], s, nl[0] * c), fmaf(nl[1], c, nl[0] * s), nl[2]);
       ct->e[m] = V(0.0f, 0.0f, 0.0f);
       ++n_hit;
       if (g_cst_on) {

@@ -55,12 +55,17 @@ struct pob_env {
 
 #define POB_MIXED (-1)  // KIND of the mixed-launch body: the kind is read from the table
 #define POB_F_STAGED (1u << 16)  // internal step flag: coalesced LDS-staged state loads
+// (test hook: POB_QUAD_FORCE_FIXUP=1 makes the fast launch hand every wave to the fix-up launch,
+// so the parity tests run the fix-up path on every env; an internal flags bit)
+#define POB_F_INT_FORCE_FIXUP (1u << 30)
+#define POB_F_INTERNAL (POB_F_STAGED | POB_F_INT_FORCE_FIXUP)
+#define POB_F_PUBLIC (POB_F_EPISODE | POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)
 
 // ---------------------------------------------------------------------------- state
 #define POB_STATE_FIELDS(X)                                                                    \
   X(pos) X(rot) X(vel) X(ang) X(obs) X(reward) X(done) X(steps) X(truncation) X(m0) X(m1) X(m2) \
   X(rng) X(first_pos) X(first_rot) X(first_vel) X(first_ang) X(first_obs) X(any_done) X(done_u8) X(trunc_i32) \
-  X(m0_i32) X(m1_i32) X(any_done_clear) X(obs_masked)
+  X(m0_i32) X(m1_i32) X(any_done_clear) X(obs_masked) X(ovf_mark)
 
 struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   float *pos, *rot, *vel, *ang, *obs, *reward, *done, *steps, *truncation, *m0, *m1, *m2;
@@ -71,6 +76,7 @@ struct StatePtrs {  // device pointers (kernel-argument copy of pob_state)
   int32_t *trunc_i32, *m0_i32, *m1_i32;
   uint32_t *any_done_clear;  // pob_reset_where_done zeroes it (optional)
   float *obs_masked;         // obs[:, mask] (optional, ABI v7)
+  uint8_t *ovf_mark;         // the split launch's per-wave overflow marks (optional, ABI v8)
 };
 // obs[:, mask] of a pass's staged observation rows (rows x D floats in LDS at stg), stored
 // next to the obs rows: each row's K columns by the wave's lanes (pob_env_set_obs_mask)
@@ -743,17 +749,17 @@ __device__ __forceinline__ void quad_store_dyn(const StatePtrs &in, const StateP
 }
 
 // Wall-contact overflow handling of the four-lane kernel (MODE): 0 = in the kernel (the position
-// and velocity passes re-walk an overflowing lane's faces); 1 = the fast launch: a wave with an
-// overflowing lane stores nothing but POB_OVF_MARK in its first env's first obs element and
-// exits; 2 = the fix-up launch right after it: only the marked waves run, the whole step with
-// the re-walks.  The re-walk code's mere presence in the substep loop cost 15 % (HH) through
-// register pressure (profiles/r6a_ab.txt); split, the common launch carries none of it.  The
-// mark lives in the state's own obs buffer (obs is an output only: no kernel reads it), so
-// concurrent launches on disjoint state slices (GraphRollout groups) do not interfere.
-#define POB_OVF_MARK 0x7FA5A5A5u  // a signalling NaN with a payload: no arithmetic produces it
-// (test hook: POB_QUAD_FORCE_FIXUP=1 makes the fast launch hand every wave to the fix-up launch,
-// so the parity tests run the fix-up path on every env; an internal flags bit)
-#define POB_F_INT_FORCE_FIXUP (1u << 30)
+// and velocity passes re-walk an overflowing lane's faces); 1 = the fast launch: every wave
+// records in ovf_mark[its first env] whether one of its lanes overflowed the contact store (its
+// first store clears the mark: AntGather's no-wall pass never reaches the overflow test), and a
+// wave that overflowed stores nothing else and exits; 2 = the fix-up launch right after it: only
+// the marked waves run, the whole step with the re-walks.  The re-walk code's mere presence in
+// the substep loop cost 15 % (HH) through register pressure (profiles/r6a_ab.txt); split, the
+// common launch carries none of it.  The marks are a caller-provided scratch array (pob_state
+// ovf_mark, ABI v8) outside every output -- round 5's in-band mark (a signalling NaN in the
+// wave's first obs element) could be forged by a first_obs row that AUTORESET copies -- and
+// every wave of the fast launch writes its mark, so the array needs no initialisation; slices
+// of it serve concurrent launches on disjoint state slices (GraphRollout groups).
 template <int KIND, typename QT, bool LEG = false, int MODE = 0>
 POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const float *__restrict__ act,
                           const StatePtrs &out, const uint32_t flags, const int L, const int gt, float *lds,
@@ -775,7 +781,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   // the wave's 16 envs are consecutive rows of every state array
   int b_first = (gt - lane) >> 2;
   if (b_first >= B) return;  // (wave-uniform: a block's waves past the batch; no barrier follows)
-  if (MODE == 2 && __float_as_uint(out.obs[(size_t)b_first * D]) != POB_OVF_MARK) return;  // (not marked)
+  if (MODE == 2 && out.ovf_mark[b_first] == 0) return;  // (not marked)
+  if (MODE == 1 && lane == 0) out.ovf_mark[b_first] = 0;  // (every wave: the passes that finish leave it)
   int nenv = B - b_first < 16 ? B - b_first : 16;
   int le = b - b_first;
   // The physics runs on all 64 lanes (the wave walk's DPP / bpermute rounds need every lane):
@@ -979,7 +986,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         if (__any(ovf)) break;
       }
       if (__any(ovf) || (flags & POB_F_INT_FORCE_FIXUP)) {
-        if (lane == 0) out.obs[(size_t)b_first * D] = __uint_as_float(POB_OVF_MARK);
+        if (lane == 0) out.ovf_mark[b_first] = 1;
         return;
       }
       break;
@@ -1217,11 +1224,11 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 
 // MODE 2 (the fix-up launch): does any wave of the block carry the overflow mark?  (before
 // the block's table staging: a block without one exits at once)
-POB_D bool quad_block_marked(const int B, const int D, const float *obs, const int bt0) {
+POB_D bool quad_block_marked(const int B, const uint8_t *mark, const int bt0) {
   bool any = false;
   for (int w = 0; w < (int)blockDim.x / 64; ++w) {
     const int bf = (bt0 + 64 * w) >> 2;
-    if (bf < B) any = any | (__float_as_uint(obs[(size_t)bf * D]) == POB_OVF_MARK);
+    if (bf < B) any = any | (mark[bf] != 0);
   }
   return any;
 }
@@ -1233,7 +1240,7 @@ __global__ __launch_bounds__(256, POB_QUAD_MIN_WAVES) void k_step_quad(const voi
                                                                        const int L) {
   __shared__ float lds[QL_FLOATS * 256];
   __shared__ __attribute__((aligned(16))) float legtab[POB_TAB_FLOATS];
-  if (MODE == 2 && !quad_block_marked(B, obs_dim<KIND>(*(csys_t *)(size_t)sysp), out.obs, (int)(blockIdx.x * blockDim.x)))
+  if (MODE == 2 && !quad_block_marked(B, out.ovf_mark, (int)(blockIdx.x * blockDim.x)))
     return;
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<KIND, QT, false, MODE>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
@@ -1321,7 +1328,7 @@ __global__ __launch_bounds__(256, POB_MIXED_MIN_WAVES) void k_step_mixed(const M
   const float *act = POB_PICK(act);
   const int B = POB_PICK(B), blk0 = POB_PICK(blk0);
 #undef POB_PICK
-  if (MODE == 2 && !quad_block_marked(B, obs_dim<POB_MIXED>(*(csys_t *)(size_t)sysp), out.obs, (bx - blk0) * 256))
+  if (MODE == 2 && !quad_block_marked(B, out.ovf_mark, (bx - blk0) * 256))
     return;
   stage_leg_table((csys_t *)(size_t)sysp, legtab);
   step_quad_body<POB_MIXED, QT, false, MODE>((csys_t *)(size_t)sysp, B, in, act, out, flags, L,
@@ -2636,6 +2643,22 @@ __global__ __launch_bounds__(BS) void k_reset(const void *sysp, const int B, con
   POB_TS(3);
   POB_TS(8);  // (marks the row as a reset wave's: the step kernels do not set stamp 8)
   POB_TS_WRITE();
+  if (s.obs_masked) {
+    // obs[:, mask] of the rows this launch resets (ABI v8; the step kernels fuse the same
+    // gather): from the staged rows still in LDS, or -- rows written straight from registers --
+    // read back from memory after this wave's stores (workgroup scope: the same CU's L1)
+    const bool direct = std::is_same<QT, float>::value && few;
+    if (direct) __threadfence_block();
+    const int K = S.obs_mask_n;
+    for (uint32_t m = rows; m != 0u; m &= m - 1u) {
+      const int e = __builtin_ctz(m);
+      const size_t rb = (size_t)(e0 + e);
+      for (int c = lane; c < K; c += 64) {
+        const int col = S.obs_mask[c];
+        s.obs_masked[rb * K + c] = direct ? s.obs[rb * D + col] : stg[e * WP + col];
+      }
+    }
+  }
   if (!active || k != 0) return;
   if (mode == RESET_FULL) {
     s.rng[2 * b] = R.rng0; s.rng[2 * b + 1] = R.rng1;
@@ -2865,8 +2888,9 @@ static void launch_step_quad(int kind, bool legacy, int n_cu, hipStream_t st, co
     hipLaunchKernelGGL((k_step_quad_ga3<QT>), g, b, 0, st, sp, B, pi, act, po, flags, L);
     return;
   }
-  // walls: the fast launch, then the fix-up launch of its overflowing waves (MODE 1 / 2 above)
-  const bool split = quad_split_launch(kind);
+  // walls: the fast launch, then the fix-up launch of its overflowing waves (MODE 1 / 2 above;
+  // without the caller's mark array the one-launch form)
+  const bool split = quad_split_launch(kind) && po.ovf_mark != nullptr;
   flags |= split ? quad_force_fixup() : 0u;
   switch (kind) {
     case POB_HEAVENHELL:
@@ -3004,6 +3028,7 @@ int pob_reset(pob_env *e, int B, const uint32_t *keys, const pob_state *out, voi
   if (int rc = check_state(out, true)) return rc;
   if (out->first_pos && (!out->first_rot || !out->first_vel || !out->first_ang || !out->first_obs))
     return fail(POB_EINVAL, "state: first_* pointers must be all set or all NULL");
+  if (out->obs_masked && e->sys.obs_mask_n == 0) return fail(POB_EINVAL, "obs_masked given but the env has no observation mask");
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs p = to_ptrs(*out);
   if (e->sys.qp_f16)
@@ -3033,6 +3058,7 @@ static int check_step(const pob_env *e, int B, const pob_state *in, const float 
   if (!act) return fail(POB_EINVAL, "action is NULL");
   if (int rc = check_state(in, true)) return rc;
   if (int rc = check_state(out, true)) return rc;
+  if (flags & ~(uint32_t)POB_F_PUBLIC) return fail(POB_EINVAL, "unknown step flag bits");
   if ((flags & POB_F_EPISODE) && episode_length <= 0) return fail(POB_EINVAL, "episode_length must be positive");
   if ((flags & POB_F_AUTORESET) &&
       (!in->first_pos || !in->first_rot || !in->first_vel || !in->first_ang || !in->first_obs ||
@@ -3046,7 +3072,7 @@ static int check_step(const pob_env *e, int B, const pob_state *in, const float 
 int pob_step(pob_env *e, int B, const pob_state *in, const float *act, const pob_state *out, uint32_t flags,
              int episode_length, void *stream) {
   if (int rc = check_step(e, B, in, act, out, flags, episode_length)) return rc;
-  flags &= ~POB_F_STAGED;
+  flags &= ~POB_F_INTERNAL;
   if (can_stage(e, in)) flags |= POB_F_STAGED;
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs pi = to_ptrs(*in), po = to_ptrs(*out);
@@ -3071,8 +3097,8 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   MixArgs A;
   memset(&A, 0, sizeof(A));
   A.n = n;
-  flags &= ~POB_F_STAGED;
-  bool stage = true;
+  flags &= ~POB_F_INTERNAL;
+  bool stage = true, marks = true;
   long long blk = 0;
   for (int k = 0; k < n; ++k) {
     const pob_env *e = envs[k];
@@ -3081,6 +3107,7 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
     if (e->sys.legacy) return fail(POB_EINVAL, "mixed step: legacy-spring envs step through pob_step");
     if (e->device != envs[0]->device) return fail(POB_EINVAL, "mixed step: envs must live on one device");
     stage = stage && can_stage(e, &in[k]);
+    marks = marks && out[k].ovf_mark != nullptr;
     MixSeg &s = A.s[k];
     s.sysp = e->d_sys; s.act = act[k]; s.in = to_ptrs(in[k]); s.out = to_ptrs(out[k]);
     s.B = B[k]; s.blk0 = (int)blk;
@@ -3091,7 +3118,7 @@ int pob_step_mixed(int n, pob_env *const *envs, const int *B, const pob_state *i
   if (stage) flags |= POB_F_STAGED;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g((unsigned)blk);
-  if (quad_split_launch(POB_MIXED)) {  // the fast launch, then the fix-up launch of its overflowing waves
+  if (quad_split_launch(POB_MIXED) && marks) {  // the fast launch, then the fix-up launch of its overflowing waves
     flags |= quad_force_fixup();
     if (envs[0]->sys.qp_f16) {
       hipLaunchKernelGGL((k_step_mixed<__half, 1>), g, dim3(256), 0, st, A, flags, episode_length);
@@ -3127,6 +3154,7 @@ int pob_reset_where_done_shard(pob_env *e, int B, int total, int first, int mode
     return fail(POB_EINVAL, "gym_key_in and gym_key_out must not overlap");
   if (s->any_done_clear && s->any_done_clear == s->any_done)
     return fail(POB_EINVAL, "any_done_clear must not alias any_done");
+  if (s->obs_masked && e->sys.obs_mask_n == 0) return fail(POB_EINVAL, "obs_masked given but the env has no observation mask");
   hipStream_t st = (hipStream_t)stream;
   const StatePtrs p = to_ptrs(*s);
   const uint32_t *flag = s->any_done;

@@ -22,7 +22,7 @@ RESET_GYM, RESET_OWN = 0, 1
 KINDS = {"ant_heavenhell": 0, "ant_gather": 1, "ant_tag": 2, "ant": 3}
 QP_F32, QP_F16 = 0, 1
 MIX_MAX = 4
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class pob_params(C.Structure):
@@ -48,7 +48,8 @@ class pob_state(C.Structure):
     _fields_ = [(n, _VP) for n in (
         "pos", "rot", "vel", "ang", "obs", "reward", "done", "steps", "truncation",
         "m0", "m1", "m2", "rng", "first_pos", "first_rot", "first_vel", "first_ang",
-        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32", "any_done_clear", "obs_masked")]
+        "first_obs", "any_done", "done_u8", "trunc_i32", "m0_i32", "m1_i32", "any_done_clear", "obs_masked",
+        "ovf_mark")]
 
 
 # Every symbol include/pob.h declares (checked by tests/test_lib_symbols.py).

@@ -243,6 +243,10 @@ class PoBraxEnv(Env):
             m = np.asarray(m).ravel()
             if m.dtype.kind not in "iu":
                 raise TypeError("obs_mask must hold integer column indices")
+            # range-checked on the caller's own values (a wide index must not wrap into range
+            # through the int32 cast); the exact bound 0 <= idx < D follows in _create
+            if m.size and (int(m.min()) < 0 or int(m.max()) >= 2 ** 31):
+                raise ValueError("obs_mask index out of range")
             self._obs_mask = np.ascontiguousarray(m.astype(np.int32))
         self._create()
         self.sys = System(self._owner, self._body_names())
@@ -263,7 +267,6 @@ class PoBraxEnv(Env):
             if m.size and (m.min() < 0 or m.max() >= self._D):
                 raise ValueError(f"obs_mask index out of range for observation size {self._D}")
             check(lib.pob_env_set_obs_mask(self._handle, m.ctypes.data_as(C.POINTER(C.c_int32)), int(m.size)))
-            self._obs_mask_dev = torch.from_numpy(m).to(self.device)
 
     @property
     def obs_mask(self):
@@ -273,14 +276,6 @@ class PoBraxEnv(Env):
     @property
     def masked_observation_size(self) -> int:
         return 0 if self._obs_mask is None else int(self._obs_mask.size)
-
-    def _gather_masked(self, b: dict) -> None:
-        """obs_masked from obs by the column gather kernel (the reset entry points do not fuse it)."""
-        B = b["obs"].shape[0]
-        K = int(self._obs_mask.size)
-        if B and K:
-            check(lib.pob_obs_gather(b["obs"].data_ptr(), B, self._D, self._obs_mask_dev.data_ptr(), K,
-                                     b["obs_masked"].data_ptr(), _lib.stream_handle(self.device)))
 
     @property
     def _handle(self) -> C.c_void_p:
@@ -304,7 +299,8 @@ class PoBraxEnv(Env):
                  obs=torch.empty((B, D), **f), reward=torch.empty((B,), **f),
                  done=torch.empty((B,), **f), m0=torch.empty((B,), **f), m1=torch.empty((B,), **f),
                  m2=torch.empty((B,), **f),
-                 rng=torch.empty((B, 2), dtype=torch.uint32, device=self.device))
+                 rng=torch.empty((B, 2), dtype=torch.uint32, device=self.device),
+                 ovf_mark=torch.empty((B,), dtype=torch.uint8, device=self.device))
         if episode:
             b["steps"] = torch.empty((B,), **f)
             b["truncation"] = torch.empty((B,), **f)
@@ -356,7 +352,7 @@ class PoBraxEnv(Env):
             fq = state.info["first_qp"]
             b.update(first_pos=fq.pos, first_rot=fq.rot, first_vel=fq.vel, first_ang=fq.ang,
                      first_obs=state.info["first_obs"])
-        for k in ("any_done", "any_done_clear"):
+        for k in ("any_done", "any_done_clear", "ovf_mark"):
             if k in a:
                 b[k] = a[k]
         if "obs_masked" in state.info:
@@ -398,6 +394,8 @@ class PoBraxEnv(Env):
             done = b["done_u8"].view(torch.bool)
         info = {"rng": b["rng"]} if self.info_rng else {}
         aux = {"done": b["done"], "rng": b["rng"]}
+        if b.get("ovf_mark") is not None:  # the split launch's scratch marks (pob_state.ovf_mark)
+            aux["ovf_mark"] = b["ovf_mark"]
         for k in _TYPED:
             if b.get(k) is not None:
                 aux[k] = b[k]
@@ -448,8 +446,6 @@ class PoBraxEnv(Env):
         b = self._empty(B, episode, first)
         cs = self._cstate(b)
         pob.reset(self._handle.value, B, keys.data_ptr(), C.addressof(cs), _lib.stream_handle(self.device))
-        if "obs_masked" in b:
-            self._gather_masked(b)
         return self._state_of(b, False, squeeze)
 
     @staticmethod
@@ -463,7 +459,8 @@ class PoBraxEnv(Env):
         ``info.update(steps=...)``, wrappers.py:105-111) takes the full path."""
         qp, a = state.qp, state.aux
         refs = [qp.pos, qp.rot, qp.vel, qp.ang, state.obs, state.reward, state.done,
-                a.get("any_done"), a.get("any_done_clear"), flags, episode_length, len(state.metrics)]
+                a.get("any_done"), a.get("any_done_clear"), a.get("ovf_mark"), flags, episode_length,
+                len(state.metrics)]
         refs.extend(state.metrics.values())
         for v in state.info.values():
             if isinstance(v, QP):
@@ -515,6 +512,8 @@ class PoBraxEnv(Env):
             for k in ("m0", "m1", "m2"):
                 if bout.get(k) is None:
                     bout[k] = torch.empty((B,), dtype=torch.float32, device=self.device)
+            if bout.get("ovf_mark") is None or bout["ovf_mark"].shape[0] != B:
+                bout["ovf_mark"] = torch.empty((B,), dtype=torch.uint8, device=self.device)
         else:
             bout = self._empty(B, "steps" in bin_, False)
             if "first_pos" in bin_:  # immutable: shared, not copied
@@ -548,8 +547,7 @@ class PoBraxEnv(Env):
         pob.reset_where_done_shard(self._handle.value, B, int(total) if total else B, int(first), mode,
                                    _lib.ptr(gym_in) or 0, _lib.ptr(gym_out) or 0, C.addressof(cs),
                                    _lib.stream_handle(self.device))
-        if "obs_masked" in b:  # the reset rows' masked columns (the step fuses them; this path does not)
-            self._gather_masked(b)
+        # (the reset rows' masked columns: written by the same launch, ABI v8)
 
 
 # set by envs.mixed.MixedEnv.step: PoBraxEnv._step_impl records its launch here

@@ -32,9 +32,10 @@ def _wall(c, deg, h):
     return np.array([c[0], c[1], 0.5, np.cos(a), np.sin(a), h[0], h[1], 0.5], np.float32)
 
 
-def _triangles(w):
+def _triangles(w, diag=False):
     """the box's 12 triangles in world coordinates: faces -x, +x, -y, +y, -z, +z, each split
-    along its (-a, -b) -> (+a, +b) diagonal (the restatement's face order and split)"""
+    along its (-a, -b) -> (+a, +b) diagonal (the restatement's face order and split; diag: the
+    other diagonal, (+a, -b) -> (-a, +b), as the oracle's MV_DIAG variant)"""
     c = w[:3].astype(np.float64)
     ca, sa = float(w[3]), float(w[4])
     h = w[5:8].astype(np.float64)
@@ -50,7 +51,7 @@ def _triangles(w):
                 p[kb] = ub * h[kb]
                 return c + R @ p
             v0, v1, v2, v3 = vert(-1, -1), vert(1, -1), vert(1, 1), vert(-1, 1)
-            tris += [(v0, v1, v2), (v0, v2, v3)]
+            tris += [(v1, v2, v3), (v1, v3, v0)] if diag else [(v0, v1, v2), (v0, v2, v3)]
     return tris
 
 
@@ -86,12 +87,12 @@ def _closest_on_triangle(p, a, b, c):
     return out
 
 
-def _reference(w, pa, pb, seg, r, n_samples=4001):
+def _reference(w, pa, pb, seg, r, n_samples=4001, diag=False):
     """per triangle: (distance, segment parameter u, segment point, triangle point)"""
     u = np.linspace(0.0, 1.0, n_samples) if seg else np.zeros(1)
     P = pa[None, :] + u[:, None] * ((pb - pa) if seg else 0.0)
     res = []
-    for tri in _triangles(w):
+    for tri in _triangles(w, diag):
         q = _closest_on_triangle(P, *tri)
         d = np.linalg.norm(P - q, axis=1)
         i = int(np.argmin(d))
@@ -134,6 +135,56 @@ def test_default_spelling_is_brax():
 
 @pytest.mark.parametrize("wi", range(len(WALLS)))
 def test_mesh_contacts_match_brute_force_geometry(wi, spelling):
+    _brute_force_case(wi, spelling)
+
+
+# the choices of brax's spelling that nothing in the reference pins (verdict r5 item 4; oracle
+# MV_DIAG / MV_NFLIP / MV_EDGE / MV_WORLD on top of the adopted spelling): each is a valid
+# spelling of the same geometry (this brute-force check), and their effect on a step is
+# measured against the noise floor by oracle/brax_mesh_study.py --unpinned
+UNPINNED = {"diag": BRAX | 16, "winding": BRAX | 32, "edge-loop": BRAX | 64, "world": BRAX | 128,
+            "all": BRAX | 16 | 32 | 64 | 128}
+
+
+@pytest.mark.parametrize("wi", [0, 1, 4, 5])
+@pytest.mark.parametrize("variant", list(UNPINNED), ids=list(UNPINNED))
+def test_unpinned_variants_match_brute_force_geometry(wi, variant):
+    L = orc.lib()
+    prev = L.orc_get_mesh_variant()
+    L.orc_set_mesh_variant(UNPINNED[variant])
+    try:
+        _brute_force_case(wi, BRAX, diag=bool(UNPINNED[variant] & 16))
+    finally:
+        L.orc_set_mesh_variant(prev)
+
+
+def test_unpinned_variant_hooks():
+    """The variant path with no choice changed (MV_GENERIC, 256) is bit-identical to the adopted
+    spelling on HH rollouts, and every unpinned choice changes some HH spawn step (the hooks
+    have teeth)."""
+    import pob_np as P
+    L = orc.lib()
+    prev = L.orc_get_mesh_variant()
+    k = P.split(P.prngkey(12), 129)[1:]
+    a = np.random.default_rng(4).uniform(-1, 1, (12, 128, 8)).astype(np.float32)
+    outs = {}
+    try:
+        for v in (BRAX, BRAX | 256, *UNPINNED.values()):
+            L.orc_set_mesh_variant(v)
+            e = orc.OracleEnv("ant_heavenhell")
+            s = e.reset(k, first=True, nthreads=8)
+            for t in range(len(a)):
+                e.step(s, a[t], flags=orc.F_EPISODE | orc.F_AUTORESET, episode_length=1000, nthreads=8, inplace=True)
+            outs[v] = s
+    finally:
+        L.orc_set_mesh_variant(prev)
+    for f in ("pos", "rot", "vel", "ang", "obs"):
+        assert np.array_equal(outs[BRAX][f].view(np.uint32), outs[BRAX | 256][f].view(np.uint32)), f
+    for name, v in UNPINNED.items():
+        assert not np.array_equal(outs[BRAX]["pos"], outs[v]["pos"]), name
+
+
+def _brute_force_case(wi, spelling, diag=False):
     rng = np.random.default_rng(100 + wi)
     w = _wall(*WALLS[wi])
     checked = 0
@@ -141,7 +192,7 @@ def test_mesh_contacts_match_brute_force_geometry(wi, spelling):
         pa, pb, seg, r = _case(rng, w)
         pa32, pb32 = pa.astype(np.float32), pb.astype(np.float32)
         got = orc.mesh_contacts(w, pa32, pb32, seg, r)
-        ref = _reference(w, pa32.astype(np.float64), pb32.astype(np.float64), seg, r)
+        ref = _reference(w, pa32.astype(np.float64), pb32.astype(np.float64), seg, r, diag=diag)
         step = (np.linalg.norm(pb - pa) / 4000.0) if seg else 0.0
         # brax's regularised forms move a distance by up to ~1e-4 where the segment is nearly
         # parallel to an edge (the line solution's (denom + 1e-6), denom = sin^2 of the angle)

@@ -414,3 +414,51 @@ def test_fixup_launch_mixed_forced(monkeypatch):
         for a, b in zip(outs[0], o):
             for x, y in zip(a, b):
                 assert torch.equal(x, y)
+
+
+def test_split_launch_marks_are_out_of_band():
+    """round 5 marked a wave for the fix-up launch with a signalling NaN in its first
+    obs element, so an AUTORESET copy of a first_obs row holding that bit pattern would have sent
+    an already stepped wave (in-place step) through the fix-up launch a second time.  The marks
+    live in pob_state.ovf_mark now (ABI v8): the same pattern planted in the first first_obs row
+    of every 16-env wave changes nothing -- per-step parity against the oracle through the
+    autoresets that copy it into obs."""
+    name, B, L = "ant_heavenhell", 16400, 2  # B > 16 384: the four-lane kernel's split launch
+    env = _envs().create(name, batch_size=B, episode_length=L)
+    keys = _keys(B, 31)
+    s = env.reset(torch.from_numpy(keys).cuda())
+    s.info["first_obs"].view(torch.int32)[::16, 0] = 0x7FA5A5A5
+    o = orc.OracleEnv(name)
+    planted = 0
+    for t, act in enumerate(_actions(32, B, 4)):
+        so = o.step(_state_np(s), act, flags=FLAGS, episode_length=L, nthreads=NT)
+        s = env.step_(s, torch.from_numpy(act).cuda())
+        compare_states(s, so, f"{name} B={B} step {t}")
+        planted += int((s.obs.view(torch.int32)[::16, 0] == 0x7FA5A5A5).sum())
+    assert planted >= 2 * (B // 16)  # steps 1 and 3 autoreset every env: the pattern is in obs
+
+
+def test_step_without_mark_array_takes_one_launch():
+    """A C caller that leaves pob_state.ovf_mark NULL gets the one-launch form of the four-lane
+    kernel: the same bits as the split launch the engine's own states take."""
+    import ctypes as C
+    from po_brax_amd import _lib
+    name, B, L = "ant_heavenhell", 16400, 3
+    env = _envs().create(name, batch_size=B, episode_length=L)
+    u = env.unwrapped
+    keys = _keys(B, 41)
+    a = env.reset(torch.from_numpy(keys).cuda())
+    b = env.reset(torch.from_numpy(keys).cuda())
+    flags = _lib.F_EPISODE | _lib.F_AUTORESET
+    for t, act in enumerate(_actions(42, B, 3)):
+        act = torch.from_numpy(act).cuda()
+        a = env.step_(a, act)
+        bufs = u._bufs_of(b)
+        cs = u._cstate(bufs)
+        cs.ovf_mark = None
+        _lib.check(_lib.lib.pob_step(u._handle, B, C.byref(cs), C.c_void_p(act.data_ptr()), C.byref(cs), flags, L,
+                                     C.c_void_p(_lib.stream_handle(u.device))))
+        torch.cuda.synchronize()
+        for x, y in ((a.qp.pos, b.qp.pos), (a.qp.rot, b.qp.rot), (a.qp.vel, b.qp.vel), (a.obs, b.obs),
+                     (a.reward, b.reward), (a.aux["done"], b.aux["done"])):
+            assert torch.equal(x.view(torch.int32), y.view(torch.int32)), f"step {t}"

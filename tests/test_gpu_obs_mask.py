@@ -93,6 +93,8 @@ def test_obs_mask_errors():
         envs.create("ant_heavenhell", batch_size=8, obs_mask=[0, 114])
     with pytest.raises(TypeError):
         envs.create("ant_heavenhell", batch_size=8, obs_mask=[0.5])
+    with pytest.raises(ValueError):  # (not wrapped into range by the int32 cast)
+        envs.create("ant_heavenhell", batch_size=8, obs_mask=np.array([2 ** 32 + 3], np.int64))
     env = envs.create("ant_heavenhell", batch_size=8)
     assert env.masked_observation_size == 0 and env.obs_mask is None
 
@@ -114,3 +116,33 @@ def test_obs_mask_mixed_launch():
         ms = mix.step_(ms, [a.contiguous() for a in mix.split_actions(act)])
         for n, s in zip(names, ms):
             _check(s, idx, f"mixed {n} step {t}")
+
+
+@pytest.mark.parametrize("qp_dtype", [torch.float32, torch.float16])
+def test_obs_mask_written_by_masked_reset(qp_dtype):
+    """ABI v8: the masked reset writes the masked columns of the rows it resets (no
+    second gather launch after it) -- rows written straight from registers (one to three done
+    envs per wave, float32 storage) and rows staged in LDS (a whole wave; binary16 storage
+    always) -- and leaves every other row's masked columns as the step wrote them."""
+    from po_brax_amd import _lib
+    name, B = "ant_heavenhell", 1000
+    idx = _mask(name)
+    env = _envs().create(name, batch_size=B, auto_reset=False, episode_length=1000, obs_mask=idx,
+                         qp_dtype=qp_dtype)
+    s = env.reset(torch.from_numpy(_keys(B, 23)).cuda())
+    _check(s, idx, "reset")
+    rng = np.random.default_rng(6)
+    for _ in range(2):
+        s = env.step_(s, torch.from_numpy(rng.uniform(-1, 1, (B, 8)).astype(np.float32)).cuda())
+    done = np.zeros(B, np.float32)
+    done[[3, 17, 18, 200, 515, 777, 998, 999]] = 1.0
+    done[320:336] = 1.0
+    done[480:483] = 1.0
+    s.aux["done"].copy_(torch.from_numpy(done).cuda())
+    before = s.info["obs_masked"].clone()
+    env.unwrapped._reset_where_done(s, _lib.RESET_OWN)
+    torch.cuda.synchronize()
+    _check(s, idx, "masked reset")
+    keep = torch.from_numpy(done == 0).cuda()
+    assert torch.equal(s.info["obs_masked"][keep], before[keep])
+    assert not torch.equal(s.info["obs_masked"][~keep], before[~keep])

@@ -196,7 +196,7 @@ def test_staged_load_equals_per_lane_load(name, qp_dtype, B, monkeypatch):
         assert torch.equal(getattr(a.qp, f), getattr(b.qp, f)), f
     assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done)
     for k in a.aux:
-        if isinstance(a.aux[k], torch.Tensor):
+        if isinstance(a.aux[k], torch.Tensor) and k != "ovf_mark":  # (the split launch's scratch)
             assert torch.equal(a.aux[k], b.aux[k]), k
 
 

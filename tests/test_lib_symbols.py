@@ -31,7 +31,7 @@ def test_lib_exports_every_declared_symbol():
     exported = set(re.findall(r" T (pob_\w+)", out))
     assert set(_declared()) <= exported
     from po_brax_amd import _lib
-    assert lib.pob_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.pob_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_python_binding_covers_header():
