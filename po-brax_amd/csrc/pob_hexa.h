@@ -81,7 +81,45 @@ struct HMesh {
   v3 a, b;
   uint64_t mc;
   int nct;  // wall contacts of the position pass (the first HMAXC kept in the lane's LDS store)
+#ifdef POB_HEX_POOL
+  int head;   // the lane's first contact in the wave's pool (POB_HEX_POOL)
+  bool povf;  // the wave's contacts overflowed the pool (wave-uniform)
+#endif
 };
+#ifdef POB_HEX_POOL
+// (A/B build switch) the wave's contacts in an LDS pool, stored by the walk's winner lanes and
+// linked per lane by the owners (pob_mesh.h mesh_wave_walk HAND 2, as the four-lane kernel's
+// fast launch); the per-lane store and its hand-over loop otherwise
+#define HPOOL_N 64
+struct HPoolSink {
+  float *pool;
+  int npool;  // (wave-uniform)
+  int tail, head, nct;
+  uint64_t mc;
+  POB_D int store(const bool hit, const float tau, const v3 n, const float dist) {
+    const uint64_t m = __ballot(hit);
+    const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    npool += __popcll(m);
+    const bool ok = hit && idx < HPOOL_N;
+    if (ok) {
+      float *c = pool + 6 * idx;
+      c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist;
+    }
+    return ok ? idx + 1 : 0;
+  }
+  POB_D void link(const int, const int bit, const int e) {
+    if (e > 0) {
+      const int idx = e - 1;
+      pool[6 * idx + 5] = __int_as_float(-1);
+      if (tail >= 0) pool[6 * tail + 5] = __int_as_float(idx);
+      else head = idx;
+      tail = idx;
+      ++nct;
+      mc |= 1ull << bit;
+    }
+  }
+};
+#endif
 // The position pass's wall contacts (tau, n, pen), kept in the lane's slots of the staging
 // region (idle during the substeps; lane-minor: element e of the lane at CS[64 e]) so that the
 // velocity pass applies them without evaluating their faces again; a lane with more re-walks
@@ -108,6 +146,10 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   if (gc.pen > 0.0f) oground_position(g, SC, gc.pen, gc.pe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
   ms.mc = 0ull;
   ms.nct = 0;
+#ifdef POB_HEX_POOL
+  ms.head = -1;
+  ms.povf = false;
+#endif
   if (MW == 0) return;
   uint32_t m = 0u;
   {
@@ -149,6 +191,30 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   // five floats); the position responses follow from the store in walk order, one loop over
   // the lanes' contacts instead of the response code in every round's hand-over
   uint64_t Ms[1] = {M};
+#ifdef POB_HEX_POOL
+  // (CS: the wave's pool)
+  HPoolSink sink{CS, 0, -1, -1, 0, 0ull};
+  mesh_wave_walk<1, false, 2>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
+                    [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
+                    sink);
+  ms.mc = sink.mc;
+  ms.nct = sink.nct;
+  ms.head = sink.head;
+  ms.povf = sink.npool > HPOOL_N;
+  const bool ovf = ms.povf && ms.nct > 0;
+  {
+    int ci = ms.povf ? -1 : ms.head;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = CS + 6 * ci;
+        owall_position(g, SC, HT[HT_R] - c[4], vfma(rv, c[0], b.x), V(c[1], c[2], c[3]), 1e-6f + c[4], im, b.x, b.q,
+                       pq, px, DX, DA);
+        ci = __float_as_int(c[5]);
+      }
+    }
+  }
+#else
   mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     [&](const int, const int bit, const float tau, const v3 n, const float dist) {
@@ -171,6 +237,7 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
                      b.q, pq, px, DX, DA);
     }
   }
+#endif
   if (!__any(ovf)) return;
   // (rare) more contacts than the store holds: the contact faces walked again, each contact
   // applied as it comes (the same contacts in the same order)
@@ -191,6 +258,21 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
     ocontact_vel_one(g, SC, true, gc.pen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
   if (MW == 0 || !__any(ms.nct != 0)) return;
   const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
+#ifdef POB_HEX_POOL
+  const bool ovf = ms.povf && ms.nct > 0;
+  {
+    int ci = ms.povf || ms.nct == 0 ? -1 : ms.head;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = CS + 6 * ci;
+        ocontact_vel_pe(g, SC, false, HT[HT_R] - c[4], vfma(rv, c[0], b.x), V(c[1], c[2], c[3]), 1e-6f + c[4], im, b.x,
+                        b.v, b.w, dV, dW);
+        ci = __float_as_int(c[5]);
+      }
+    }
+  }
+#else
   const bool ovf = ms.nct > HMAXC;
   const int n = ovf ? 0 : ms.nct;
 #pragma unroll 1
@@ -202,6 +284,7 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
                       b.x, b.v, b.w, dV, dW);
     }
   }
+#endif
   if (!__any(ovf)) return;
   uint64_t Ms[1] = {ovf ? ms.mc : 0ull};
   mesh_wave_walk<1, false>(g, WT, HW.fc, HW.cz, HW.hz, Ms,

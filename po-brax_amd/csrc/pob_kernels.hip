@@ -769,7 +769,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
   POB_TS_DECL();  // timing experiment only (POB_EXP_TIMING)
   POB_TS(0);
   float *stg = lds + ((int)threadIdx.x >> 6) * POB_STAGE_FLOATS;  // this wave's region
-  const Lds Ls{stg, 64, lane};
+  const QLds Ls{stg, lane};
   int b = gt >> 2;
   int k = gt & 3;
   const float *LT = legtab + k * POB_LEG_FLOATS;
@@ -890,7 +890,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #pragma unroll
     for (int jl = 0; jl < QNJ; ++jl) a[jl] = act[(size_t)bl * POB_NJ + 2 * k + jl];
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) { Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f)); Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f)); }
+    for (int l = 0; l < QNB; ++l) { Ls.set3(l, QF_CV, V(0.0f, 0.0f, 0.0f)); Ls.set3(l, QF_CA, V(0.0f, 0.0f, 0.0f)); }
     const int iters = Sp->substeps / 2;
     const float fric = quad_friction(S);
     // (per kind, bit 1 << KIND: HH 1, GA 2, TAG 4, ant 8, mixed 16 -- the register allocation of
@@ -942,8 +942,8 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         bd.q[l] = ld4<QT>(in.rot, r4 + 4 * g);
         bd.v[l] = ld3<QT>(in.vel, r3 + 3 * g);
         bd.w[l] = ld3<QT>(in.ang, r3 + 3 * g);
-        Ls.set3(QL_CV(l), V(0.0f, 0.0f, 0.0f));
-        Ls.set3(QL_CA(l), V(0.0f, 0.0f, 0.0f));
+        Ls.set3(l, QF_CV, V(0.0f, 0.0f, 0.0f));
+        Ls.set3(l, QF_CA, V(0.0f, 0.0f, 0.0f));
       }
     };
     for (;;) {
@@ -1031,7 +1031,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
         st.b = bd;
 #pragma unroll
         for (int j = 0; j < QNJ; ++j) st.act[j] = a[j];
-        qpbd_substep_slow<WALLS>(Sp, LT, WT, &st, Ls.base, Ls.stride, Ls.t, (it & 1) != 0 ? 1 : 0, fric);
+        qpbd_substep_slow<WALLS>(Sp, LT, WT, &st, Ls.base, Ls.t, (it & 1) != 0 ? 1 : 0, fric);
         bd = st.b;
       } else
 #endif
@@ -1056,7 +1056,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
       jvel[jl] = vdot(vsub(bd.w[c], bd.w[p]), ap);
     }
 #pragma unroll
-    for (int l = 0; l < QNB; ++l) { cvl[l] = Ls.get3(QL_CV(l)); cal[l] = Ls.get3(QL_CA(l)); }
+    for (int l = 0; l < QNB; ++l) { cvl[l] = Ls.get3(l, QF_CV); cal[l] = Ls.get3(l, QF_CA); }
     if (act_lane && k == 0) {
       float steps = in.steps ? in.steps[b] : 0.0f;
       if ((flags & (POB_F_AUTORESET | POB_F_ZERO_STEPS_ON_DONE)) && in.done[b] != 0.0f) steps = 0.0f;
@@ -1073,7 +1073,7 @@ POB_D void step_quad_body(csys_t *Sp, const int B, const StatePtrs &in, const fl
 #pragma unroll
         for (int q = 1; q < 4; ++q) {
 #pragma unroll
-          for (int l = 1; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(QL_CV(l), lane + q));
+          for (int l = 1; l < QNB; ++l) sc = ant_contact_add(sc, Ls.get3_lane(l, QF_CV, lane + q));
         }
         t.contact = 0.0005f * sc;
       }
@@ -1351,6 +1351,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   POB_TS(0);
   __shared__ float stg[POB_OSTAGE_FLOATS];
   __shared__ __attribute__((aligned(16))) float otab[OT_TAB_FLOATS + HW_FLOATS];
+#ifdef POB_FC_LDS
+  __shared__ __attribute__((aligned(16))) float ofc[POB_FC_TAB_FLOATS];  // the walls' face constants
+#endif
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   __shared__ float ocst[OCS_FLOATS * 64];
@@ -1435,6 +1438,9 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
     stage_table<POB_MAXW * POB_WALL_FLOATS>(otab + 8 * OT_FLOATS, wsrc, (int)threadIdx.x, 64);
     hwalls_stage(S, otab + OT_TAB_FLOATS, lane);  // the walls' broadphase boxes, z extent, scalars
+#ifdef POB_FC_LDS
+    stage_table<POB_FC_TAB_FLOATS>(ofc, &Sp->face_c[0][0][0], (int)threadIdx.x, 64);
+#endif
     wave_lds_sync();
   }
   float OT[OT_FLOATS];  // the lane's role row, in registers (constant indices only)
@@ -1443,7 +1449,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
   const float *WT = otab + 8 * OT_FLOATS;
   constexpr int OMW = hex_max_walls(KIND);
   HWalls<OMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
+#ifdef POB_FC_LDS
+  hwalls_load(otab + OT_TAB_FLOATS, HW, ofc);
+#else
   hwalls_load(otab + OT_TAB_FLOATS, HW, pob_face_table(S));
+#endif
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)
@@ -1697,10 +1707,18 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   POB_TS(0);
   __shared__ float stg[POB_HSTAGE_FLOATS];
   __shared__ __attribute__((aligned(16))) float htab[HT_TAB_FLOATS + HW_FLOATS];
+#ifdef POB_FC_LDS
+  __shared__ __attribute__((aligned(16))) float hfc[POB_FC_TAB_FLOATS];  // the walls' face constants
+#endif
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
+#ifdef POB_HEX_POOL
+  __shared__ float hpool[6 * HPOOL_N];
+  float *const hcs = hpool;  // the wave's wall-contact pool (pob_hexa.h POB_HEX_POOL)
+#else
   float *const hcs = stg + lane;  // the lane's wall-contact store during the substeps (pob_hexa.h)
+#endif
   const int r = lane & 15;
   const bool hip = r < 8, isP = r < 4 || (r >= 8 && r < 12);
   const int k = r < 4 ? r : (r < 8 ? 7 - r : (r < 12 ? r - 8 : 15 - r));  // the leg
@@ -1768,6 +1786,9 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     const __attribute__((address_space(4))) float *wsrc = &Sp->wall_row[0][0];
     stage_table<POB_MAXW * POB_WALL_FLOATS>(htab + 16 * HT_FLOATS, wsrc, (int)threadIdx.x, 64);
     hwalls_stage(S, htab + HT_TAB_FLOATS, lane);  // the walls' broadphase boxes, z extent, scalars
+#ifdef POB_FC_LDS
+    stage_table<POB_FC_TAB_FLOATS>(hfc, &Sp->face_c[0][0][0], (int)threadIdx.x, 64);
+#endif
     wave_lds_sync();
   }
   float HT[HT_FLOATS];  // the lane's role row, in registers (constant indices only)
@@ -1775,7 +1796,11 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   for (int i = 0; i < HT_FLOATS; ++i) HT[i] = htab[r * HT_FLOATS + i];
   const float *WT = htab + 16 * HT_FLOATS;
   HWalls<HMW> HW;  // the walls in VGPRs (LDS loads: the compiler keeps them per lane)
+#ifdef POB_FC_LDS
+  hwalls_load(htab + HT_TAB_FLOATS, HW, hfc);
+#else
   hwalls_load(htab + HT_TAB_FLOATS, HW, pob_face_table(S));
+#endif
   POB_TS(1);
 
   // ---- physics (10 substeps in registers)

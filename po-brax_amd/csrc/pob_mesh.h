@@ -22,7 +22,10 @@
 
 #define POB_MESH_MARGIN 1e-3f
 // the face constants table (pob_sys::face_c) is read through the constant address space
-#ifdef POB_MESH_HOST
+// (POB_FC_LDS: a generic pointer -- the eight- and sixteen-lane kernels pass their LDS copy of
+// the table, the four-lane kernel the device table; the compiler infers each one's address
+// space through the inlined walk)
+#if defined(POB_MESH_HOST) || defined(POB_FC_LDS)
 typedef const float *fcptr_t;
 #else
 typedef __attribute__((address_space(4))) const float *fcptr_t;
@@ -202,13 +205,16 @@ struct MFace {
   float sg, ha, hb, w0, ha2, hb2;
   BSeg A;          // the capsule's segment
   fcptr_t fc;      // the face's constants (POB_FC_*)
-#ifdef POB_MESH_FC_INLINE  // A/B build switch: the constants formed per face evaluation
+#if defined(POB_MESH_FC_INLINE) || defined(POB_MESH_FC_VEC)
+  // (A/B build switches: the constants formed per face evaluation, or the face's row loaded
+  // whole -- three 16-B loads -- and each lane's class picked by selects instead of per-lane
+  // scattered loads)
   float cv[POB_FACE_FLOATS];
 #endif
 };
 // the face's constants: edge class c's (il, hl, idd), the diagonal's d.d, triangle t's 1 / det
 POB_D void mfc_edge(const MFace &F, const int c, float &il, float &hl, float &idd) {
-#ifdef POB_MESH_FC_INLINE
+#if defined(POB_MESH_FC_INLINE) || defined(POB_MESH_FC_VEC)
   il = c == 0 ? F.cv[POB_FC_IL(0)] : (c == 1 ? F.cv[POB_FC_IL(1)] : F.cv[POB_FC_IL(2)]);
   hl = c == 0 ? F.cv[POB_FC_HL(0)] : (c == 1 ? F.cv[POB_FC_HL(1)] : F.cv[POB_FC_HL(2)]);
   idd = c == 0 ? F.cv[POB_FC_IDD(0)] : (c == 1 ? F.cv[POB_FC_IDD(1)] : F.cv[POB_FC_IDD(2)]);
@@ -219,14 +225,14 @@ POB_D void mfc_edge(const MFace &F, const int c, float &il, float &hl, float &id
 #endif
 }
 POB_D float mfc_ed(const MFace &F) {
-#ifdef POB_MESH_FC_INLINE
+#if defined(POB_MESH_FC_INLINE) || defined(POB_MESH_FC_VEC)
   return F.cv[POB_FC_ED];
 #else
   return F.fc[POB_FC_ED];
 #endif
 }
 POB_D float mfc_idet(const MFace &F, const int t) {
-#ifdef POB_MESH_FC_INLINE
+#if defined(POB_MESH_FC_INLINE) || defined(POB_MESH_FC_VEC)
   return t == 0 ? F.cv[POB_FC_IDET(0)] : F.cv[POB_FC_IDET(1)];
 #else
   return F.fc[POB_FC_IDET(t)];
@@ -252,6 +258,23 @@ POB_D MFace mface(G &g, const int f, const BSeg &capw, const float hx, const flo
   F.ha2 = F.ha + F.ha;  // V1 - V0 = (ha - (-ha), ..): exact
   F.hb2 = F.hb + F.hb;
   F.fc = fcw + POB_FACE_FLOATS * k;
+#ifdef POB_MESH_FC_VEC
+#ifdef POB_MESH_HOST
+  for (int i = 0; i < POB_FACE_FLOATS; ++i) F.cv[i] = F.fc[i];
+#else
+  static_assert(POB_FACE_FLOATS == 12, "three 16-B loads per face row");
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#ifdef POB_FC_LDS
+    const f4v q = reinterpret_cast<const f4v *>(F.fc)[i];
+#else
+    const f4v q = reinterpret_cast<const __attribute__((address_space(4))) f4v *>(F.fc)[i];
+#endif
+    F.cv[4 * i] = q.x; F.cv[4 * i + 1] = q.y; F.cv[4 * i + 2] = q.z; F.cv[4 * i + 3] = q.w;
+  }
+#endif
+#endif
 #ifdef POB_MESH_FC_INLINE  // (pob_face_consts' operations in the guard's policy)
   {
     const float dA = F.ha2 * F.ha2, dB = F.hb2 * F.hb2, e_d = FMA(F.hb2, F.hb2, F.ha2 * F.ha2);
@@ -276,16 +299,27 @@ template <class G>
 POB_D float mface_tt(G &g, const MFace &F) {
   return bclamp01((F.sg * F.w0 - F.sg * F.A.p0.w) * g.rcp(F.sg * F.A.d.w + 1e-6f));
 }
-// edge e of the face as a segment: 0 V0 V1, 1 V1 V2, 2 V0 V2, 3 V2 V3, 4 V0 V3, 5 V2 V0, 6 V3 V0
+// edge e of the face as a segment: 0 V0 V1, 1 V1 V2, 2 V0 V2, 3 V2 V3, 4 V0 V3, 5 V2 V0, 6 V3 V0:
+// p0 = (sa ha, sb hb, w0), d = (ca 2ha, cb 2hb, 0) with signs and classes from bit tables indexed
+// by e -- branch-free for a runtime e (the walk's candidate lanes: a chain of compares and
+// branches per round before), constant-folded for a constant one; the products with +-1 and 0
+// are exact, so the terms are the same bits as the spelled-out selects of round 5
+#define ME_PA_NEG 0x55u   // e = 0, 2, 4, 6: p0.a = -ha
+#define ME_PB_NEG 0x17u   // e = 0, 1, 2, 4: p0.b = -hb
+#define ME_DA_NZ 0x2Du    // e = 0, 2, 3, 5: d.a != 0
+#define ME_DA_NEG 0x28u   // e = 3, 5: d.a = -2ha
+#define ME_DB_NZ 0x76u    // e = 1, 2, 4, 5, 6: d.b != 0
+#define ME_DB_NEG 0x60u   // e = 5, 6: d.b = -2hb
+#define ME_CLS 0x1924u    // class (2 bits per e): a-edges 0, b-edges 1, diagonals 2
 POB_D BSeg medge(const MFace &F, const int e) {
-  const float ha = F.ha, hb = F.hb, w0 = F.w0;
+  const float w0 = F.w0;
   BSeg s;
-  const bool ea = e == 0 || e == 3, eb = e == 1 || e == 4 || e == 6, ed = e == 2 || e == 5;
-  const float da = ea ? (e == 3 ? -F.ha2 : F.ha2) : (ed ? (e == 5 ? -F.ha2 : F.ha2) : 0.0f);
-  const float db = eb ? (e == 6 ? -F.hb2 : F.hb2) : (ed ? (e == 5 ? -F.hb2 : F.hb2) : 0.0f);
-  const float pa = (e == 1) ? ha : ((e == 3 || e == 5) ? ha : -ha);
-  const float pb = (e == 3 || e == 5 || e == 6) ? hb : -hb;
-  const int cls = ea ? 0 : (eb ? 1 : 2);
+  const float ca = ((ME_DA_NZ >> e) & 1u) ? (((ME_DA_NEG >> e) & 1u) ? -1.0f : 1.0f) : 0.0f;
+  const float cb = ((ME_DB_NZ >> e) & 1u) ? (((ME_DB_NEG >> e) & 1u) ? -1.0f : 1.0f) : 0.0f;
+  const float da = ca * F.ha2, db = cb * F.hb2;
+  const float pa = ((ME_PA_NEG >> e) & 1u) ? -F.ha : F.ha;
+  const float pb = ((ME_PB_NEG >> e) & 1u) ? -F.hb : F.hb;
+  const int cls = (int)((ME_CLS >> (2 * e)) & 3u);
   s.p0 = f3(pa, pb, w0);
   s.d = f3(da, db, 0.0f);
   mfc_edge(F, cls, s.il, s.hl, s.idd);
@@ -700,11 +734,17 @@ POB_D void mesh_lane_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
 }
 
 // (LANE_FALLBACK false: the caller guarantees all 64 lanes active and handles the per-lane
-// walk itself -- the four-lane kernel keeps it out of line)
-template <int NB, bool LANE_FALLBACK = true, class G, class SegOf, class Apply>
+// walk itself -- the four-lane kernel keeps it out of line.  HAND, how the contacts reach their
+// owners: 0 apply(s, bit, tau, n, dist) on the owner lane, triangle by triangle; 1 the same
+// hand-over with apply(want, s, bit, tau, n, dist) called on every lane (want: the owner's flag)
+// -- for a caller that allocates wave-shared storage by ballot; 2 the winners store their
+// contacts themselves (apply.store(hit, tau, n, dist) on every lane returns the stored entry + 1,
+// 0 for none), each triangle's entry is summed over its quad and the owners read their (at most
+// four) entries in one pass and link them in order (apply.link(s, bit, entry)): no hand-over loop)
+template <int NB, bool LANE_FALLBACK = true, int HAND = 0, class G, class SegOf, class Apply>
 POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, const float hz, uint64_t (&M)[NB],
                           SegOf &&seg_of, Apply &&apply) {
-  if (LANE_FALLBACK) {
+  if constexpr (LANE_FALLBACK) {
 #ifdef POB_MESH_LANE_WALK
     if (true) {  // A/B build switch: the per-lane walk everywhere
 #else
@@ -802,18 +842,30 @@ POB_D void mesh_wave_walk(G &g, const float *WT, fcptr_t FC, const float cz, con
       hit = mface_contact(g, F.k, c, ro, T, tau, nl, dst);
       if (hit) nw = mwall_world_n(W, nl);
     }
-    // the owners take their items' triangles in order: the winners' lanes first (all four
-    // fetches in flight), then each contact
-    const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 4 + mlane_read_i(kmin, g1 + 4);
-    const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 4 + mlane_read_i(kmin, g2 + 4);
-    const int nt = __any(own2) ? 4 : 2;
+    if constexpr (HAND == 2) {
+      // the winners' entries (a lane-order compaction: group, then triangle order -- each owner's
+      // contacts in walk order), summed over each triangle's quad (only its winner is nonzero)
+      const int e = apply.store(hit, tau, nw, dst);
+      const int eq = msum_dpp<0x4E>(msum_dpp<0xB1>(e));
+      const int e10 = mlane_read_i(eq, g1), e11 = mlane_read_i(eq, g1 + 4);
+      const int e20 = mlane_read_i(eq, g2), e21 = mlane_read_i(eq, g2 + 4);
+      if (own1) { apply.link(s, b1, e10); apply.link(s, b1, e11); }
+      if (own2) { apply.link(s, b2, e20); apply.link(s, b2, e21); }
+    } else {
+      // the owners take their items' triangles in order: the winners' lanes first (all four
+      // fetches in flight), then each contact
+      const int w10 = g1 + mlane_read_i(kmin, g1), w11 = g1 + 4 + mlane_read_i(kmin, g1 + 4);
+      const int w20 = g2 + mlane_read_i(kmin, g2), w21 = g2 + 4 + mlane_read_i(kmin, g2 + 4);
+      const int nt = __any(own2) ? 4 : 2;
 #pragma nounroll
-    for (int t = 0; t < nt; ++t) {
-      const int wl = t == 0 ? w10 : (t == 1 ? w11 : (t == 2 ? w20 : w21));
-      const int h = mlane_read_i(hit ? 1 : 0, wl);
-      const float tw = mlane_read(tau, wl), dw = mlane_read(dst, wl);
-      const v3 nn = V(mlane_read(nw.x, wl), mlane_read(nw.y, wl), mlane_read(nw.z, wl));
-      if ((t < 2 ? own1 : own2) && h != 0) apply(s, t < 2 ? b1 : b2, tw, nn, dw);
+      for (int t = 0; t < nt; ++t) {
+        const int wl = t == 0 ? w10 : (t == 1 ? w11 : (t == 2 ? w20 : w21));
+        const int h = mlane_read_i(hit ? 1 : 0, wl);
+        const float tw = mlane_read(tau, wl), dw = mlane_read(dst, wl);
+        const v3 nn = V(mlane_read(nw.x, wl), mlane_read(nw.y, wl), mlane_read(nw.z, wl));
+        if constexpr (HAND == 1) apply((t < 2 ? own1 : own2) && h != 0, s, t < 2 ? b1 : b2, tw, nn, dw);
+        else if ((t < 2 ? own1 : own2) && h != 0) apply(s, t < 2 ? b1 : b2, tw, nn, dw);
+      }
     }
   }
 }

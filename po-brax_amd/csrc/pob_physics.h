@@ -29,7 +29,7 @@ POB_D csys_t *launder(csys_t *p) {
   return p;
 }
 // the walls' face constants (pob_sys::face_c, pob_mesh.h MFace)
-POB_D fcptr_t pob_face_table(csys_t &S) { return &S.face_c[0][0][0]; }
+POB_D fcptr_t pob_face_table(csys_t &S) { return (fcptr_t)&S.face_c[0][0][0]; }
 // Scheduling fence between the independent joint / contact blocks: without it the machine
 // scheduler interleaves all of them for ILP and the live set blows past 512 registers.
 #ifdef POB_NO_FENCE

@@ -74,13 +74,67 @@ POB_D float q_cap_r(csys_t &S, const float *LT, int l) { return l == 0 ? S.cap_r
 
 POB_D constexpr int qbody_global(int l, int k) { return l == 0 ? 0 : l + 2 * k; }
 
-// Per-lane LDS scratch (lane-minor): substep-start pose of the 3 local bodies (21 floats)
-// and their Info.contact accumulators (18 floats).
-#define QL_PX(l) (7 * (l))
-#define QL_PQ(l) (7 * (l) + 3)
-#define QL_CV(l) (21 + 6 * (l))
-#define QL_CA(l) (21 + 6 * (l) + 3)
+// The wave's LDS region (QL_FLOATS x 64 floats; the obs / qp staging area between steps):
+// * lane-minor per-lane slots of the lane's own bodies (Aux k+1, lower leg): substep-start pose
+//   (7 floats each) and Info.contact accumulators (6 each), and the head of the lane's wall
+//   contact list (QLL_*; element e of lane t at base[64 e + t]);
+// * the torso's pose and accumulators once per lane quad (QLT_*; element e of quad j at
+//   base[64 QLL_FLOATS + 16 e + j]): the four lanes' torso replicas are bit-identical, lane
+//   k = 0 writes them, all four read (a broadcast);
+// * the wave's wall-contact pool (QPOOL_N contacts of 6 floats) of the fast launch: each
+//   collide substep's contacts in walk order, a list per lane (round 6: the four-lane kernel's
+//   per-lane contact array lived in scratch -- 384 B/lane, reads at 2.25x the algorithmic bytes).
+#define QLL_PX(l) (7 * ((l) - 1))       // l = 1, 2
+#define QLL_PQ(l) (7 * ((l) - 1) + 3)
+#define QLL_CV(l) (14 + 6 * ((l) - 1))
+#define QLL_CA(l) (14 + 6 * ((l) - 1) + 3)
+#define QLL_HEAD 26
+#define QLL_FLOATS 27
+#define QLT_PX 0
+#define QLT_PQ 3
+#define QLT_CV 7
+#define QLT_CA 10
+#define QLT_FLOATS 13
 #define QL_FLOATS 39
+#define QPOOL_OFF (QLL_FLOATS * 64 + QLT_FLOATS * 16)
+#define QPOOL_N ((QL_FLOATS * 64 - QPOOL_OFF) / 6)
+static_assert(QPOOL_N >= 64, "the contact pool holds at least one contact per lane");
+// field codes of a body's slots
+#define QF_PX 0
+#define QF_PQ 1
+#define QF_CV 2
+#define QF_CA 3
+struct QLds {
+  float *base;  // the wave's region
+  int t;        // the lane
+  POB_D static constexpr int lane_off(int l, int f) {
+    return f == QF_PX ? QLL_PX(l) : (f == QF_PQ ? QLL_PQ(l) : (f == QF_CV ? QLL_CV(l) : QLL_CA(l)));
+  }
+  POB_D static constexpr int torso_off(int f) {
+    return f == QF_PX ? QLT_PX : (f == QF_PQ ? QLT_PQ : (f == QF_CV ? QLT_CV : QLT_CA));
+  }
+  // element i of field f of local body l (torso: the quad's slot)
+  POB_D float *at(int l, int f, int i) const {
+    return l == 0 ? base + 64 * QLL_FLOATS + 16 * (torso_off(f) + i) + (t >> 2) : base + 64 * (lane_off(l, f) + i) + t;
+  }
+  POB_D v3 get3(int l, int f) const { return V(*at(l, f, 0), *at(l, f, 1), *at(l, f, 2)); }
+  POB_D q4 get4(int l, int f) const {
+    q4 q; q.w = *at(l, f, 0); q.x = *at(l, f, 1); q.y = *at(l, f, 2); q.z = *at(l, f, 3); return q;
+  }
+  POB_D void set3(int l, int f, v3 v) const {
+    if (l != 0 || (t & 3) == 0) { *at(l, f, 0) = v.x; *at(l, f, 1) = v.y; *at(l, f, 2) = v.z; }
+  }
+  POB_D void set4(int l, int f, q4 q) const {
+    if (l != 0 || (t & 3) == 0) { *at(l, f, 0) = q.w; *at(l, f, 1) = q.x; *at(l, f, 2) = q.y; *at(l, f, 3) = q.z; }
+  }
+  // body l's (l >= 1) accumulator of another lane of the wave
+  POB_D v3 get3_lane(int l, int f, int lane) const {
+    const float *p = base + 64 * lane_off(l, f) + lane;
+    return V(p[0], p[64], p[128]);
+  }
+  POB_D float *head() const { return base + 64 * QLL_HEAD + t; }
+  POB_D float *pool() const { return base + QPOOL_OFF; }
+};
 
 POB_D constexpr int qcontact_body(int c) { return c == 0 ? 0 : (c == 1 ? 2 : c - 2); }
 
@@ -124,7 +178,7 @@ struct QMesh {
 #endif
 struct QWalls {
   int nct;                // wall contacts of the position pass
-  float c[6 * QK];        // the first QK: body, tau, n, dist
+  float c[6 * QK];        // the first QK: body, tau, n, dist (the re-walk builds, OVF)
   float seg[6 * QNB];     // nct > QK only: the segments a, b of the three bodies
 };
 #ifndef POB_QUAD_WAVE_WALK
@@ -306,6 +360,81 @@ __device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float
   return ws->nct;
 }
 
+// The fast launch's walk (OVF false): the contacts go to the wave's LDS pool (QLds) in walk
+// order -- each hand-over step allocates the pool slots of the lanes receiving a contact by
+// ballot / mbcnt, and a lane links its contacts into a list (head in its LDS slot, each entry's
+// last float = body | (next + 1) << 2) -- so the passes read them from LDS instead of a private
+// array in scratch.  A wave whose contacts exceed the pool reports it in ovf (the fix-up launch
+// then steps it with the re-walks).
+// (POB_QUAD_POOL_DIRECT, the default: the winner lanes store the contacts and the owners only
+// link them -- pob_mesh.h mesh_wave_walk HAND 2)
+#ifndef POB_QUAD_POOL_DIRECT
+#define POB_QUAD_POOL_DIRECT 1
+#endif
+struct QPoolSink {
+  float *pool;
+  float *head;
+  int npool;  // (wave-uniform)
+  int tail, tail_l, nct;
+  POB_D int store(const bool hit, const float tau, const v3 n, const float dist) {
+    const uint64_t m = __ballot(hit);
+    const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    npool += __popcll(m);
+    const bool ok = hit && idx < QPOOL_N;
+    if (ok) {
+      float *c = pool + 6 * idx;
+      c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist;
+    }
+    return ok ? idx + 1 : 0;
+  }
+  POB_D void link(const int l, const int, const int e) {
+    if (e > 0) {
+      const int idx = e - 1;
+      pool[6 * idx + 5] = __int_as_float(l);
+      if (tail >= 0) pool[6 * tail + 5] = __int_as_float(((idx + 1) << 2) | tail_l);
+      else *head = __int_as_float(idx);
+      tail = idx;
+      tail_l = l;
+      ++nct;
+    }
+  }
+};
+POB_D void qwalls_walk_pool(csys_t &S, const float *LT, const float *WT, const QBody &b, uint64_t (&M)[QNB],
+                            QWalls &ws, const QLds &L, bool &ovf) {
+  GuardBranch g;
+#if POB_QUAD_POOL_DIRECT
+  QPoolSink sink{L.pool(), L.head(), 0, -1, 0, 0};
+  mesh_wave_walk<QNB, false, 2>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); }, sink);
+  ws.nct += sink.nct;
+  ovf = ovf | (sink.npool > QPOOL_N);
+  return;
+#endif
+  float *pool = L.pool();
+  int npool = 0;  // (wave-uniform)
+  int tail = -1, tail_l = 0;
+  mesh_wave_walk<QNB, false, 1>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
+             [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); },
+             [&](const bool want, const int l, const int, const float tau, const v3 n, const float dist) {
+    const uint64_t m = __ballot(want);
+    if (m == 0ull) return;
+    const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    npool += __popcll(m);
+    if (want) {
+      if (idx < QPOOL_N) {
+        float *c = pool + 6 * idx;
+        c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist; c[5] = __int_as_float(l);
+        if (tail >= 0) pool[6 * tail + 5] = __int_as_float(((idx + 1) << 2) | tail_l);
+        else *L.head() = __int_as_float(idx);
+        tail = idx;
+        tail_l = l;
+      }
+      ++ws.nct;
+    }
+  });
+  ovf = ovf | (npool > QPOOL_N);
+}
+
 // Wall contact detection of a collide substep, at the pose the position pass projects from
 // (after the kinetic update, before the joint projection: the face walk's working set then
 // meets only the pose -- the velocities are dead until the velocity projection rewrites them,
@@ -316,7 +445,8 @@ __device__ __attribute__((noinline)) int qwalls_walk_ool(csys_t *Sp, const float
 // it in *ovf (the wave then runs the step again in the slow pass, OVF true: the detection-time
 // segments kept for the re-walks)
 template <bool WALLS, bool OVF = true>
-POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws, bool *ovf = nullptr) {
+POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBody &b, QWalls &ws, const QLds &L,
+                         bool *ovf = nullptr) {
   ws.nct = 0;
   if (!WALLS) return;
   csys_t &S = *launder(Sp);
@@ -347,6 +477,10 @@ POB_D void qwalls_detect(csys_t *Sp, const float *LT, const float *WT, const QBo
   if (!__any((M[0] | M[1] | M[2]) != 0ull)) return;
 #if POB_QUAD_WAVE_WALK
   // (the step kernel runs its substeps on all 64 lanes of every wave: step_quad_body)
+  if (!OVF) {
+    qwalls_walk_pool(S, LT, WT, b, M, ws, L, *ovf);
+    return;
+  }
   qwalls_walk<false>(S, LT, WT, b, M, ws);
 #else
   ws.nct = qwalls_walk_ool(Sp, LT, WT, b.x[0], b.x[1], b.x[2], b.q[0], b.q[1], b.q[2], M[0], M[1], M[2], &ws);
@@ -446,7 +580,7 @@ __device__ __attribute__((noinline)) void qwalls_rewalk(csys_t *Sp, const float 
 #define POB_QUAD_REWALK_INLINE 1
 #endif
 template <bool VEL>
-POB_D void qwalls_rewalk_inl(csys_t &S, const float *LT, const float *WT, const QBody &b, const Lds &L,
+POB_D void qwalls_rewalk_inl(csys_t &S, const float *LT, const float *WT, const QBody &b, const QLds &L,
                              const QWalls &ws, const bool ovf, const float fric, v3 (&d0)[QNB], v3 (&d1)[QNB]) {
   GuardBranch g;
   const HCon SC{fric, S.inv_h};
@@ -468,7 +602,7 @@ POB_D void qwalls_rewalk_inl(csys_t &S, const float *LT, const float *WT, const 
       v3 px[QNB];
       q4 pq[QNB];
 #pragma unroll
-      for (int k = 0; k < QNB; ++k) { px[k] = L.get3(QL_PX(k)); pq[k] = L.get4(QL_PQ(k)); }
+      for (int k = 0; k < QNB; ++k) { px[k] = L.get3(k, QF_PX); pq[k] = L.get4(k, QF_PQ); }
       qwall_pos_one(g, S, SC, LT, b.x, b.q, px, pq, l, tau, n, dist, d0, d1);
     }
   });
@@ -477,7 +611,7 @@ POB_D void qwalls_rewalk_inl(csys_t &S, const float *LT, const float *WT, const 
 // Position pass of a collide substep: ground contacts (ground first per body, oracle order),
 // then the wall contacts from the store in detection order
 template <bool WALLS, bool OVF = true>
-POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBody &b, const Lds &L, QGround &gc,
+POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBody &b, const QLds &L, QGround &gc,
                               const QWalls &ws, v3 (&DX)[QNB], v3 (&DA)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
@@ -492,7 +626,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBod
       const int l = qcontact_body(c);
       if (gc.pen[c] > 0.0f)
         oground_position(g, SC, gc.pen[c], pe[c], qground_r(S, LT, c), q_inv_mass(S, LT, l), b.x[l], b.q[l],
-                         L.get4(QL_PQ(l)), L.get3(QL_PX(l)), DX[l], DA[l]);
+                         L.get4(l, QF_PQ), L.get3(l, QF_PX), DX[l], DA[l]);
     }
   }
   if (!WALLS || !__any(ws.nct != 0)) return;
@@ -500,7 +634,23 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBod
   v3 px[QNB];
   q4 pq[QNB];
 #pragma unroll
-  for (int l = 0; l < QNB; ++l) { px[l] = L.get3(QL_PX(l)); pq[l] = L.get4(QL_PQ(l)); }
+  for (int l = 0; l < QNB; ++l) { px[l] = L.get3(l, QF_PX); pq[l] = L.get4(l, QF_PQ); }
+#if POB_QUAD_WAVE_WALK
+  if (!OVF) {  // the fast pass: the lane's list in the wave's pool (a wave with an overflow runs the step again)
+    const float *pool = L.pool();
+    int ci = ws.nct > 0 ? __float_as_int(*L.head()) : -1;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = pool + 6 * ci;
+        const int meta = __float_as_int(c[5]);
+        qwall_pos_one(g, S, SC, LT, b.x, b.q, px, pq, meta & 3, c[0], V(c[1], c[2], c[3]), c[4], DX, DA);
+        ci = (meta >> 2) - 1;
+      }
+    }
+    return;
+  }
+#endif
   const bool ovf = ws.nct > QK;
   const int nc = ovf ? 0 : ws.nct;
 #pragma unroll 1
@@ -542,7 +692,7 @@ POB_D void qcontacts_position(csys_t *Sp, const float *LT, const float *WT, QBod
 // x + tau rotate(e0, q) at the post-projection pose)
 template <bool WALLS, bool OVF = true>
 POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, QBody &b, const QGround &gc,
-                              const QWalls &ws, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
+                              const QWalls &ws, const QLds &L, v3 (&dV)[QNB], v3 (&dW)[QNB], const float fric) {
   csys_t &S = *launder(Sp);
   const HCon SC{fric, S.inv_h};
   GuardBranch g;
@@ -562,6 +712,22 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, QBod
   return;  // timing experiment only: no velocity-pass wall contacts
 #endif
   POB_FENCE();
+#if POB_QUAD_WAVE_WALK
+  if (!OVF) {
+    const float *pool = L.pool();
+    int ci = ws.nct > 0 ? __float_as_int(*L.head()) : -1;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = pool + 6 * ci;
+        const int meta = __float_as_int(c[5]);
+        qwall_vel_one(g, S, SC, LT, b.x, b.q, b.v, b.w, meta & 3, c[0], V(c[1], c[2], c[3]), c[4], dV, dW);
+        ci = (meta >> 2) - 1;
+      }
+    }
+    return;
+  }
+#endif
   const bool ovf = ws.nct > QK;
   const int nc = ovf ? 0 : ws.nct;
 #pragma unroll 1
@@ -575,7 +741,7 @@ POB_D void qcontacts_velocity(csys_t *Sp, const float *LT, const float *WT, QBod
   if (!OVF) return;  // (the fast pass: a wave with an overflow runs the step again)
 #if POB_QUAD_REWALK_INLINE
 #ifndef POB_EXP_NO_REWALK
-  if (__any(ovf)) qwalls_rewalk_inl<true>(S, LT, WT, b, Lds{nullptr, 0, 0}, ws, ovf, fric, dV, dW);
+  if (__any(ovf)) qwalls_rewalk_inl<true>(S, LT, WT, b, QLds{nullptr, 0}, ws, ovf, fric, dV, dW);
 #endif
   if (false) {
 #else
@@ -747,10 +913,10 @@ POB_D float quad_friction(const csys_t &S) {
 // mask is not empty in *near -- with every mask empty the wall pass finds no face item, so
 // the two passes compute the same bits.
 template <bool WALLS, bool CHECK = false, bool OVF = true>
-POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const Lds &L,
+POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ], const QLds &L,
                         const bool COLLIDE, const float fric, bool *near = nullptr, bool *ovf = nullptr) {
 #pragma unroll
-  for (int l = 0; l < QNB; ++l) { L.set3(QL_PX(l), b.x[l]); L.set4(QL_PQ(l), b.q[l]); }
+  for (int l = 0; l < QNB; ++l) { L.set3(l, QF_PX, b.x[l]); L.set4(l, QF_PQ, b.q[l]); }
   // 1. acceleration level.  Torso: dw0 = (((0 - t0) - t2) - t4) - t6 over the quad.
   {
     v3 tt[QNJ];
@@ -794,7 +960,7 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   // 2b. wall contact detection (collide substeps), at the pose the projection starts from
   QWalls ws;
   ws.nct = 0;
-  if (COLLIDE) qwalls_detect<WALLS, OVF>(Sp, LT, WT, b, ws, ovf);
+  if (COLLIDE) qwalls_detect<WALLS, OVF>(Sp, LT, WT, b, ws, L, ovf);
   if (CHECK && COLLIDE) *near = *near | (qwall_mask(*launder(Sp), b) != 0u);
   // 3. position projection
   QGround gc;
@@ -836,8 +1002,8 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
   for (int l = 0; l < QNB; ++l) {
     csys_t &S = *launder(Sp);
     b.q[l] = qnormalize(b.q[l]);
-    b.v[l] = vscl(vsub(b.x[l], L.get3(QL_PX(l))), S.inv_h);
-    q4 dq = qmul(b.q[l], qinv(L.get4(QL_PQ(l))));
+    b.v[l] = vscl(vsub(b.x[l], L.get3(l, QF_PX)), S.inv_h);
+    q4 dq = qmul(b.q[l], qinv(L.get4(l, QF_PQ)));
     // sg ((2 dq) inv_h) == dq (sg 2 inv_h) bit for bit (scaling by 2 and by +-1 is exact)
     const float k2 = 2.0f * S.inv_h;
     const float kw = dq.w >= 0.0f ? k2 : -k2;
@@ -848,12 +1014,12 @@ POB_D void qpbd_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, 
     v3 dV[QNB], dW[QNB];
 #pragma unroll
     for (int l = 0; l < QNB; ++l) { dV[l] = V(0.0f, 0.0f, 0.0f); dW[l] = V(0.0f, 0.0f, 0.0f); }
-    qcontacts_velocity<WALLS, OVF>(Sp, LT, WT, b, gc, ws, dV, dW, fric);
+    qcontacts_velocity<WALLS, OVF>(Sp, LT, WT, b, gc, ws, L, dV, dW, fric);
 #pragma unroll
     for (int l = 0; l < QNB; ++l) {
       b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
-      L.set3(QL_CV(l), vadd(L.get3(QL_CV(l)), dV[l]));
-      L.set3(QL_CA(l), vadd(L.get3(QL_CA(l)), dW[l]));
+      L.set3(l, QF_CV, vadd(L.get3(l, QF_CV), dV[l]));
+      L.set3(l, QF_CA, vadd(L.get3(l, QF_CA), dW[l]));
     }
   }
 }
@@ -867,13 +1033,13 @@ struct QSlow {
 };
 template <bool WALLS>
 __device__ __attribute__((noinline)) void qpbd_substep_slow(csys_t *Sp, const float *LT, const float *WT, QSlow *st,
-                                                           float *lbase, const int lstride, const int lt, const int collide,
+                                                           float *lbase, const int lt, const int collide,
                                                            const float fric) {
   QBody b = st->b;
   float act[QNJ];
 #pragma unroll
   for (int j = 0; j < QNJ; ++j) act[j] = st->act[j];
-  const Lds L{lbase, lstride, lt};
+  const QLds L{lbase, lt};
   qpbd_substep<WALLS>(Sp, LT, WT, b, act, L, collide != 0, fric);
   st->b = b;
 }
@@ -918,7 +1084,7 @@ POB_D QSpring qlegacy_joint(csys_t &S, const float *LT, const QBody &b, const in
 
 template <bool WALLS>
 POB_D void qlegacy_substep(csys_t *Sp, const float *LT, const float *WT, QBody &b, const float (&act)[QNJ],
-                           const Lds &L) {
+                           const QLds &L) {
   // kinetic
   {
     csys_t &S = *launder(Sp);
@@ -968,7 +1134,7 @@ POB_D void qlegacy_substep(csys_t *Sp, const float *LT, const float *WT, QBody &
 #pragma unroll
   for (int l = 0; l < QNB; ++l) {
     b.v[l] = vadd(b.v[l], dV[l]); b.w[l] = vadd(b.w[l], dW[l]);
-    L.set3(QL_CV(l), vadd(L.get3(QL_CV(l)), dV[l]));
-    L.set3(QL_CA(l), vadd(L.get3(QL_CA(l)), dW[l]));
+    L.set3(l, QF_CV, vadd(L.get3(l, QF_CV), dV[l]));
+    L.set3(l, QF_CA, vadd(L.get3(l, QF_CA), dW[l]));
   }
 }

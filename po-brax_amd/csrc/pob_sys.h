@@ -45,6 +45,7 @@
 // same IEEE operations as the oracle's per-face evaluation (sqrt, division and fma are
 // correctly rounded here and there), formed once per env instead of per face evaluation.
 #define POB_FACE_FLOATS 12
+#define POB_FC_TAB_FLOATS (POB_MAXW * 3 * POB_FACE_FLOATS)  // pob_sys::face_c
 #define POB_FC_IL(c) (3 * (c))
 #define POB_FC_HL(c) (3 * (c) + 1)
 #define POB_FC_IDD(c) (3 * (c) + 2)
@@ -90,7 +91,7 @@ struct pob_sys {
   // a culled wall is farther than r from the capsule, no contact)
   float wall_lo[POB_MAXW][3], wall_hi[POB_MAXW][3];
   float wall_cz, wall_hz;  // the common centre z / half-extent z of every wall
-  float face_c[POB_MAXW][3][POB_FACE_FLOATS];  // pob_face_consts of every wall's three axes
+  alignas(16) float face_c[POB_MAXW][3][POB_FACE_FLOATS];  // pob_face_consts of every wall's three axes (rows of 48 B, 16-B aligned)
   float friction, s_pos, half_s_ang;
   // legacy spring dynamics (pob_params.legacy_spring; brax <= 0.0.12): joint stiffness, spring
   // damping, limit strength, Baumgarte rate (baumgarte_erp * substeps / dt)
