@@ -77,19 +77,24 @@ struct HGround {
   float pen;
   v3 pe;  // x + rotate(end, q)
 };
+// (POB_HEX_POOL, the default since round 6: the wave's contacts in an LDS pool, stored by the
+// walk's winner lanes and linked per lane by the owners -- HH B = 4 096 0.0596 -> 0.0563 ms,
+// 8 192 0.0699 -> 0.0672, profiles/r7g/ab.txt; 0: the per-lane store with its hand-over loop)
+#ifndef POB_HEX_POOL
+#define POB_HEX_POOL 1
+#endif
 struct HMesh {
   v3 a, b;
   uint64_t mc;
   int nct;  // wall contacts of the position pass (the first HMAXC kept in the lane's LDS store)
-#ifdef POB_HEX_POOL
+#if POB_HEX_POOL
   int head;   // the lane's first contact in the wave's pool (POB_HEX_POOL)
   bool povf;  // the wave's contacts overflowed the pool (wave-uniform)
 #endif
 };
-#ifdef POB_HEX_POOL
-// (A/B build switch) the wave's contacts in an LDS pool, stored by the walk's winner lanes and
-// linked per lane by the owners (pob_mesh.h mesh_wave_walk HAND 2, as the four-lane kernel's
-// fast launch); the per-lane store and its hand-over loop otherwise
+#if POB_HEX_POOL
+// the wave's contact pool (pob_mesh.h mesh_wave_walk HAND 2, as the four-lane kernel's fast
+// launch): each entry tau, n, dist and the index of the lane's next entry (-1: the last)
 #define HPOOL_N 64
 struct HPoolSink {
   float *pool;
@@ -100,22 +105,23 @@ struct HPoolSink {
     const uint64_t m = __ballot(hit);
     const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     npool += __popcll(m);
-    const bool ok = hit && idx < HPOOL_N;
-    if (ok) {
+    if (hit && idx < HPOOL_N) {
       float *c = pool + 6 * idx;
       c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist;
     }
-    return ok ? idx + 1 : 0;
+    return hit ? idx + 1 : 0;  // (past the pool too: the owner still counts the contact and its face)
   }
   POB_D void link(const int, const int bit, const int e) {
     if (e > 0) {
       const int idx = e - 1;
-      pool[6 * idx + 5] = __int_as_float(-1);
-      if (tail >= 0) pool[6 * tail + 5] = __int_as_float(idx);
-      else head = idx;
-      tail = idx;
       ++nct;
-      mc |= 1ull << bit;
+      mc |= 1ull << bit;  // (the face's contacts are re-walked if the pool overflowed)
+      if (idx < HPOOL_N) {
+        pool[6 * idx + 5] = __int_as_float(-1);
+        if (tail >= 0) pool[6 * tail + 5] = __int_as_float(idx);
+        else head = idx;
+        tail = idx;
+      }
     }
   }
 };
@@ -146,7 +152,7 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   if (gc.pen > 0.0f) oground_position(g, SC, gc.pen, gc.pe, HT[HT_GR], im, b.x, b.q, pq, px, DX, DA);
   ms.mc = 0ull;
   ms.nct = 0;
-#ifdef POB_HEX_POOL
+#if POB_HEX_POOL
   ms.head = -1;
   ms.povf = false;
 #endif
@@ -191,7 +197,7 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
   // five floats); the position responses follow from the store in walk order, one loop over
   // the lanes' contacts instead of the response code in every round's hand-over
   uint64_t Ms[1] = {M};
-#ifdef POB_HEX_POOL
+#if POB_HEX_POOL
   // (CS: the wave's pool)
   HPoolSink sink{CS, 0, -1, -1, 0, 0ull};
   mesh_wave_walk<1, false, 2>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
@@ -258,7 +264,7 @@ POB_D void hcontacts_velocity(G &g, const HCon &SC, const float *HT, const float
     ocontact_vel_one(g, SC, true, gc.pen, HTV(HT, HT_GE), V(0.0f, 0.0f, 1.0f), HT[HT_GR], im, b.x, b.q, b.v, b.w, dV, dW);
   if (MW == 0 || !__any(ms.nct != 0)) return;
   const v3 rv = qrot_xy(HTV(HT, HT_E0), b.q);
-#ifdef POB_HEX_POOL
+#if POB_HEX_POOL
   const bool ovf = ms.povf && ms.nct > 0;
   {
     int ci = ms.povf || ms.nct == 0 ? -1 : ms.head;

@@ -1713,7 +1713,7 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
   const int lane = (int)threadIdx.x;
-#ifdef POB_HEX_POOL
+#if POB_HEX_POOL
   __shared__ float hpool[6 * HPOOL_N];
   float *const hcs = hpool;  // the wave's wall-contact pool (pob_hexa.h POB_HEX_POOL)
 #else

@@ -380,22 +380,23 @@ struct QPoolSink {
     const uint64_t m = __ballot(hit);
     const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     npool += __popcll(m);
-    const bool ok = hit && idx < QPOOL_N;
-    if (ok) {
+    if (hit && idx < QPOOL_N) {
       float *c = pool + 6 * idx;
       c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist;
     }
-    return ok ? idx + 1 : 0;
+    return hit ? idx + 1 : 0;  // (past the pool: counted, never stored -- the wave goes to the fix-up launch)
   }
   POB_D void link(const int l, const int, const int e) {
     if (e > 0) {
       const int idx = e - 1;
-      pool[6 * idx + 5] = __int_as_float(l);
-      if (tail >= 0) pool[6 * tail + 5] = __int_as_float(((idx + 1) << 2) | tail_l);
-      else *head = __int_as_float(idx);
-      tail = idx;
-      tail_l = l;
       ++nct;
+      if (idx < QPOOL_N) {
+        pool[6 * idx + 5] = __int_as_float(l);
+        if (tail >= 0) pool[6 * tail + 5] = __int_as_float(((idx + 1) << 2) | tail_l);
+        else *head = __int_as_float(idx);
+        tail = idx;
+        tail_l = l;
+      }
     }
   }
 };
