@@ -630,14 +630,16 @@ def step_kernel(B: int, env: str = "ant_heavenhell") -> str:
 
 def split_launch(env: str, B: int, legacy: bool) -> bool:
     """Does pob_step launch the four-lane kernel as a fast launch + a fix-up launch here
-    (pob_kernels.hip quad_split_launch: HH, GA, TAG on the four-lane kernel; GA at <= 3 waves
-    per SIMD and the mixed launch stay one launch; POB_QUAD_SPLIT overrides)?"""
-    if legacy or env in ("ant", "mixed") or step_kernel(B, env) != "k_step_quad":
+    (pob_kernels.hip quad_split_launch: HH, GA, TAG on the four-lane kernel and, since round 6,
+    the mixed launch; GA at <= 3 waves per SIMD stays one launch; POB_QUAD_SPLIT overrides)?"""
+    f = os.environ.get("POB_QUAD_SPLIT")
+    if env == "mixed" and not legacy:
+        return int(f) != 0 if f else True
+    if legacy or env == "ant" or step_kernel(B, env) != "k_step_quad":
         return False
     n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     if env == "ant_gather" and 4 * B <= 3 * 64 * 4 * n_cu:
         return False
-    f = os.environ.get("POB_QUAD_SPLIT")
     return int(f) != 0 if f else True
 
 

@@ -1356,7 +1356,11 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 #endif
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
+#if POB_OCT_POOL
+  __shared__ float ocst[OCS_FLOATS * 64 + 6 * OPOOL_N];  // the lanes' stores, then the wave's contact pool
+#else
   __shared__ float ocst[OCS_FLOATS * 64];
+#endif
   const int lane = (int)threadIdx.x;
   float *const ocs = ocst + lane;  // the lane's wall-contact store (pob_octet.h)
   const int m = lane & 7;
@@ -2879,9 +2883,11 @@ static void launch_step_oct(int kind, int n_cu, hipStream_t st, const void *sp, 
 }
 // The fast + fix-up launches per kind (bit 1 << kind, mixed 16): HH B = 65 536 0.1877 ->
 // 0.1634 ms, TAG 0.1192 -> 0.1055, GA 0.1148 -> 0.1145, mixed fp16 B = 32 768 0.1281 -> 0.1316
-// (profiles/r6b_ab.txt, r6c_ab.txt); POB_QUAD_SPLIT=0 / 1 forces the one-launch form / the split.
+// (profiles/r6b_ab.txt, r6c_ab.txt); since round 6's LDS contact pool (no scratch in the fast
+// launch) the mixed launch too: fp16 B = 32 768 0.1231 -> 0.1149 ms (profiles/r7h).
+// POB_QUAD_SPLIT=0 / 1 forces the one-launch form / the split.
 #ifndef POB_QUAD_SPLIT_KINDS
-#define POB_QUAD_SPLIT_KINDS 7
+#define POB_QUAD_SPLIT_KINDS 23
 #endif
 static bool quad_split_launch(int kind) {
   const char *f = getenv("POB_QUAD_SPLIT");

@@ -72,11 +72,56 @@ struct OGround {
   float pen;
   v3 pe;  // x + rotate(end, q)
 };
+// (POB_OCT_POOL: the wave's contacts in an LDS pool after the per-lane store -- OPOOL_N entries
+// of tau, n, dist and (next + 1) << 1 | slot -- stored by the walk's winner lanes and linked
+// per lane by the owners (pob_mesh.h mesh_wave_walk HAND 2); the position responses then follow
+// the list after the walk instead of inside its hand-over)
+#ifndef POB_OCT_POOL
+#define POB_OCT_POOL 0
+#endif
+#define OPOOL_N 64
 struct OMesh {
   v3 a[ONB], b[ONB];
   uint64_t mc[ONB];
   int nct;  // wall contacts of the position pass (the first OMAXC kept in the lane's LDS store)
+#if POB_OCT_POOL
+  int head;
+  bool povf;
+#endif
 };
+#if POB_OCT_POOL
+struct OPoolSink {
+  float *pool;
+  int npool;  // (wave-uniform)
+  int tail, tail_s, head, nct;
+  uint64_t mc0, mc1;
+  POB_D int store(const bool hit, const float tau, const v3 n, const float dist) {
+    const uint64_t m = __ballot(hit);
+    const int idx = npool + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    npool += __popcll(m);
+    if (hit && idx < OPOOL_N) {
+      float *c = pool + 6 * idx;
+      c[0] = tau; c[1] = n.x; c[2] = n.y; c[3] = n.z; c[4] = dist;
+    }
+    return hit ? idx + 1 : 0;
+  }
+  POB_D void link(const int s, const int bit, const int e) {
+    if (e > 0) {
+      const int idx = e - 1;
+      ++nct;
+      mc0 |= s == 0 ? 1ull << bit : 0ull;
+      mc1 |= s == 1 ? 1ull << bit : 0ull;
+      if (idx < OPOOL_N) {
+        pool[6 * idx + 5] = __int_as_float(s);
+        if (tail >= 0) pool[6 * tail + 5] = __int_as_float(((idx + 1) << 1) | tail_s);
+        else head = idx;
+        tail = idx;
+        tail_s = s;
+      }
+    }
+  }
+};
+#endif
 // The position pass's wall contacts (slot, tau, n, dist), kept in the lane's LDS store
 // (lane-minor: element e at CS[64 e]) so that the velocity pass applies them without evaluating
 // their faces again; a lane with more re-walks its contact faces (ms.mc) from its segments,
@@ -216,6 +261,56 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
 #ifdef POB_EXP_NO_WALK
   return;  // timing experiment only: broadphase and face cull, no face walk
 #endif
+  // one position response (slot s, the contact's tau, n, dist)
+  auto pos_one = [&](const int s, const float tau, const v3 n, const float dist) {
+    const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
+    const q4 q = qsel(s == 0, b.q[0], b.q[1]);
+    const v3 pe = vfma(vsel3(s == 0, rv[0], rv[1]), tau, x);
+    v3 dx = vsel3(s == 0, DX[0], DX[1]), da = vsel3(s == 0, DA[0], DA[1]);
+    owall_position(g, SC, (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) - dist, pe, n, 1e-6f + dist,
+                   s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, q, qsel(s == 0, pqs[0], pqs[1]), vsel3(s == 0, pxs[0], pxs[1]),
+                   dx, da);
+    DX[0] = vsel3(s == 0, dx, DX[0]); DX[1] = vsel3(s == 1, dx, DX[1]);
+    DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
+  };
+#if POB_OCT_POOL
+  {
+    float *pool = CS - (int)__lane_id() + OCS_FLOATS * 64;  // (after the lanes' stores)
+    OPoolSink sink{pool, 0, -1, 0, -1, 0, 0ull, 0ull};
+    mesh_wave_walk<ONB, false, 2>(g, WT, HW.fc, HW.cz, HW.hz, M,
+                        [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
+                        sink);
+    ms.mc[0] = sink.mc0; ms.mc[1] = sink.mc1;
+    ms.nct = sink.nct;
+    ms.head = sink.head;
+    ms.povf = sink.npool > OPOOL_N;
+    int ci = ms.povf ? -1 : ms.head;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = pool + 6 * ci;
+        const int meta = __float_as_int(c[5]);
+        pos_one(meta & 1, c[0], V(c[1], c[2], c[3]), c[4]);
+        ci = (meta >> 1) - 1;
+      }
+    }
+    const bool ovf = ms.povf && ms.nct > 0;
+    if (__any(ovf)) {
+      // (rare) the pool overflowed: the lanes with contacts walk their contact faces again,
+      // each response applied as it comes, and keep their segments for the velocity pass
+      uint64_t Mo[ONB] = {ovf ? ms.mc[0] : 0ull, ovf ? ms.mc[1] : 0ull};
+      mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, Mo,
+                          [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
+                          [&](const int s, const int, const float tau, const v3 n, const float dist) { pos_one(s, tau, n, dist); });
+#pragma unroll
+      for (int q = 0; q < ONB; ++q) {
+        float *c = CS + 64 * (OCS_SEG + 6 * q);
+        c[0] = ms.a[q].x; c[64] = ms.a[q].y; c[128] = ms.a[q].z; c[192] = ms.b[q].x; c[256] = ms.b[q].y; c[320] = ms.b[q].z;
+      }
+    }
+    return;
+  }
+#endif
   mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
                       [&](const int s, const int bit, const float tau, const v3 n, const float dist) {
@@ -259,6 +354,31 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
                        b.q[s], b.v[s], b.w[s], dV[s], dW[s]);
   }
   if (MW == 0 || !__any(ms.nct != 0)) return;
+#if POB_OCT_POOL
+  const bool ovf = ms.povf && ms.nct > 0;
+  {
+    const float *pool = CS - (int)__lane_id() + OCS_FLOATS * 64;
+    int ci = ms.povf || ms.nct == 0 ? -1 : ms.head;
+#pragma unroll 1
+    while (__any(ci >= 0)) {
+      if (ci >= 0) {
+        const float *c = pool + 6 * ci;
+        const int meta = __float_as_int(c[5]);
+        const int s = meta & 1;
+        const v3 x = vsel3(s == 0, b.x[0], b.x[1]);
+        const q4 q = qsel(s == 0, b.q[0], b.q[1]);
+        const v3 pe = vfma(qrot_xy(s == 0 ? OTV(OT, OT_B(0) + 2) : OTV(OT, OT_B(1) + 2), q), c[0], x);
+        v3 dv = vsel3(s == 0, dV[0], dV[1]), dw = vsel3(s == 0, dW[0], dW[1]);
+        ocontact_vel_pe(g, SC, false, (s == 0 ? OT[OT_B(0) + 1] : OT[OT_B(1) + 1]) - c[4], pe, V(c[1], c[2], c[3]),
+                        1e-6f + c[4], s == 0 ? OT[OT_B(0)] : OT[OT_B(1)], x, vsel3(s == 0, b.v[0], b.v[1]),
+                        vsel3(s == 0, b.w[0], b.w[1]), dv, dw);
+        dV[0] = vsel3(s == 0, dv, dV[0]); dV[1] = vsel3(s == 1, dv, dV[1]);
+        dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
+        ci = (meta >> 1) - 1;
+      }
+    }
+  }
+#else
   const bool ovf = ms.nct > OMAXC;
   const int nc = ovf ? 0 : ms.nct;
 #pragma unroll 1
@@ -278,6 +398,7 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
       dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
     }
   }
+#endif
   if (!__any(ovf)) return;
   uint64_t M[ONB] = {ovf ? ms.mc[0] : 0ull, ovf ? ms.mc[1] : 0ull};
   mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
