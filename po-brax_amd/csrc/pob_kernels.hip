@@ -1356,11 +1356,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
 #endif
   csys_t *Sp = (csys_t *)(size_t)sysp;
   csys_t &S = *Sp;
-#if POB_OCT_POOL
-  __shared__ float ocst[OCS_FLOATS * 64 + 6 * OPOOL_N];  // the lanes' stores, then the wave's contact pool
-#else
-  __shared__ float ocst[OCS_FLOATS * 64];
-#endif
+  __shared__ float ocst[OCS_FLOATS * 64 + (oct_pool(KIND) ? 6 * OPOOL_N : 0)];  // the lanes' stores (then the wave's contact pool)
   const int lane = (int)threadIdx.x;
   float *const ocs = ocst + lane;  // the lane's wall-contact store (pob_octet.h)
   const int m = lane & 7;
@@ -1482,15 +1478,15 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
     const int iters = Sp->substeps / 2;
 #if defined(POB_EXP_NO_COLLIDE)
     GuardBranch gb;
-    for (int it = 0; it < 2 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
+    for (int it = 0; it < 2 * iters; ++it) opbd_substep<OMW, oct_pool(KIND)>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
 #elif defined(POB_EXP_NO_PHYSICS)
     GuardBranch gb;
-    for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
+    for (int it = 0; it < 0 * iters; ++it) opbd_substep<OMW, oct_pool(KIND)>(gb, Sp, OT, WT, HW, isA, bd, a, cvl, cal, false, ocs);  // timing experiment only
 #else
 #ifdef POB_EXP_TIMING_SUB  // timing experiment only: phase durations into stamps 5..12
 #define OCT_SUBSTEPS(G)                                                                       \
   _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs, pob_ts + 5);
+    opbd_substep<OMW, oct_pool(KIND)>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs, pob_ts + 5);
 #else
 // At two waves per SIMD (the branch-guard build, B > 8 x SIMDs) the four-lane kernel's falling
 // issue priority keeps a SIMD's waves together (k_step_quad): HH B = 16 384 -2.2 %, TAG -3 %,
@@ -1504,7 +1500,7 @@ __global__ __launch_bounds__(64) void k_step_oct(const void *sysp, const int B, 
       else if (lvl_ == 2) __builtin_amdgcn_s_setprio(1);                                       \
       else __builtin_amdgcn_s_setprio(0);                                                      \
     }                                                                                          \
-    opbd_substep<OMW>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs);                \
+    opbd_substep<OMW, oct_pool(KIND)>(G, Sp, OT, WT, HW, isA, bd, a, cvl, cal, (it & 1) != 0, ocs);                \
   }
 #endif
     if constexpr (!GACC) {

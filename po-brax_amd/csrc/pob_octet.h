@@ -72,24 +72,24 @@ struct OGround {
   float pen;
   v3 pe;  // x + rotate(end, q)
 };
-// (POB_OCT_POOL: the wave's contacts in an LDS pool after the per-lane store -- OPOOL_N entries
-// of tau, n, dist and (next + 1) << 1 | slot -- stored by the walk's winner lanes and linked
-// per lane by the owners (pob_mesh.h mesh_wave_walk HAND 2); the position responses then follow
-// the list after the walk instead of inside its hand-over)
-#ifndef POB_OCT_POOL
-#define POB_OCT_POOL 0
+// The wave's contact pool (per kind, bit 1 << KIND of POB_OCT_POOL_KINDS): the wave's contacts
+// in LDS after the lanes' stores -- OPOOL_N entries of tau, n, dist and (next + 1) << 1 | slot --
+// stored by the walk's winner lanes and linked per lane by the owners (pob_mesh.h
+// mesh_wave_walk HAND 2), the position responses then following the list after the walk
+// instead of inside its hand-over.  HH B = 16 384 0.1075 -> 0.0950 ms; TAG B = 12 288 / 16 384
+// +0.8 / +1.7 %, GA +1.3 % (profiles/r7i/ab.txt), so HH only.
+#ifndef POB_OCT_POOL_KINDS
+#define POB_OCT_POOL_KINDS 1
 #endif
+__host__ __device__ constexpr bool oct_pool(int kind) { return kind >= 0 && ((POB_OCT_POOL_KINDS >> kind) & 1) != 0; }
 #define OPOOL_N 64
 struct OMesh {
   v3 a[ONB], b[ONB];
   uint64_t mc[ONB];
   int nct;  // wall contacts of the position pass (the first OMAXC kept in the lane's LDS store)
-#if POB_OCT_POOL
-  int head;
-  bool povf;
-#endif
+  int head;   // (pool) the lane's first contact
+  bool povf;  // (pool) the wave's contacts overflowed it (wave-uniform)
 };
-#if POB_OCT_POOL
 struct OPoolSink {
   float *pool;
   int npool;  // (wave-uniform)
@@ -121,7 +121,6 @@ struct OPoolSink {
     }
   }
 };
-#endif
 // The position pass's wall contacts (slot, tau, n, dist), kept in the lane's LDS store
 // (lane-minor: element e at CS[64 e]) so that the velocity pass applies them without evaluating
 // their faces again; a lane with more re-walks its contact faces (ms.mc) from its segments,
@@ -193,7 +192,7 @@ POB_D void omesh_seg(const float *OT, const bool isA, const OMesh &ms, const int
   seg = !(isA && s == 0);
 }
 
-template <int MW, class G>
+template <int MW, bool POOL, class G>
 POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
                               const bool isA, const OBody &b, const v3 (&pxs)[ONB], const q4 (&pqs)[ONB],
                               OGround &gc, OMesh &ms, v3 (&DX)[ONB], v3 (&DA)[ONB], float *CS) {
@@ -273,8 +272,7 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
     DX[0] = vsel3(s == 0, dx, DX[0]); DX[1] = vsel3(s == 1, dx, DX[1]);
     DA[0] = vsel3(s == 0, da, DA[0]); DA[1] = vsel3(s == 1, da, DA[1]);
   };
-#if POB_OCT_POOL
-  {
+  if constexpr (POOL) {
     float *pool = CS - (int)__lane_id() + OCS_FLOATS * 64;  // (after the lanes' stores)
     OPoolSink sink{pool, 0, -1, 0, -1, 0, 0ull, 0ull};
     mesh_wave_walk<ONB, false, 2>(g, WT, HW.fc, HW.cz, HW.hz, M,
@@ -310,7 +308,6 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
     }
     return;
   }
-#endif
   mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
                       [&](const int s, v3 &A, v3 &B, float &r, bool &seg) { omesh_seg(OT, isA, ms, s, A, B, r, seg); },
                       [&](const int s, const int bit, const float tau, const v3 n, const float dist) {
@@ -341,7 +338,7 @@ POB_D void ocontacts_position(G &g, const HCon &SC, const float *OT, const float
   }
 }
 
-template <int MW, class G>
+template <int MW, bool POOL, class G>
 POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float *WT, const HWalls<MW> &HW,
                               const bool isA, const OBody &b, const OGround &gc, const OMesh &ms, v3 (&dV)[ONB],
                               v3 (&dW)[ONB], const float *CS) {
@@ -354,9 +351,9 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
                        b.q[s], b.v[s], b.w[s], dV[s], dW[s]);
   }
   if (MW == 0 || !__any(ms.nct != 0)) return;
-#if POB_OCT_POOL
-  const bool ovf = ms.povf && ms.nct > 0;
-  {
+  bool ovf;
+  if constexpr (POOL) {
+    ovf = ms.povf && ms.nct > 0;
     const float *pool = CS - (int)__lane_id() + OCS_FLOATS * 64;
     int ci = ms.povf || ms.nct == 0 ? -1 : ms.head;
 #pragma unroll 1
@@ -377,9 +374,8 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
         ci = (meta >> 1) - 1;
       }
     }
-  }
-#else
-  const bool ovf = ms.nct > OMAXC;
+  } else {
+  ovf = ms.nct > OMAXC;
   const int nc = ovf ? 0 : ms.nct;
 #pragma unroll 1
   for (int i = 0; i < OMAXC; ++i) {
@@ -398,7 +394,7 @@ POB_D void ocontacts_velocity(G &g, const HCon &SC, const float *OT, const float
       dW[0] = vsel3(s == 0, dw, dW[0]); dW[1] = vsel3(s == 1, dw, dW[1]);
     }
   }
-#endif
+  }
   if (!__any(ovf)) return;
   uint64_t M[ONB] = {ovf ? ms.mc[0] : 0ull, ovf ? ms.mc[1] : 0ull};
   mesh_wave_walk<ONB, false>(g, WT, HW.fc, HW.cz, HW.hz, M,
@@ -475,7 +471,7 @@ POB_D void ojoint_position(G &g, csys_t &S, const float s_pos, const float *OT, 
 // trip would sit on the lone wave's dependency chain)
 // G: the range-guard policy (pob_math.h GuardBranch / GuardAcc); HW: the walls and the
 // loop's table scalars in registers.
-template <int MW, class G>
+template <int MW, bool POOL = false, class G>
 POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, const HWalls<MW> &HW, const bool isA, OBody &b,
                         const float act, v3 (&cv)[ONB], v3 (&ca)[ONB], const bool COLLIDE, float *CS,
                         unsigned long long *tacc = nullptr) {
@@ -567,7 +563,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     }
     HSUB_T(1)
     if (COLLIDE) {
-      ocontacts_position<MW>(g, SC, OT, WT, HW, isA, b, px, pq, gc, ms, DX, DA, CS);
+      ocontacts_position<MW, POOL>(g, SC, OT, WT, HW, isA, b, px, pq, gc, ms, DX, DA, CS);
       HSUB_T(4)
     }
 #pragma unroll
@@ -594,7 +590,7 @@ POB_D void opbd_substep(G &g, csys_t *Sp, const float *OT, const float *WT, cons
     v3 dV[ONB], dW[ONB];
 #pragma unroll
     for (int s = 0; s < ONB; ++s) { dV[s] = V(0.0f, 0.0f, 0.0f); dW[s] = V(0.0f, 0.0f, 0.0f); }
-    ocontacts_velocity<MW>(g, SC, OT, WT, HW, isA, b, gc, ms, dV, dW, CS);
+    ocontacts_velocity<MW, POOL>(g, SC, OT, WT, HW, isA, b, gc, ms, dV, dW, CS);
 #pragma unroll
     for (int s = 0; s < ONB; ++s) {
       b.v[s] = vadd(b.v[s], dV[s]); b.w[s] = vadd(b.w[s], dW[s]);
