@@ -617,10 +617,10 @@ def rank_devices(dev, world: int) -> list:
 
 def step_kernel(B: int, env: str = "ant_heavenhell") -> str:
     """The step kernel pob_step launches for a batch of B envs (pob_kernels.hip pob_step:
-    sixteen lanes per env up to POB_HEXA_MAX_B (per kind: HH 48, TAG 32, else 16 x the CU
+    sixteen lanes per env up to POB_HEXA_MAX_B (per kind: HH and TAG 32, else 16 x the CU
     count), eight up to POB_OCTET_MAX_B (16 384), four above)."""
     n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    hex_default = {"ant_heavenhell": 48, "ant_tag": 32}.get(env, 16) * n_cu
+    hex_default = {"ant_heavenhell": 32, "ant_tag": 32}.get(env, 16) * n_cu
     if B <= int(os.environ.get("POB_HEXA_MAX_B", str(hex_default))):
         return "k_step_hex"
     if B <= int(os.environ.get("POB_OCTET_MAX_B", "16384")):

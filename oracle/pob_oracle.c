@@ -21,6 +21,13 @@
  *   wrappers       envs/__init__.py:50-72 (create chain), envs/wrappers.py:16-24,
  *                  :245-262 (gym autoreset); brax EpisodeWrapper / AutoResetWrapper [ext]
  *   physics        brax v1 System.step / info / default_qp [ext] -- restated, DESIGN.md §3
+ *
+ * PARITY UNPINNED where no reference artefact reaches: the PBD solver (brax v1 is not vendored;
+ * no recorded PBD trajectory exists) and every wall contact -- the default spelling MV_BRAX is
+ * brax v1's capsule_mesh as recalled, its triangulation / winding / edge loop / frame choices
+ * measured against the 1-ulp noise floor but not pinned.  Pinned: threefry
+ * (public KATs), FK / reset / the shared actuator gate and kinetic step (the notebook's 21
+ * legacy frames), the Config tables, the POMDP logic line by line.
  */
 #include "pob_oracle.h"
 
@@ -798,6 +805,7 @@ static cand_t seg_tri(int t, float ha, float hb, float w0, f3 A, f3 B, int seg, 
 #define MV_POS_TRI 4
 #define MV_FORM 8
 #define MV_BRAX (MV_EPS_NORMAL | MV_POS_TRI | MV_FORM)
+/* (the default, MV_BRAX: brax's spelling as recalled -- parity-unpinned, see the file header) */
 static int g_mesh_variant = MV_BRAX;
 void orc_set_mesh_variant(int v) { g_mesh_variant = v; }
 int orc_get_mesh_variant(void) { return g_mesh_variant; }

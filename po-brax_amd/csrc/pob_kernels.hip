@@ -2823,12 +2823,14 @@ static int octet_max_batch() {
 //   HH   B = 6 144 0.0715 / 0.0998, 8 192 0.0750 / 0.1009, 12 288 0.1036 / 0.1098, 16 384 0.1178 / 0.1149
 //   TAG  B = 6 144 0.0502 / 0.0488, 8 192 0.0514 / 0.0541, 12 288 0.0751 / 0.0645
 //   GA   B = 6 144 0.0374 / 0.0356, 8 192 0.0381 / 0.0369
-// so the sixteen-lane kernel runs HH up to 3 waves per SIMD (48 x CUs: 12 288), TAG up to 2
-// (8 192), GA and the stock ant up to 1.
+// so the sixteen-lane kernel ran HH up to 3 waves per SIMD (48 x CUs: 12 288), TAG up to 2
+// (8 192), GA and the stock ant up to 1.  Round 6 (the eight-lane kernel's contact pool for HH,
+// profiles/r7k): HH B = 12 288 hex / oct 0.0924 / 0.0891, 8 192 0.0662 / 0.0803; TAG 6 144
+// 0.0476 / 0.0457, 8 192 0.0490 / 0.0500 -- so HH up to 2 waves per SIMD too (32 x CUs).
 static int hexa_max_batch(int n_cu, int kind) {
   const char *e = getenv("POB_HEXA_MAX_B");
   if (e) return atoi(e);
-  return (kind == POB_HEAVENHELL ? 48 : (kind == POB_TAG ? 32 : 16)) * n_cu;
+  return (kind == POB_HEAVENHELL || kind == POB_TAG ? 32 : 16) * n_cu;
 }
 template <typename QT, bool GACC>
 static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
