@@ -400,15 +400,29 @@ struct QPoolSink {
     }
   }
 };
+// (POB_QUAD_WALK_GACC, an A/B switch: the walk's range guards branch-free, GuardAcc -- a lane
+// that saw an operand outside the fast forms' range sends its wave to the fix-up launch, whose
+// exact branch guards give the same bits for every lane that stayed in range.  Measured HH
+// B = 65 536 0.1509 -> 0.1546 ms, TAG ±0 (profiles/r7m/ab.txt): off)
+#ifndef POB_QUAD_WALK_GACC
+#define POB_QUAD_WALK_GACC 0
+#endif
 POB_D void qwalls_walk_pool(csys_t &S, const float *LT, const float *WT, const QBody &b, uint64_t (&M)[QNB],
                             QWalls &ws, const QLds &L, bool &ovf) {
+#if POB_QUAD_WALK_GACC
+  GuardAcc g;
+#else
   GuardBranch g;
+#endif
 #if POB_QUAD_POOL_DIRECT
   QPoolSink sink{L.pool(), L.head(), 0, -1, 0, 0};
   mesh_wave_walk<QNB, false, 2>(g, WT, pob_face_table(S), S.wall_cz, S.wall_hz, M,
              [&](const int l, v3 &A, v3 &B, float &r, bool &seg) { qpose_seg(S, LT, b, l, A, B, r, seg); }, sink);
   ws.nct += sink.nct;
   ovf = ovf | (sink.npool > QPOOL_N);
+#if POB_QUAD_WALK_GACC
+  ovf = ovf | g.bad();
+#endif
   return;
 #endif
   float *pool = L.pool();
