@@ -200,9 +200,15 @@ POB_D void hcontacts_position(G &g, const HCon &SC, const float *HT, const float
 #if POB_HEX_POOL
   // (CS: the wave's pool)
   HPoolSink sink{CS, 0, -1, -1, 0, 0ull};
+#ifdef POB_EXP_TIMING_SUB
+  const unsigned long long _tw0 = __builtin_amdgcn_s_memtime();  // (slot 3: the walk alone)
+#endif
   mesh_wave_walk<1, false, 2>(g, WT, HW.fc, HW.cz, HW.hz, Ms,
                     [&](const int, v3 &A, v3 &B, float &r, bool &seg) { A = ms.a; B = ms.b; r = HT[HT_R]; seg = !torso; },
                     sink);
+#ifdef POB_EXP_TIMING_SUB
+  if (tacc) tacc[3] += __builtin_amdgcn_s_memtime() - _tw0;
+#endif
   ms.mc = sink.mc;
   ms.nct = sink.nct;
   ms.head = sink.head;

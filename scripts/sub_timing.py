@@ -2,9 +2,9 @@
 
 Needs a library built with -DPOB_EXP_TIMING -DPOB_EXP_TIMING_SUB (POB_LIB=...): stamps 5..12 of
 each wave's row hold the shader-clock durations of the step's substep phases summed over its
-ten substeps (accel + kinetic, joint projection, wall-contact position + the state update,
-wall-contact velocity, contact detection, ground-contact position, velocity projection,
-ground-contact velocity).  argv: B (<= 16 384: the sixteen-lane kernel up to 4 096, the eight-lane one above), env name."""
+ten substeps (sixteen lanes: accel + kinetic, joint projection, the position update, the face
+walk alone, contact detection with the position responses, its broadphase + face cull, velocity
+projection, velocity-level contacts).  argv: B (<= 16 384: the sixteen-lane kernel up to 4 096, the eight-lane one above), env name."""
 import ctypes as C
 import os
 import sys
@@ -25,7 +25,7 @@ for _ in range(20):
     jumpy.random_actions_(key, B, 0, act)
     s = env.step_(s, act)
 torch.cuda.synchronize()
-LPE = 16 if B <= 4096 else 8  # lanes per env: the default switch on 256 CUs (B <= 16 384)
+LPE = 16 if B <= (8192 if NAME in ("ant_heavenhell", "ant_tag") else 4096) else 8  # the default switch on 256 CUs
 W = (B * LPE + 63) // 64
 NTS = 16  # POB_TS_N of a POB_EXP_TIMING_SUB build
 buf = np.zeros((W, NTS + 4), np.uint64)
@@ -37,8 +37,8 @@ tot = t[:, NTS - 1] - t[:, 0]
 print(f"{NAME} B={B} waves={W}: wave ticks p50 {np.median(tot):.0f} max {tot.max()}")
 phys = t[:, 2] - t[:, 1]
 print(f"physics (stamp 1->2) p50 {np.median(phys):.0f}")
-names = (("accel+kinetic", "joint", "wall position+update", "wall contact vel", "contact detect",
-          "(of which broadphase + face cull)", "velocity projection", "ground contact vel") if LPE == 16 else
+names = (("accel+kinetic", "joint", "position update", "(of detect: the face walk)", "contact detect + position",
+          "(of detect: broadphase + face cull)", "velocity projection", "velocity contacts") if LPE == 16 else
          ("accel+kinetic", "joint", "position update", "contact vel (ground+wall)", "contact detect",
           "contact position (ground+wall)", "velocity projection", "-"))
 for i, n in zip(range(5, 13), names):
