@@ -148,8 +148,11 @@ class ObsGatherer:
         import torch
         import torch.distributed as dist
         self.total, self.D, self.group = int(total), int(D), group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        # (with a process group the all-gather runs at any world size, 1 included: the one-GPU
+        # box exercises RCCL and the side-stream ordering through it)
+        self.dist = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.rank = dist.get_rank(group) if self.dist else 0
         self.bounds = [shard_range(self.total, self.world, r) for r in range(self.world)]
         self.m = max(hi - lo for lo, hi in self.bounds)
         self.ragged = any(hi - lo != self.m for lo, hi in self.bounds)
@@ -177,7 +180,7 @@ class ObsGatherer:
         self.k += 1
         if not self.cuda:
             self.stage[p][:hi - lo].copy_(obs)
-            if self.world > 1:
+            if self.dist:
                 dist.all_gather_into_tensor(self.full[p], self.stage[p], group=self.group)
             else:
                 self.full[p].copy_(self.stage[p])
@@ -192,7 +195,7 @@ class ObsGatherer:
             self.stream.wait_event(staged)
             t0 = torch.cuda.Event(enable_timing=True)
             t0.record(self.stream)
-            if self.world > 1:
+            if self.dist:
                 dist.all_gather_into_tensor(self.full[p], self.stage[p], group=self.group)
             else:
                 self.full[p].copy_(self.stage[p])

@@ -1,6 +1,7 @@
-"""GPU, two ranks on one device (gloo collectives on device tensors): the sharded brax and
-gym paths with the HIP kernels equal the single-process batch (scripts/multirank_check.py;
-the 8-GPU RCCL run uses the same script with --backend nccl)."""
+"""GPU, two ranks on one device (gloo collectives on device tensors) and one rank over RCCL:
+the sharded brax and gym paths and the overlapped obs gather with the HIP kernels equal the
+single-process batch (scripts/multirank_check.py; the 8-GPU RCCL run uses the same script with
+--backend nccl)."""
 import os
 import socket
 import subprocess
@@ -29,4 +30,21 @@ def test_two_ranks_one_gpu_equal_single(name):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
     print(r.stdout[-2000:], r.stderr[-2000:])
     assert r.returncode == 0
-    assert "brax True gym True key True" in r.stdout
+    assert "brax True gym True key True gather True" in r.stdout
+
+
+@pytest.mark.parametrize("name", ["ant_heavenhell"])
+def test_rccl_world1_product_path(name):
+    """The same check over RCCL (backend nccl) with one rank: the process group, the sharded
+    brax and gym chains' collectives (the gym path's any-done all-reduce) and ObsGatherer's
+    side-stream all-gather run through RCCL on the device.  (RCCL refuses two ranks on one
+    device -- "Duplicate GPU detected", profiles/r7v -- so world 2 runs over gloo above and
+    the 8-GPU node is the first place RCCL sees more than one rank.)"""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "scripts", "multirank_check.py"), "--backend", "nccl", "--env", name]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    assert "world=1 backend=nccl: brax True gym True key True gather True" in r.stdout
