@@ -107,7 +107,7 @@ def main() -> int:
                     help="graph rollout: env groups stepped on their own streams (rollout.GraphRollout)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying the K steps from a "
-                         "hipGraph (po_brax_amd.rollout); --gather-obs and the sharded gym path are eager")
+                         "hipGraph (po_brax_amd.rollout); --gather-obs and the gloo-sharded gym path are eager")
     ap.add_argument("--obs-mask", default="none", choices=sorted(OBS_MASKS),
                     help="observation mask fused into the step kernel (create(..., obs_mask=idx), C ABI v7): "
                          "the step also stores obs[:, idx] (BASELINE config 2: '--global-batch 4096 "
@@ -215,9 +215,10 @@ def main() -> int:
         one_step(t)
     torch.cuda.synchronize()
 
-    # the gym path's K steps replay from a graph too when it has no cross-rank all-reduce
-    use_graph = not args.no_graph and not do_gather and pre and (gym is None or world == 1) and \
-        (gym is None or args.steps % 2 == 0)
+    # the gym path's K steps replay from a graph too; sharded, its per-step any-done all-reduce
+    # is captured with them over RCCL (rollout.GymGraphRollout), gloo steps eagerly
+    use_graph = not args.no_graph and not do_gather and pre and \
+        (gym is None or world == 1 or args.dist_backend == "nccl") and (gym is None or args.steps % 2 == 0)
     roll = None
     if args.policy_mlp:
         if gym is not None or args.env == "mixed" or do_gather:

@@ -284,7 +284,7 @@ class AutoresetVmapGymWrapper(VmapGymWrapper):
         from ..sharding import all_reduce_any_done
         self._step_local(action)
         sh = self._shard
-        if sh is not None and sh.world > 1:
+        if sh is not None:  # (a no-op without a process group)
             all_reduce_any_done(self._any, sh.group)
         return self._autoreset()
 

@@ -158,8 +158,12 @@ class GymGraphRollout:
     The wrapper's host-side bookkeeping (the alternating any-done words and gym-key buffers)
     is advanced by the capture itself, so ``T`` must be even: after T steps it is back where
     it started, and every replay continues from the device state the last one left.
-    ``actions`` (T, B, A) is read at replay time (refill it between replays).  One process
-    only: the sharded wrapper's per-step RCCL all-reduce stays eager."""
+    ``actions`` (T, B, A) is read at replay time (refill it between replays).  Sharded
+    (``create_gym_env(shard=...)``) under an RCCL process group, each step's 4-byte any-done
+    all-reduce is captured with the kernels (RCCL collectives are stream-ordered and
+    capturable: bit-equal to the eager steps through a one-rank communicator,
+    ``scripts/gym_capture_check.py``, profiles/r7w); a gloo group's host-side collective
+    cannot be captured, so that case is refused."""
 
     def __init__(self, gym, actions: torch.Tensor):
         from .envs.wrappers import AutoresetVmapGymWrapper, EvalGymWrapper
@@ -176,8 +180,11 @@ class GymGraphRollout:
             raise NotImplementedError(f"GymGraphRollout captures create_gym_env's AutoresetVmapGymWrapper, "
                                       f"not {type(gym).__name__}")
         sh = getattr(gym, "_shard", None)
-        if sh is not None and sh.world > 1:
-            raise NotImplementedError("a sharded gym step (RCCL any-done all-reduce) runs eagerly")
+        if sh is not None:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_backend(sh.group) != "nccl":
+                raise NotImplementedError("a sharded gym step captures its any-done all-reduce over RCCL "
+                                          "(backend nccl) only; over gloo it steps eagerly")
         if gym._state is None:
             raise ValueError("reset() the gym before capturing its steps")
         self.gym, self.actions = gym, actions

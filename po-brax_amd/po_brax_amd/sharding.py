@@ -89,11 +89,12 @@ def shard_keys(key, total: int, world: int, rank: int):
 
 def all_reduce_any_done(flag, group=None):
     """In place: this rank's any-done word (``flag[0]``, uint32 0/1, written by the step
-    kernel) becomes the MAX over all ranks.  A no-op outside torch.distributed or at
-    world size 1.  4 bytes per call; on RCCL it is stream-ordered (no host sync)."""
+    kernel) becomes the MAX over all ranks.  A no-op outside torch.distributed; with a process
+    group it runs at any world size, 1 included (the one-GPU box exercises it over RCCL).
+    4 bytes per call; on RCCL it is stream-ordered (no host sync)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return flag
     v = flag[:1].view(torch.int32) if flag.dtype == torch.uint32 else flag[:1]
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)

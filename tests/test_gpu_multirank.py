@@ -48,3 +48,17 @@ def test_rccl_world1_product_path(name):
     print(r.stdout[-2000:], r.stderr[-2000:])
     assert r.returncode == 0
     assert "world=1 backend=nccl: brax True gym True key True gather True" in r.stdout
+
+
+def test_rccl_world1_gym_graph_capture():
+    """The sharded gym step's any-done all-reduce captured into the hipGraph with the kernels
+    (rollout.GymGraphRollout over RCCL): two replays of 8 captured steps equal 16 eager steps
+    bit for bit -- obs, reward, done and the gym key (every env ends an episode on the way)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "scripts", "gym_capture_check.py"), "--backend", "nccl"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    assert "world=1 rank=0 backend=nccl: obs True reward True done True key True" in r.stdout
