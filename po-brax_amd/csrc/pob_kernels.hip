@@ -32,6 +32,9 @@
 #ifndef POB_OCT_PRIO  // the same in the eight-lane kernel's branch-guard build (two waves per SIMD)
 #define POB_OCT_PRIO 1
 #endif
+#ifndef POB_HEX_PRIO  // the same in the sixteen-lane kernel at two or more waves per SIMD:
+#define POB_HEX_PRIO 1  // HH B = 8 192 0.0669 -> 0.0630 ms, TAG 0.0490 -> 0.0461 (profiles/r7ab)
+#endif
 #include "pob_quad.h"
 #include "pob_octet.h"
 #include "pob_hexa.h"
@@ -1698,7 +1701,9 @@ static_assert(POB_HSTAGE_FLOATS >= HCS_FLOATS * 64, "the sixteen-lane staging re
 #ifndef POB_HEX_MINW  // experiment: the register budget of this many waves per SIMD
 #define POB_HEX_MINW 1
 #endif
-template <int KIND, typename QT, bool GACC>
+// PRIO: the falling issue priority over the substeps (POB_HEX_PRIO), launched from two waves
+// per SIMD on (at one wave per SIMD it only costs: HH B = 4 096 0.0563 -> 0.0574 ms, profiles/r7ac)
+template <int KIND, typename QT, bool GACC, bool PRIO = false>
 __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp, const int B, const StatePtrs in,
                                                  const float *__restrict__ act, const StatePtrs out,
                                                  const uint32_t flags, const int L) {
@@ -1840,8 +1845,16 @@ __global__ __launch_bounds__(64, POB_HEX_MINW) void k_step_hex(const void *sysp,
     hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, hcs, pob_ts + 5);
 #else
 #define HEX_SUBSTEPS(G)                                                                       \
-  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it)                                 \
-    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, hcs);
+  _Pragma("nounroll") for (int it = 0; it < 2 * iters; ++it) {                               \
+    if constexpr (PRIO) {                                                                    \
+      const int lvl_ = (it * 4) / (2 * iters);                                               \
+      if (lvl_ == 0) __builtin_amdgcn_s_setprio(3);                                          \
+      else if (lvl_ == 1) __builtin_amdgcn_s_setprio(2);                                     \
+      else if (lvl_ == 2) __builtin_amdgcn_s_setprio(1);                                     \
+      else __builtin_amdgcn_s_setprio(0);                                                    \
+    }                                                                                        \
+    hpbd_substep<hex_max_walls(KIND)>(G, S, HT, WT, HW, bd, a, cvl, cal, (it & 1) != 0, hcs); \
+  }
 #endif
     if constexpr (!GACC) {
       GuardBranch gb;
@@ -2834,8 +2847,18 @@ static int hexa_max_batch(int n_cu, int kind) {
 }
 template <typename QT, bool GACC>
 static void launch_step_hex_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
-                              const StatePtrs &po, uint32_t flags, int L) {
+                              const StatePtrs &po, uint32_t flags, int L, int n_cu) {
   const dim3 g((unsigned)((B + 3) / 4)), b(64);
+  if (POB_HEX_PRIO && (B + 3) / 4 > 4 * n_cu) {  // two or more waves per SIMD (HH and TAG run that far)
+    if (kind == POB_HEAVENHELL) {
+      hipLaunchKernelGGL((k_step_hex<POB_HEAVENHELL, QT, GACC, true>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      return;
+    }
+    if (kind == POB_TAG) {
+      hipLaunchKernelGGL((k_step_hex<POB_TAG, QT, GACC, true>), g, b, 0, st, sp, B, pi, act, po, flags, L);
+      return;
+    }
+  }
   switch (kind) {
     case POB_HEAVENHELL: hipLaunchKernelGGL((k_step_hex<POB_HEAVENHELL, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
     case POB_GATHER: hipLaunchKernelGGL((k_step_hex<POB_GATHER, QT, GACC>), g, b, 0, st, sp, B, pi, act, po, flags, L); break;
@@ -2855,8 +2878,8 @@ static void launch_step_hex(int kind, int n_cu, hipStream_t st, const void *sp, 
                             const float *act, const StatePtrs &po, uint32_t flags, int L) {
   const char *f = getenv("POB_HEX_GACC");
   const bool acc = f ? atoi(f) != 0 : (kind == POB_HEAVENHELL || kind == POB_TAG || (B + 3) / 4 <= 4 * n_cu);
-  if (acc) launch_step_hex_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L);
-  else launch_step_hex_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L);
+  if (acc) launch_step_hex_g<QT, true>(kind, st, sp, B, pi, act, po, flags, L, n_cu);
+  else launch_step_hex_g<QT, false>(kind, st, sp, B, pi, act, po, flags, L, n_cu);
 }
 template <typename QT, bool GACC>
 static void launch_step_oct_g(int kind, hipStream_t st, const void *sp, int B, const StatePtrs &pi, const float *act,
